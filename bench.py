@@ -1,0 +1,257 @@
+#!/usr/bin/env python3
+"""bench.py — MI355X quantized MUL_MAT throughput (BASELINE.json metric) on 1..8 GPUs.
+
+Workload (N=1 headline, BASELINE.json configs[1]): Q4_0 mat-vec, K=4096, N=4096 rows, M=1
+column, HBM-cold. One *step* = one pass over a batch of L=64 distinct weight matrices
+(64 x 9.44 MB = 604 MB > 256 MB Infinity Cache, so every GEMV streams from HBM), issued as a
+captured hipGraph of 64 dependent-free launches on one stream. value = algorithmic bytes of
+all GEMVs of all ranks / max-over-ranks wall time of the timed steps (GB/s).
+
+Multi-GPU (torchrun, one rank per GPU): every rank runs the same per-GPU workload on its own
+weights (weak scaling, no data-path collective — GEMV batches over independent matrices
+partition with no exchange); barriers + max-over-ranks timing use torch.distributed (RCCL).
+
+Extra fields on the single JSON line:
+  roofline      dominant kernel (the GEMV): algorithmic bytes per launch / its mean duration,
+                timed live with HIP events around each launch on the launch stream
+  cpu_baseline  the reference's own ggml-cpu (oracle/_ref, built from the reference sources)
+                on a bounded sample of the same workload (falls back to the C oracle port)
+  configs       the other BASELINE.json kernel configs (Q4_K north star, Q4_K/Q5_K/Q6_K
+                4096x11008, Q8_0 M=512), kernel-time GB/s, TFLOP/s and roofline fractions
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ggml-gfx906_amd"))
+
+import mi355x_qmm as M  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_MEASURED_GBS = 6290.0      # float4 copy measured on MI355X (same guide)
+I8_PEAK_TOPS = 5000.0          # dense int8 / fp8 MFMA (no sparsity)
+F16_PEAK_TFLOPS = 2500.0       # dense f16/bf16 MFMA
+
+
+def synthetic_weights(t: int, N: int, K: int, seed: int) -> np.ndarray:
+    """Random quant bits with realistic fp16 scales (no oracle involved)."""
+    rng = np.random.default_rng(seed)
+    nblk = K // M.BLCK[t]
+    bs = M.TSIZE[t]
+    w = rng.integers(0, 256, size=(N, nblk, bs), dtype=np.uint8)
+    d = np.float16(0.01).view(np.uint16)
+    dm = np.float16(0.002).view(np.uint16)
+    lo, hi = np.uint8(d & 0xFF), np.uint8(d >> 8)
+    if t in (M.Q4_0, M.Q8_0):
+        w[:, :, 0], w[:, :, 1] = lo, hi
+    elif t in (M.Q4_K, M.Q5_K):
+        w[:, :, 0], w[:, :, 1] = lo, hi
+        w[:, :, 2], w[:, :, 3] = np.uint8(dm & 0xFF), np.uint8(dm >> 8)
+    elif t == M.Q6_K:
+        w[:, :, 208], w[:, :, 209] = lo, hi
+    return w.reshape(N, nblk * bs)
+
+
+def alg_bytes(t: int, K: int, N: int, Mc: int) -> int:
+    return M.row_size(t, K) * N + 4 * K * Mc + 4 * N * Mc
+
+
+class GemvSet:
+    """L device copies of one weight matrix + activations/outputs for one config."""
+
+    def __init__(self, torch, t: int, K: int, N: int, Mc: int, copies: int, seed: int = 1234):
+        self.torch, self.t, self.K, self.N, self.Mc, self.copies = torch, t, K, N, Mc, copies
+        host = synthetic_weights(t, N, K, seed)
+        base = torch.from_numpy(host.reshape(-1)).cuda()
+        self.w = [base] + [base.clone() for _ in range(copies - 1)]
+        rng = np.random.default_rng(seed + 1)
+        self.x = torch.from_numpy(rng.uniform(-1, 1, size=(Mc, K)).astype(np.float32)).cuda()
+        self.y = torch.zeros((Mc, N), dtype=torch.float32, device="cuda")
+        self.B = M.tensor(M.F32, self.x.data_ptr(), [K, Mc, 1, 1], M.contiguous_nb(M.F32, [K, Mc]))
+        self.D = M.tensor(M.F32, self.y.data_ptr(), [N, Mc, 1, 1], M.contiguous_nb(M.F32, [N, Mc]))
+        self.A = [M.tensor(t, wi.data_ptr(), [K, N, 1, 1], M.contiguous_nb(t, [K, N])) for wi in self.w]
+        self.bytes = alg_bytes(t, K, N, Mc)
+        self.flops = 2.0 * K * N * Mc
+
+    def launch(self, i: int, stream=None) -> None:
+        M.mul_mat(self.A[i % self.copies], self.B, self.D, stream)
+
+    def sweep(self) -> None:
+        for i in range(self.copies):
+            self.launch(i)
+
+    def kernel_time_us(self, reps: int) -> float:
+        """mean duration of one launch, HIP events around each launch on the launch stream"""
+        torch = self.torch
+        st = torch.cuda.current_stream()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for i, (a, b) in enumerate(evs):
+            a.record(st)
+            self.launch(i)
+            b.record(st)
+        torch.cuda.synchronize()
+        ts = sorted(a.elapsed_time(b) * 1e3 for a, b in evs)
+        return float(np.mean(ts[: max(1, int(0.9 * len(ts)))]))   # drop the slowest 10 % (host jitter)
+
+
+def cpu_baseline(seconds: float) -> dict:
+    """Reference ggml-cpu (oracle/_ref) on the host cores, bounded sample of the same config."""
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_cpu_bench")
+    sample = f"Q4_0 K=4096 N=4096 M=1 mat-vec, 32 rotated weight copies (302 MB), ~{seconds:.0f} s"
+    if os.path.exists(exe):
+        env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+        out = subprocess.run([exe, "q4_0", "4096", "4096", "1", str(threads), str(seconds), "32"],
+                             capture_output=True, text=True, env=env, timeout=300)
+        if out.returncode == 0:
+            r = json.loads(out.stdout.strip().splitlines()[-1])
+            return {"value": round(r["GBps"], 3), "unit": "GB/s", "cores": threads, "kind": "reference",
+                    "sample": sample, "us_per_mul_mat": round(r["sec_per_mul_mat"] * 1e6, 2)}
+    # fallback: the C oracle restatement (scalar generic-order dots)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import qref
+    K = N = 4096
+    w = qref.quantize(qref.Q4_0, qref.fill_uniform(N * K, 1234), n_per_row=K)
+    x = qref.fill_uniform(K, 5678).reshape(1, K)
+    t0, runs = time.perf_counter(), 0
+    while time.perf_counter() - t0 < seconds:
+        qref.mul_mat_simple(qref.Q4_0, w, N, K, x, 1, threads=threads)
+        runs += 1
+    per = (time.perf_counter() - t0) / runs
+    return {"value": round(alg_bytes(M.Q4_0, K, N, 1) / per / 1e9, 3), "unit": "GB/s", "cores": threads,
+            "kind": "port", "sample": sample.replace("32 rotated weight copies (302 MB)", "1 weight copy"),
+            "us_per_mul_mat": round(per * 1e6, 2)}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--copies", type=int, default=64)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-extra", action="store_true", help="skip the secondary configs")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a hipGraph step")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    M.build()
+    if M.device_count() < 1:
+        raise SystemExit("no gfx950 device visible: the MI355X backend cannot run")
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # ---------------- headline: Q4_0 4096x4096 M=1, 64 rotated copies per step ----------------
+    g = GemvSet(torch, M.Q4_0, 4096, 4096, 1, args.copies)
+    g.sweep()
+    torch.cuda.synchronize()
+    graph = None
+    if not args.no_graph:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            g.sweep()
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            g.sweep()
+
+    def step():
+        if graph is not None:
+            graph.replay()
+        else:
+            g.sweep()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    t_max = elapsed
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+
+    kernel_us = g.kernel_time_us(256)
+    launches = args.steps * args.copies
+    total_bytes = g.bytes * launches * world
+    value = total_bytes / t_max / 1e9
+    achieved = g.bytes / (kernel_us * 1e-6) / 1e9
+
+    extra = {}
+    if not args.no_extra and rank == 0:
+        for name, t, K, N, Mc, copies in (
+            ("q4_K_4096x4096_m1", M.Q4_K, 4096, 4096, 1, 64),
+            ("q4_K_4096x11008_m1", M.Q4_K, 4096, 11008, 1, 24),
+            ("q5_K_4096x11008_m1", M.Q5_K, 4096, 11008, 1, 24),
+            ("q6_K_4096x11008_m1", M.Q6_K, 4096, 11008, 1, 24),
+            ("q8_0_4096x4096_m512", M.Q8_0, 4096, 4096, 512, 24),
+        ):
+            s2 = GemvSet(torch, t, K, N, Mc, copies)
+            s2.sweep()
+            torch.cuda.synchronize()
+            us = s2.kernel_time_us(64 if Mc == 1 else 24)
+            gbs = s2.bytes / (us * 1e-6) / 1e9
+            tf = s2.flops / (us * 1e-6) / 1e12
+            extra[name] = {"kernel_us": round(us, 3), "GB/s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+                           "TFLOP/s": round(tf, 2)}
+            del s2
+            torch.cuda.empty_cache()
+
+    cpu = cpu_baseline(args.cpu_seconds) if (rank == 0 and world == 1) else None
+
+    if rank == 0:
+        line = {
+            "metric": "quantized GEMM GB/s (Q4_0 mul_mat_vec 4096x4096, M=1, HBM-cold)",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "q4_0 x int8 (int32 block dots, fp32 scale accumulate)",
+            "data": "synthetic (random quant bits, fp16 scales 0.01; x ~ U[-1,1])",
+            "config": {"workload": "configs[1]: Q4_0 mul_mat_vec K=4096 N=4096 M=1",
+                       "gemv_per_step": args.copies, "weight_copies": args.copies,
+                       "weight_bytes_per_gpu": g.bytes * args.copies, "graph": graph is not None,
+                       "parallelism": f"independent weight sets per GPU x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel_us": round(kernel_us, 3), "alg_bytes_per_launch": g.bytes,
+                         "frac_of_measured_copy_bw": round(achieved / HBM_MEASURED_GBS, 4)},
+            "cpu_baseline": cpu,
+            "configs": extra,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

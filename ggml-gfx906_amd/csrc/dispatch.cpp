@@ -1,0 +1,264 @@
+// dispatch.cpp — host-side dispatch of GGML_OP_MUL_MAT / GGML_OP_MUL_MAT_ID onto the gfx950
+// kernels, plus the direct C API of include/ggml-mi355x.h.
+//
+// Behavioural reference: ggml_cuda_mul_mat (src/ggml-cuda/ggml-cuda.cu:2007-2090) picks the
+// mat-vec kernel for ne11 <= 8 (MMVQ_MAX_BATCH_SIZE) and the tiled matrix kernel otherwise;
+// this file keeps that split but routes to our own kernels.
+#include "dispatch.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/ggml-mi355x.h"
+#include "qcommon.h"
+
+namespace mi355x {
+
+hipError_t mmvq_launch(int type, const MmArgs &a, int nc, int rpw, hipStream_t st);
+hipError_t mmvq_id_launch(int type, const MmArgs &a, int rpw, hipStream_t st);
+size_t mmvq_lds_bytes(int K, int nc);
+hipError_t dequant_launch(int type, const void *src, float *dst, int64_t n, hipStream_t st);
+hipError_t mmq_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
+bool mmq_supported(int type, const MmArgs &a);
+
+static constexpr size_t LDS_LIMIT = 160 * 1024;
+
+int type_blck(int t) {
+    switch (t) {
+        case T_Q4_0: case T_Q8_0: return 32;
+        case T_Q4_K: case T_Q5_K: case T_Q6_K: return 256;
+        default: return 0;
+    }
+}
+
+int type_bytes(int t) {
+    switch (t) {
+        case T_Q4_0: return 18;
+        case T_Q8_0: return 34;
+        case T_Q4_K: return 144;
+        case T_Q5_K: return 176;
+        case T_Q6_K: return 210;
+        case T_F32: case T_I32: return 4;
+        default: return 0;
+    }
+}
+
+bool is_hot_quant(int t) { return type_blck(t) != 0; }
+
+// rows per wave for the mat-vec: enough workgroups to cover 256 CUs at least twice,
+// more rows per wave (fewer redundant activation quantizations) once N is large.
+static int pick_rpw(int N) {
+    if (N >= 16384) return 4;
+    if (N >= 4096) return 2;
+    return 1;
+}
+
+static bool aligned16(const void *p, int64_t s1, int64_t s2, int64_t s3) {
+    return ((uintptr_t)p % 16) == 0 && s1 % 16 == 0 && s2 % 16 == 0 && s3 % 16 == 0;
+}
+
+int check_mul_mat(const TensorView &a, const TensorView &b, const TensorView &d) {
+    if (!is_hot_quant(a.type) || b.type != T_F32 || d.type != T_F32) return GGML_MI355X_EINVAL;
+    if (a.ne[0] != b.ne[0] || a.ne[0] % type_blck(a.type) != 0) return GGML_MI355X_EINVAL;
+    if (a.ne[2] <= 0 || a.ne[3] <= 0 || b.ne[2] % a.ne[2] != 0 || b.ne[3] % a.ne[3] != 0) return GGML_MI355X_EINVAL;
+    if (d.ne[0] != a.ne[1] || d.ne[1] != b.ne[1] || d.ne[2] != b.ne[2] || d.ne[3] != b.ne[3]) return GGML_MI355X_EINVAL;
+    if ((int64_t)a.nb[0] != type_bytes(a.type) || b.nb[0] != 4 || d.nb[0] != 4) return GGML_MI355X_EINVAL;
+    if (a.ne[0] > (1 << 24) || a.ne[1] > (1LL << 31) - 1 || b.ne[1] > (1LL << 31) - 1) return GGML_MI355X_EINVAL;
+    if (mmvq_lds_bytes((int)a.ne[0], 1) > LDS_LIMIT) return GGML_MI355X_EINVAL;
+    return GGML_MI355X_OK;
+}
+
+static MmArgs base_args(const TensorView &a, const TensorView &b, const TensorView &d) {
+    MmArgs m{};
+    m.w = static_cast<const uint8_t *>(a.data);
+    m.nb01 = (int64_t)a.nb[1]; m.nb02 = (int64_t)a.nb[2]; m.nb03 = (int64_t)a.nb[3];
+    m.x = static_cast<const uint8_t *>(b.data);
+    m.nb11 = (int64_t)b.nb[1]; m.nb12 = (int64_t)b.nb[2]; m.nb13 = (int64_t)b.nb[3];
+    m.dst = static_cast<uint8_t *>(d.data);
+    m.nb1 = (int64_t)d.nb[1]; m.nb2 = (int64_t)d.nb[2]; m.nb3 = (int64_t)d.nb[3];
+    m.K = (int)a.ne[0];
+    m.N = (int)a.ne[1];
+    m.M = (int)b.ne[1];
+    m.ne12 = (int)b.ne[2];
+    m.ne13 = (int)b.ne[3];
+    m.r2 = (int)(b.ne[2] / a.ne[2]);
+    m.r3 = (int)(b.ne[3] / a.ne[3]);
+    m.x_aligned16 = aligned16(b.data, m.nb11, m.nb12, m.nb13);
+    return m;
+}
+
+// mat-vec over columns [c0, c0 + ncols) in groups of at most 8
+static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st) {
+    const int rpw = pick_rpw(m.N);
+    while (ncols > 0) {
+        int nc = std::min(ncols, 8);
+        while (nc > 1 && mmvq_lds_bytes(m.K, nc) > LDS_LIMIT) --nc;
+        MmArgs g = m;
+        g.x = m.x + (int64_t)c0 * m.nb11;
+        g.dst = m.dst + (int64_t)c0 * m.nb1;
+        g.M = nc;
+        g.x_aligned16 = m.x_aligned16;
+        const hipError_t e = mmvq_launch(type, g, nc, rpw, st);
+        if (e != hipSuccess) return e;
+        c0 += nc;
+        ncols -= nc;
+    }
+    return hipSuccess;
+}
+
+int mul_mat(const TensorView &a, const TensorView &b, const TensorView &d, hipStream_t st, Scratch &scratch) {
+    const int rc = check_mul_mat(a, b, d);
+    if (rc != GGML_MI355X_OK) return rc;
+    if (a.ne[1] == 0 || b.ne[1] == 0 || b.ne[2] == 0 || b.ne[3] == 0) return GGML_MI355X_OK;
+    MmArgs m = base_args(a, b, d);
+    hipError_t e;
+    if (m.M > 8 && mmq_supported(a.type, m)) e = mmq_launch(a.type, m, st, scratch);
+    else e = run_mmvq(a.type, m, 0, m.M, st);
+    return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
+}
+
+int check_mul_mat_id(const TensorView &as, const TensorView &b, const TensorView &ids, const TensorView &d) {
+    if (!is_hot_quant(as.type) || b.type != T_F32 || ids.type != T_I32 || d.type != T_F32) return GGML_MI355X_EINVAL;
+    if (as.ne[0] != b.ne[0] || as.ne[0] % type_blck(as.type) != 0 || as.ne[3] != 1 || b.ne[3] != 1) return GGML_MI355X_EINVAL;
+    if (ids.ne[1] != b.ne[2] || b.ne[1] <= 0 || ids.ne[0] % b.ne[1] != 0) return GGML_MI355X_EINVAL;
+    if (d.ne[0] != as.ne[1] || d.ne[1] != ids.ne[0] || d.ne[2] != ids.ne[1]) return GGML_MI355X_EINVAL;
+    if ((int64_t)as.nb[0] != type_bytes(as.type) || b.nb[0] != 4 || d.nb[0] != 4 || ids.nb[0] != 4) return GGML_MI355X_EINVAL;
+    if (mmvq_lds_bytes((int)as.ne[0], 1) > LDS_LIMIT) return GGML_MI355X_EINVAL;
+    if (ids.ne[0] * ids.ne[1] > 65535) return GGML_MI355X_EINVAL;
+    return GGML_MI355X_OK;
+}
+
+int mul_mat_id(const TensorView &as, const TensorView &b, const TensorView &ids, const TensorView &d, hipStream_t st,
+               Scratch &) {
+    const int rc = check_mul_mat_id(as, b, ids, d);
+    if (rc != GGML_MI355X_OK) return rc;
+    if (ids.ne[0] == 0 || ids.ne[1] == 0 || as.ne[1] == 0) return GGML_MI355X_OK;
+    MmArgs m{};
+    m.w = static_cast<const uint8_t *>(as.data);
+    m.nb01 = (int64_t)as.nb[1]; m.nb02 = (int64_t)as.nb[2]; m.nb03 = (int64_t)as.nb[3];
+    m.x = static_cast<const uint8_t *>(b.data);
+    m.nb11 = (int64_t)b.nb[1]; m.nb12 = (int64_t)b.nb[2]; m.nb13 = (int64_t)b.nb[3];
+    m.dst = static_cast<uint8_t *>(d.data);
+    m.nb1 = (int64_t)d.nb[1]; m.nb2 = (int64_t)d.nb[2]; m.nb3 = (int64_t)d.nb[3];
+    m.K = (int)as.ne[0];
+    m.N = (int)as.ne[1];
+    m.M = 1;
+    m.ne12 = 1; m.ne13 = 1; m.r2 = 1; m.r3 = 1;
+    m.ids = static_cast<const int32_t *>(ids.data);
+    m.ids_nb0 = (int64_t)ids.nb[0];
+    m.ids_nb1 = (int64_t)ids.nb[1];
+    m.n_used = (int)ids.ne[0];
+    m.n_tok = (int)ids.ne[1];
+    m.ne11_b = (int)b.ne[1];
+    m.n_expert = (int)as.ne[2];
+    m.x_aligned16 = aligned16(b.data, m.nb11, m.nb12, m.nb13);
+    const hipError_t e = mmvq_id_launch(as.type, m, pick_rpw(m.N), st);
+    return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
+}
+
+int dequantize(int type, const void *src, float *dst, int64_t n, hipStream_t st) {
+    if (!is_hot_quant(type) || n < 0 || n % type_blck(type) != 0) return GGML_MI355X_EINVAL;
+    if (n == 0) return GGML_MI355X_OK;
+    return dequant_launch(type, src, dst, n, st) == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
+}
+
+// ------------------------------------------------------------------------------------------
+// scratch: grow-only device buffer, one per (device, stream) user
+// ------------------------------------------------------------------------------------------
+void *Scratch::get(size_t bytes, hipStream_t st) {
+    if (bytes <= cap) return ptr;
+    if (ptr) {
+        (void)hipStreamSynchronize(st);    // previous users of the old buffer on this stream
+        (void)hipFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+    }
+    size_t want = std::max(bytes, (size_t)1 << 20);
+    want = (want + 0xFFFFF) & ~(size_t)0xFFFFF;
+    if (hipMalloc(&ptr, want) != hipSuccess) {
+        ptr = nullptr;
+        return nullptr;
+    }
+    cap = want;
+    return ptr;
+}
+
+Scratch::~Scratch() {
+    if (ptr) (void)hipFree(ptr);
+}
+
+}  // namespace mi355x
+
+// ==========================================================================================
+// direct C API (include/ggml-mi355x.h)
+// ==========================================================================================
+using namespace mi355x;
+
+static TensorView view_of(const ggml_mi355x_tensor *t) {
+    TensorView v;
+    v.type = t->type;
+    v.data = t->data;
+    for (int i = 0; i < 4; ++i) {
+        v.ne[i] = t->ne[i];
+        v.nb[i] = t->nb[i];
+    }
+    return v;
+}
+
+static Scratch &api_scratch() {
+    // one scratch per host thread for the direct API (the ggml backend owns its own per stream)
+    static thread_local Scratch s;
+    return s;
+}
+
+extern "C" {
+
+int ggml_mi355x_mul_mat(const ggml_mi355x_tensor *src0, const ggml_mi355x_tensor *src1, ggml_mi355x_tensor *dst,
+                        void *stream) {
+    if (!src0 || !src1 || !dst) return GGML_MI355X_EINVAL;
+    return mul_mat(view_of(src0), view_of(src1), view_of(dst), static_cast<hipStream_t>(stream), api_scratch());
+}
+
+int ggml_mi355x_mul_mat_id(const ggml_mi355x_tensor *as, const ggml_mi355x_tensor *b, const ggml_mi355x_tensor *ids,
+                           ggml_mi355x_tensor *dst, void *stream) {
+    if (!as || !b || !ids || !dst) return GGML_MI355X_EINVAL;
+    return mul_mat_id(view_of(as), view_of(b), view_of(ids), view_of(dst), static_cast<hipStream_t>(stream),
+                      api_scratch());
+}
+
+int ggml_mi355x_dequantize(int32_t type, const void *src, float *dst, int64_t n, void *stream) {
+    return dequantize(type, src, dst, n, static_cast<hipStream_t>(stream));
+}
+
+int ggml_mi355x_supports_mul_mat(const ggml_mi355x_tensor *src0, const ggml_mi355x_tensor *src1) {
+    if (!src0 || !src1) return 0;
+    return is_hot_quant(src0->type) && src1->type == T_F32 && src0->ne[0] % type_blck(src0->type) == 0 &&
+           mmvq_lds_bytes((int)src0->ne[0], 1) <= LDS_LIMIT;
+}
+
+int ggml_mi355x_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    int good = 0;
+    for (int i = 0; i < n; ++i) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, i) == hipSuccess && strncmp(p.gcnArchName, "gfx950", 6) == 0) ++good;
+    }
+    return good;
+}
+
+const char *ggml_mi355x_strerror(int status) {
+    switch (status) {
+        case GGML_MI355X_OK: return "ok";
+        case GGML_MI355X_EINVAL: return "unsupported type or inconsistent shapes/strides";
+        case GGML_MI355X_ENOMEM: return "device scratch allocation failed";
+        case GGML_MI355X_EHIP: return "HIP runtime error";
+        case GGML_MI355X_ENODEV: return "no gfx950 device";
+        default: return "unknown status";
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,489 @@
+// mmvq.hip — quantized mat-vec (decode, ne11 <= 8) for gfx950.
+//
+// Replaces the reference's mul_mat_vec_q / quantize_q8_1 pair (src/ggml-cuda/mmvq.cu:139-226,
+// quantize.cu:4-48) with a CDNA4-first design:
+//
+//  * one 256-thread workgroup = 4 waves; each wave owns RPW consecutive weight rows;
+//  * a lane owns a fixed 64-weight "slot" of K for every row it touches (Q4_0/Q8_0: two
+//    32-blocks; Q4_K/Q5_K: one 64-chunk of a super-block; Q6_K: a quarter of a 128-half),
+//    so the weight stream of a wave is a set of wide (dwordx4) loads from one row, issued for
+//    all RPW rows before any arithmetic, read straight to VGPRs (no LDS round trip);
+//  * src1 is quantized to int8 per 32-block (d = amax/127, round-to-nearest-even) once per
+//    workgroup, into LDS, in a slot-interleaved layout so lane s reads its 64 activations with
+//    4 conflict-free ds_read_b128; d and d*sum(q) per 32-block sit beside them;
+//  * integer block dots on v_dot4_i32_i8 (weights unpacked to signed int8 lanes), fp32 scale
+//    accumulation per block, exactly the reference's per-block arithmetic (ggml-cpu/quants.c);
+//  * cross-lane reduction by a butterfly transpose: RPW*NC partial sums per lane collapse to
+//    one value per lane in log2 steps of halving width, then the plain tail.
+//
+// Templated on <type, NC columns, RPW rows per wave, IDS = MUL_MAT_ID routing>.
+#include "qcommon.h"
+#include "qmm_args.h"
+
+namespace mi355x {
+
+constexpr int MMVQ_WAVES = 4;
+constexpr int MMVQ_THREADS = MMVQ_WAVES * WAVE;
+
+// ------------------------------------------------------------------------------------------
+// slot geometry: K-chunk (16 activations) q  <->  (slot s, part j) with q = chunk_of(s, j)
+// ------------------------------------------------------------------------------------------
+template <int T> struct SlotMap {
+    // slot s covers activations [64 s, 64 s + 64): parts are consecutive 16-chunks
+    __device__ static inline void place(int q, int &s, int &j) { s = q >> 2; j = q & 3; }
+};
+template <> struct SlotMap<T_Q6_K> {
+    // slot s = 4 sb + 2 h + p covers 256 sb + 128 h + 16 p + 32 j + [0,16), j = 0..3
+    __device__ static inline void place(int q, int &s, int &j) {
+        const int sb = q >> 4, r = q & 15, h = r >> 3, r2 = r & 7;
+        j = r2 >> 1;
+        s = 4 * sb + 2 * h + (r2 & 1);
+    }
+};
+
+// ------------------------------------------------------------------------------------------
+// activation quantization into LDS
+//   xq : int8 [NC][Kpad]   slot-interleaved: chunk (s, j) at (j * nslots + s) * 16
+//   xd : f32  [NC][Kpad/32] block scale d = amax / 127
+//   xs : f32  [NC][Kpad/32] d * sum(q)   (for the k-quant min terms)
+// ------------------------------------------------------------------------------------------
+template <int T, int NC>
+__device__ inline void quantize_x_to_lds(const MmArgs &a, const uint8_t *xcol0, int64_t col_stride,
+                                         int Kpad, int8_t *xq, float *xd, float *xs) {
+    const int nslots = Kpad / 64;
+    const int nblk = Kpad / 32;
+    const int sub = threadIdx.x & 7;            // 8 lanes per 32-block, 4 values each
+    for (int b = threadIdx.x >> 3; b < NC * nblk; b += MMVQ_THREADS / 8) {
+        const int m = b / nblk, kb = b - m * nblk;
+        const int k0 = kb * 32 + sub * 4;
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        if (k0 < a.K) {
+            const float *src = reinterpret_cast<const float *>(xcol0 + (int64_t)m * col_stride) + k0;
+            if (a.x_aligned16) {
+                const float4 t = *reinterpret_cast<const float4 *>(src);
+                v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+            } else {
+                v[0] = src[0]; v[1] = src[1]; v[2] = src[2]; v[3] = src[3];
+            }
+        }
+        float amax = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+        amax = fmaxf(amax, __shfl_xor(amax, 1));
+        amax = fmaxf(amax, __shfl_xor(amax, 2));
+        amax = fmaxf(amax, __shfl_xor(amax, 4));
+        const float d = amax / 127.f;
+        const float id = amax > 0.f ? 127.f / amax : 0.f;
+        int q[4], qs = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            q[i] = (int)rintf(v[i] * id);
+            qs += q[i];
+        }
+        const uint32_t packed = (uint32_t)(q[0] & 0xff) | ((uint32_t)(q[1] & 0xff) << 8) |
+                                ((uint32_t)(q[2] & 0xff) << 16) | ((uint32_t)(q[3] & 0xff) << 24);
+        int s, j;
+        SlotMap<T>::place(kb * 2 + (sub >> 2), s, j);
+        *reinterpret_cast<uint32_t *>(xq + (size_t)m * Kpad + (size_t)(j * nslots + s) * 16 + (sub & 3) * 4) = packed;
+        qs += __shfl_xor(qs, 1);
+        qs += __shfl_xor(qs, 2);
+        qs += __shfl_xor(qs, 4);
+        if (sub == 0) {
+            xd[m * nblk + kb] = d;
+            xs[m * nblk + kb] = d * (float)qs;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// per-type weight fragment: load (raw bytes of one slot of one row) and dot with a column
+// ------------------------------------------------------------------------------------------
+template <int T> struct Frag;
+
+// Q4_0: slot = blocks 2s, 2s+1 (36 contiguous bytes)
+template <> struct Frag<T_Q4_0> {
+    uint32_t D[9];
+    __device__ inline void load(const uint8_t *row, int s, int nblk) {
+        const uint8_t *p = row + (size_t)s * 36;
+        ld16(p, D);
+        if (2 * s + 1 < nblk) {
+            ld16(p + 16, D + 4);
+            D[8] = ld4(p + 32);
+        } else {                     // ragged tail: K % 64 == 32, second block absent
+            D[4] = ld2(p + 16);
+            D[5] = D[6] = D[7] = D[8] = 0;
+        }
+    }
+    __device__ inline void zero() { for (int i = 0; i < 9; ++i) D[i] = 0; }
+    // X: 16 dwords of int8 activations (parts 0..3), xd: d of blocks 2s, 2s+1
+    __device__ inline float dot(const uint32_t X[16], const float xd[2], const float *) const {
+        const float d0 = h2f((uint16_t)(D[0] & 0xffff));
+        const float d1 = h2f((uint16_t)(D[4] >> 16));
+        int s0 = 0, s1 = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t q0 = align2(D[i + 1], D[i]);      // qs of block 0 at byte 2
+            s0 = dot4(sub8_bytes(q0 & 0x0f0f0f0fu), X[i], s0);
+            s0 = dot4(sub8_bytes((q0 >> 4) & 0x0f0f0f0fu), X[4 + i], s0);
+            const uint32_t q1 = D[5 + i];                   // qs of block 1 at byte 20
+            s1 = dot4(sub8_bytes(q1 & 0x0f0f0f0fu), X[8 + i], s1);
+            s1 = dot4(sub8_bytes((q1 >> 4) & 0x0f0f0f0fu), X[12 + i], s1);
+        }
+        return (d0 * xd[0]) * (float)s0 + (d1 * xd[1]) * (float)s1;
+    }
+};
+
+// Q8_0: slot = blocks 2s, 2s+1 (68 contiguous bytes)
+template <> struct Frag<T_Q8_0> {
+    uint32_t D[17];
+    __device__ inline void load(const uint8_t *row, int s, int nblk) {
+        const uint8_t *p = row + (size_t)s * 68;
+        ld16(p, D);
+        ld16(p + 16, D + 4);
+        if (2 * s + 1 < nblk) {
+            ld16(p + 32, D + 8);
+            ld16(p + 48, D + 12);
+            D[16] = ld4(p + 64);
+        } else {
+            D[8] = ld2(p + 32);
+            for (int i = 9; i < 17; ++i) D[i] = 0;
+        }
+    }
+    __device__ inline void zero() { for (int i = 0; i < 17; ++i) D[i] = 0; }
+    __device__ inline float dot(const uint32_t X[16], const float xd[2], const float *) const {
+        const float d0 = h2f((uint16_t)(D[0] & 0xffff));
+        const float d1 = h2f((uint16_t)(D[8] >> 16));
+        int s0 = 0, s1 = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            s0 = dot4(align2(D[i + 1], D[i]), X[i], s0);
+            s1 = dot4(D[9 + i], X[8 + i], s1);
+        }
+        return (d0 * xd[0]) * (float)s0 + (d1 * xd[1]) * (float)s1;
+    }
+};
+
+// Q4_K: slot = (super-block s/4, 64-chunk c = s%4): header 16 B + qs[32c .. 32c+32)
+template <> struct Frag<T_Q4_K> {
+    uint32_t H[4], Q[8];
+    int c;
+    __device__ inline void load(const uint8_t *row, int s, int) {
+        const uint8_t *p = row + (size_t)(s >> 2) * 144;
+        c = s & 3;
+        ld16(p, H);
+        ld16(p + 16 + 32 * c, Q);
+        ld16(p + 32 + 32 * c, Q + 4);
+    }
+    __device__ inline void zero() { for (int i = 0; i < 4; ++i) H[i] = 0; for (int i = 0; i < 8; ++i) Q[i] = 0; c = 0; }
+    __device__ inline float dot(const uint32_t X[16], const float xd[2], const float xs[2]) const {
+        const float d = h2f((uint16_t)(H[0] & 0xffff)), dmin = h2f((uint16_t)(H[0] >> 16));
+        const uint32_t S[3] = {H[1], H[2], H[3]};
+        uint32_t sc0, sc1, m0, m1;
+        k4_scale_min_pair(S, c, sc0, sc1, m0, m1);
+        int s0 = 0, s1 = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            s0 = dot4(Q[i] & 0x0f0f0f0fu, X[i], s0);
+            s1 = dot4((Q[i] >> 4) & 0x0f0f0f0fu, X[8 + i], s1);
+        }
+        return d * ((float)sc0 * xd[0] * (float)s0 + (float)sc1 * xd[1] * (float)s1) -
+               dmin * ((float)m0 * xs[0] + (float)m1 * xs[1]);
+    }
+};
+
+// Q5_K: as Q4_K plus the 32-byte qh (bit 2c / 2c+1 of qh[l] is the 5th bit)
+template <> struct Frag<T_Q5_K> {
+    uint32_t H[4], QH[8], Q[8];
+    int c;
+    __device__ inline void load(const uint8_t *row, int s, int) {
+        const uint8_t *p = row + (size_t)(s >> 2) * 176;
+        c = s & 3;
+        ld16(p, H);
+        ld16(p + 16, QH);
+        ld16(p + 32, QH + 4);
+        ld16(p + 48 + 32 * c, Q);
+        ld16(p + 64 + 32 * c, Q + 4);
+    }
+    __device__ inline void zero() {
+        for (int i = 0; i < 4; ++i) H[i] = 0;
+        for (int i = 0; i < 8; ++i) QH[i] = Q[i] = 0;
+        c = 0;
+    }
+    __device__ inline float dot(const uint32_t X[16], const float xd[2], const float xs[2]) const {
+        const float d = h2f((uint16_t)(H[0] & 0xffff)), dmin = h2f((uint16_t)(H[0] >> 16));
+        const uint32_t S[3] = {H[1], H[2], H[3]};
+        uint32_t sc0, sc1, m0, m1;
+        k4_scale_min_pair(S, c, sc0, sc1, m0, m1);
+        int s0 = 0, s1 = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t lo = (Q[i] & 0x0f0f0f0fu) | (((QH[i] >> (2 * c)) & 0x01010101u) << 4);
+            const uint32_t hi = ((Q[i] >> 4) & 0x0f0f0f0fu) | (((QH[i] >> (2 * c + 1)) & 0x01010101u) << 4);
+            s0 = dot4(lo, X[i], s0);
+            s1 = dot4(hi, X[8 + i], s1);
+        }
+        return d * ((float)sc0 * xd[0] * (float)s0 + (float)sc1 * xd[1] * (float)s1) -
+               dmin * ((float)m0 * xs[0] + (float)m1 * xs[1]);
+    }
+};
+
+// Q6_K: slot = (super-block sb = s/4, half h = (s/2)%2, part p = s%2); lane handles
+// positions 128h + 16p + 32k + [0,16) for k = 0..3, i.e. ql[64h+16p..], ql[64h+32+16p..],
+// qh[32h+16p..] and scales 8h + p + 2k.
+template <> struct Frag<T_Q6_K> {
+    uint32_t L0[4], L1[4], QH[4], SC[2];
+    uint16_t dh;
+    int p;
+    __device__ inline void load(const uint8_t *row, int s, int) {
+        const uint8_t *b = row + (size_t)(s >> 2) * 210;
+        const int h = (s >> 1) & 1;
+        p = s & 1;
+        ld16(b + 64 * h + 16 * p, L0);
+        ld16(b + 64 * h + 32 + 16 * p, L1);
+        ld16(b + 128 + 32 * h + 16 * p, QH);
+        ld8(b + 192 + 8 * h, SC);
+        dh = ld2(b + 208);
+    }
+    __device__ inline void zero() {
+        for (int i = 0; i < 4; ++i) L0[i] = L1[i] = QH[i] = 0;
+        SC[0] = SC[1] = 0;
+        dh = 0;
+        p = 0;
+    }
+    // xd: d of the four 32-blocks 4h + k
+    __device__ inline float dot(const uint32_t X[16], const float xd[4], const float *) const {
+        int s[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const uint32_t w0 = (L0[t] & 0x0f0f0f0fu) | ((QH[t] & 0x03030303u) << 4);
+            const uint32_t w1 = (L1[t] & 0x0f0f0f0fu) | ((QH[t] & 0x0c0c0c0cu) << 2);
+            const uint32_t w2 = ((L0[t] >> 4) & 0x0f0f0f0fu) | (QH[t] & 0x30303030u);
+            const uint32_t w3 = ((L1[t] >> 4) & 0x0f0f0f0fu) | ((QH[t] & 0xc0c0c0c0u) >> 2);
+            s[0] = dot4(sub32_bytes(w0), X[t], s[0]);
+            s[1] = dot4(sub32_bytes(w1), X[4 + t], s[1]);
+            s[2] = dot4(sub32_bytes(w2), X[8 + t], s[2]);
+            s[3] = dot4(sub32_bytes(w3), X[12 + t], s[3]);
+        }
+        // scales sc[8h + p + 2k]: byte (p + 2k) of the 8 loaded scale bytes
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int byte = p + 2 * k;
+            const int8_t sc = (int8_t)((SC[byte >> 2] >> (8 * (byte & 3))) & 0xff);
+            acc += (float)sc * xd[k] * (float)s[k];
+        }
+        return h2f(dh) * acc;
+    }
+};
+
+template <int T> struct XdCount { static constexpr int n = 2; };
+template <> struct XdCount<T_Q6_K> { static constexpr int n = 4; };
+
+// ------------------------------------------------------------------------------------------
+// butterfly-transpose wave reduction: V (power of two, <= 64) partial sums per lane.
+// On return lane L holds the full sum of value index (L >> (6 - log2 V)), replicated over the
+// 64/V lanes that share those high bits.
+// ------------------------------------------------------------------------------------------
+template <int x> struct Log2 { static constexpr int v = 1 + Log2<x / 2>::v; };
+template <> struct Log2<1> { static constexpr int v = 0; };
+constexpr int pow2ceil(int x) { return x <= 1 ? 1 : 2 * pow2ceil((x + 1) / 2); }
+
+template <int V>
+__device__ inline float wave_reduce_transpose(float (&v)[V]) {
+    constexpr int LV = Log2<V>::v;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int step = 0; step < LV; ++step) {
+        const int half = V >> (step + 1);
+        const int dist = 32 >> step;
+        const bool upper = (lane & dist) != 0;
+#pragma unroll
+        for (int i = 0; i < half; ++i) {
+            const float send = upper ? v[i] : v[i + half];
+            const float keep = upper ? v[i + half] : v[i];
+            v[i] = keep + __shfl_xor(send, dist);
+        }
+    }
+    float r = v[0];
+#pragma unroll
+    for (int dist = 32 >> LV; dist >= 1; dist >>= 1) r += __shfl_xor(r, dist);
+    return r;
+}
+
+// ------------------------------------------------------------------------------------------
+// the kernel
+// ------------------------------------------------------------------------------------------
+template <int T, int NC, int RPW, bool IDS>
+__global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    constexpr int NX = XdCount<T>::n;
+    constexpr int V = pow2ceil(RPW * NC);
+
+    const int blck = QT<T>::blck;
+    const int Kpad = (a.K + 63) & ~63;
+    const int nslots = Kpad / 64;
+    const int nblk = a.K / blck;                  // quant blocks per row
+    const int nxblk = Kpad / 32;
+
+    int8_t *xq = reinterpret_cast<int8_t *>(smem);
+    float *xd = reinterpret_cast<float *>(smem + (size_t)NC * Kpad);
+    float *xs = xd + NC * nxblk;
+
+    // ---- which matrix / columns this workgroup serves
+    const uint8_t *wmat;
+    const uint8_t *xcol0;
+    uint8_t *dcol0;
+    int64_t xstride, dstride;
+    if constexpr (IDS) {
+        // one (expert slot e, token t) pair per blockIdx.y, NC == 1
+        const int e = blockIdx.y % a.n_used, t = blockIdx.y / a.n_used;
+        const int ex = *reinterpret_cast<const int32_t *>(reinterpret_cast<const uint8_t *>(a.ids) + e * a.ids_nb0 + t * a.ids_nb1);
+        if (ex < 0 || ex >= a.n_expert) return;   // host validates; never index out of bounds
+        wmat = a.w + (int64_t)ex * a.nb02;
+        xcol0 = a.x + (int64_t)(e % a.ne11_b) * a.nb11 + (int64_t)t * a.nb12;
+        dcol0 = a.dst + (int64_t)e * a.nb1 + (int64_t)t * a.nb2;
+        xstride = a.nb11;
+        dstride = a.nb1;
+    } else {
+        const int i12 = blockIdx.y % a.ne12, i13 = blockIdx.y / a.ne12;
+        wmat = a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03;
+        xcol0 = a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13 + (int64_t)blockIdx.z * NC * a.nb11;
+        dcol0 = a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3 + (int64_t)blockIdx.z * NC * a.nb1;
+        xstride = a.nb11;
+        dstride = a.nb1;
+    }
+
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int row0 = (blockIdx.x * MMVQ_WAVES + wave) * RPW;
+
+    // ---- issue the first slot's weight loads for all RPW rows before touching LDS
+    Frag<T> f[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        if (row0 + r < a.N && lane < nslots) f[r].load(wmat + (int64_t)(row0 + r) * a.nb01, lane, nblk);
+        else f[r].zero();
+    }
+
+    quantize_x_to_lds<T, NC>(a, xcol0, xstride, Kpad, xq, xd, xs);
+    __syncthreads();
+
+    float acc[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc[i] = 0.f;
+
+    for (int s = lane; s < nslots; s += WAVE) {
+        if (s != lane) {
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                if (row0 + r < a.N) f[r].load(wmat + (int64_t)(row0 + r) * a.nb01, s, nblk);
+                else f[r].zero();
+            }
+        }
+        // x block indices of this slot
+        int xb0;
+        if constexpr (T == T_Q6_K) xb0 = 8 * (s >> 2) + 4 * ((s >> 1) & 1);
+        else xb0 = 2 * s;
+#pragma unroll
+        for (int m = 0; m < NC; ++m) {
+            uint32_t X[16];
+            const int8_t *xm = xq + (size_t)m * Kpad;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint4 t4 = *reinterpret_cast<const uint4 *>(xm + (size_t)(j * nslots + s) * 16);
+                X[4 * j + 0] = t4.x; X[4 * j + 1] = t4.y; X[4 * j + 2] = t4.z; X[4 * j + 3] = t4.w;
+            }
+            float dx[NX], sx[NX];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                dx[i] = xd[m * nxblk + xb0 + i];
+                sx[i] = xs[m * nxblk + xb0 + i];
+            }
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) acc[r * NC + m] += f[r].dot(X, dx, sx);
+        }
+    }
+
+    const float sum = wave_reduce_transpose<V>(acc);
+    constexpr int SHIFT = 6 - Log2<V>::v;
+    const int idx = lane >> SHIFT;
+    if ((lane & ((1 << SHIFT) - 1)) == 0 && idx < RPW * NC) {
+        const int r = idx / NC, m = idx % NC;
+        if (row0 + r < a.N) reinterpret_cast<float *>(dcol0 + (int64_t)m * dstride)[row0 + r] = sum;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// host-side launch helpers (called from dispatch.cpp)
+// ------------------------------------------------------------------------------------------
+size_t mmvq_lds_bytes(int K, int nc) {
+    const int Kpad = (K + 63) & ~63;
+    return (size_t)nc * Kpad + 2 * sizeof(float) * (size_t)nc * (Kpad / 32);
+}
+
+template <int T, int NC, int RPW, bool IDS>
+static hipError_t launch_one(const MmArgs &a, int grid_y, int grid_z, hipStream_t st) {
+    const size_t lds = mmvq_lds_bytes(a.K, NC);
+    auto kern = mmvq_kernel<T, NC, RPW, IDS>;
+    static bool attr_set = false;   // per-instantiation
+    if (!attr_set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
+    const int rows_per_wg = MMVQ_WAVES * RPW;
+    dim3 grid((a.N + rows_per_wg - 1) / rows_per_wg, grid_y, grid_z);
+    hipLaunchKernelGGL(kern, grid, dim3(MMVQ_THREADS), lds, st, a);
+    return hipGetLastError();
+}
+
+template <int T, int RPW>
+static hipError_t launch_nc(const MmArgs &a, int nc, int grid_y, int grid_z, hipStream_t st) {
+    switch (nc) {
+        case 1: return launch_one<T, 1, RPW, false>(a, grid_y, grid_z, st);
+        case 2: return launch_one<T, 2, RPW, false>(a, grid_y, grid_z, st);
+        case 3: return launch_one<T, 3, RPW, false>(a, grid_y, grid_z, st);
+        case 4: return launch_one<T, 4, RPW, false>(a, grid_y, grid_z, st);
+        case 5: return launch_one<T, 5, RPW, false>(a, grid_y, grid_z, st);
+        case 6: return launch_one<T, 6, RPW, false>(a, grid_y, grid_z, st);
+        case 7: return launch_one<T, 7, RPW, false>(a, grid_y, grid_z, st);
+        case 8: return launch_one<T, 8, RPW, false>(a, grid_y, grid_z, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <int T>
+static hipError_t launch_type(const MmArgs &a, int nc, int grid_y, int grid_z, int rpw, hipStream_t st) {
+    switch (rpw) {
+        case 1: return launch_nc<T, 1>(a, nc, grid_y, grid_z, st);
+        case 2: return launch_nc<T, 2>(a, nc, grid_y, grid_z, st);
+        default: return launch_nc<T, 4>(a, nc, grid_y, grid_z, st);
+    }
+}
+
+// plain MUL_MAT, a.M <= 8 columns per launch group; columns split into groups of nc
+hipError_t mmvq_launch(int type, const MmArgs &a, int nc, int rpw, hipStream_t st) {
+    const int grid_y = a.ne12 * a.ne13;
+    const int grid_z = a.M / nc;
+    switch (type) {
+        case T_Q4_0: return launch_type<T_Q4_0>(a, nc, grid_y, grid_z, rpw, st);
+        case T_Q8_0: return launch_type<T_Q8_0>(a, nc, grid_y, grid_z, rpw, st);
+        case T_Q4_K: return launch_type<T_Q4_K>(a, nc, grid_y, grid_z, rpw, st);
+        case T_Q5_K: return launch_type<T_Q5_K>(a, nc, grid_y, grid_z, rpw, st);
+        case T_Q6_K: return launch_type<T_Q6_K>(a, nc, grid_y, grid_z, rpw, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// MUL_MAT_ID: one (expert slot, token) GEMV per grid.y
+hipError_t mmvq_id_launch(int type, const MmArgs &a, int rpw, hipStream_t st) {
+    const int grid_y = a.n_used * a.n_tok;
+    (void)rpw;
+    switch (type) {
+        case T_Q4_0: return launch_one<T_Q4_0, 1, 2, true>(a, grid_y, 1, st);
+        case T_Q8_0: return launch_one<T_Q8_0, 1, 2, true>(a, grid_y, 1, st);
+        case T_Q4_K: return launch_one<T_Q4_K, 1, 2, true>(a, grid_y, 1, st);
+        case T_Q5_K: return launch_one<T_Q5_K, 1, 2, true>(a, grid_y, 1, st);
+        case T_Q6_K: return launch_one<T_Q6_K, 1, 2, true>(a, grid_y, 1, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace mi355x

@@ -1,0 +1,78 @@
+// qcommon.h — shared device-side definitions for the MI355X quantized MUL_MAT path.
+//
+// Block layouts are the ggml on-disk/in-memory formats (reference src/ggml-common.h:170-344);
+// the kernels read them in place (no repacking), so a ggml tensor uploaded by set_tensor is
+// consumed byte-for-byte.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mi355x {
+
+// ggml type ids (reference include/ggml.h:372-412)
+enum : int {
+    T_F32 = 0, T_F16 = 1, T_Q4_0 = 2, T_Q8_0 = 8, T_Q4_K = 12, T_Q5_K = 13, T_Q6_K = 14, T_I32 = 26,
+};
+
+constexpr int WAVE = 64;
+
+template <int T> struct QT;
+template <> struct QT<T_Q4_0> { static constexpr int blck = 32,  bytes = 18;  };
+template <> struct QT<T_Q8_0> { static constexpr int blck = 32,  bytes = 34;  };
+template <> struct QT<T_Q4_K> { static constexpr int blck = 256, bytes = 144; };
+template <> struct QT<T_Q5_K> { static constexpr int blck = 256, bytes = 176; };
+template <> struct QT<T_Q6_K> { static constexpr int blck = 256, bytes = 210; };
+
+// 16-byte / 8-byte / 4-byte loads that only assume 2-byte alignment. gfx950 runs with
+// unaligned global access enabled (HSA default), so these still lower to one
+// global_load_dwordx4/x2/dword; the hot configurations are 4- or 16-byte aligned anyway.
+struct __attribute__((packed, aligned(2))) u32x4_a2 { uint32_t v[4]; };
+struct __attribute__((packed, aligned(2))) u32x2_a2 { uint32_t v[2]; };
+struct __attribute__((packed, aligned(2))) u32x1_a2 { uint32_t v; };
+
+__device__ __forceinline__ void ld16(const uint8_t *p, uint32_t *o) {
+    const u32x4_a2 t = *reinterpret_cast<const u32x4_a2 *>(p);
+    o[0] = t.v[0]; o[1] = t.v[1]; o[2] = t.v[2]; o[3] = t.v[3];
+}
+__device__ __forceinline__ void ld8(const uint8_t *p, uint32_t *o) {
+    const u32x2_a2 t = *reinterpret_cast<const u32x2_a2 *>(p);
+    o[0] = t.v[0]; o[1] = t.v[1];
+}
+__device__ __forceinline__ uint32_t ld4(const uint8_t *p) { return reinterpret_cast<const u32x1_a2 *>(p)->v; }
+__device__ __forceinline__ uint16_t ld2(const uint8_t *p) { return *reinterpret_cast<const uint16_t *>(p); }
+
+__device__ __forceinline__ float h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+
+// 4-way int8 dot with int32 accumulate (v_dot4_i32_i8)
+__device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int c) {
+    return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
+}
+
+// bytewise (b - 8) for b in [0,15]  -> int8 in [-8,7]    (no inter-byte carries)
+__device__ __forceinline__ uint32_t sub8_bytes(uint32_t v) { return (v + 0x78787878u) ^ 0x80808080u; }
+// bytewise (b - 32) for b in [0,63] -> int8 in [-32,31]
+__device__ __forceinline__ uint32_t sub32_bytes(uint32_t v) { return (v + 0x60606060u) ^ 0x80808080u; }
+
+// funnel: bytes [off, off+4) of the 8-byte little-endian pair (lo, hi)
+__device__ __forceinline__ uint32_t align2(uint32_t hi, uint32_t lo) { return __builtin_amdgcn_alignbyte(hi, lo, 2); }
+
+// Q4_K / Q5_K 6-bit (scale, min) for sub-blocks 2c and 2c+1 of a super-block whose 12
+// scale bytes are S[0..2] (restates get_scale_min_k4, reference src/ggml-quants.c:703-710,
+// in the 32-bit form of src/ggml-cpu/quants.c:580-585, branch-free for per-lane c).
+__device__ __forceinline__ void k4_scale_min_pair(const uint32_t S[3], int c, uint32_t &sc0, uint32_t &sc1,
+                                                  uint32_t &m0, uint32_t &m1) {
+    const uint32_t sc_lo = S[0] & 0x3f3f3f3fu;                                         // scales j=0..3
+    const uint32_t sc_hi = (S[2] & 0x0f0f0f0fu) | (((S[0] >> 6) & 0x03030303u) << 4);   // scales j=4..7
+    const uint32_t mn_lo = S[1] & 0x3f3f3f3fu;                                         // mins   j=0..3
+    const uint32_t mn_hi = ((S[2] >> 4) & 0x0f0f0f0fu) | (((S[1] >> 6) & 0x03030303u) << 4);
+    const uint32_t sw = c < 2 ? sc_lo : sc_hi;
+    const uint32_t mw = c < 2 ? mn_lo : mn_hi;
+    const int sh = (c & 1) * 16;
+    sc0 = (sw >> sh) & 0xff;
+    sc1 = (sw >> (sh + 8)) & 0xff;
+    m0  = (mw >> sh) & 0xff;
+    m1  = (mw >> (sh + 8)) & 0xff;
+}
+
+}  // namespace mi355x

@@ -1,0 +1,34 @@
+// qmm_args.h — launch descriptors shared by the host dispatch and the kernels.
+//
+// A descriptor carries ggml tensor geometry verbatim (ne / nb in elements and bytes), so the
+// kernels honour every layout test-backend-ops produces: broadcast over dims 2/3 (r2, r3),
+// permuted src0/src1 (arbitrary nb01..nb03, nb11..nb13) and views (reference
+// src/ggml-cpu/ggml-cpu.c:1133-1191 defines the semantics).
+#pragma once
+#include <stdint.h>
+
+namespace mi355x {
+
+struct MmArgs {
+    const uint8_t *w;      // src0, quantized rows (nb00 == block bytes)
+    int64_t nb01, nb02, nb03;
+    const uint8_t *x;      // src1, f32 rows (nb10 == 4)
+    int64_t nb11, nb12, nb13;
+    uint8_t *dst;          // dst, f32 rows (nb0 == 4)
+    int64_t nb1, nb2, nb3;
+    int K;                 // ne00 == ne10
+    int N;                 // ne01: weight rows = dst ne0
+    int M;                 // ne11: src1 columns handled by this launch
+    int ne12, ne13;        // batch dims of src1 / dst
+    int r2, r3;            // ne12/ne02, ne13/ne03
+    // MUL_MAT_ID (ids != nullptr): dst[e, t] = as[ids[e,t]] @ b[:, e % ne11_b, t]
+    const int32_t *ids;
+    int64_t ids_nb0, ids_nb1;
+    int n_used;            // ids->ne[0]
+    int n_tok;             // ids->ne[1]
+    int ne11_b;            // b->ne[1]
+    int n_expert;          // as->ne[2]
+    int x_aligned16;       // src1 rows / strides are 16-byte aligned
+};
+
+}  // namespace mi355x

@@ -1,0 +1,35 @@
+#!/bin/bash
+# scripts/gpu_session.sh — one guarded GPU session on the box (used via gpurun).
+# Each step runs under its own time limit; a crash-class exit (abort, segfault, timeout,
+# kill) ends the session so nothing else touches a possibly faulted GPU. Assertion failures
+# (exit 1) do not stop the later measurement steps.
+#   scripts/gpu_session.sh <step> [<step> ...]   steps: info tests smoke tbo bench prof
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+run() {  # run <name> <seconds> <cmd...>
+    local name=$1 secs=$2; shift 2
+    echo "=== $name ($(date +%T))"
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "=== $name rc=$rc"
+    tail -n 5 "$OUT/$name.log"
+    case $rc in 124|134|137|139) echo "crash-class exit $rc: stopping session"; exit $rc;; esac
+    return 0
+}
+for step in "$@"; do
+    case $step in
+        info)  run info 60 bash -c 'lscpu | head -20; nproc; rocm-smi --showproductname; python -c "import torch;print(torch.cuda.get_device_name(0))"' ;;
+        build) run build 600 python -c "import __graft_entry__ as g; g.build()" ;;
+        tests) run tests 900 python -m pytest tests -m gpu -x -q ;;
+        testsall) run testsall 900 python -m pytest tests -m gpu -q ;;
+        smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        tbo)   run tbo 900 env GGML_BACKEND_PATH=$PWD/ggml-gfx906_amd/libggml-hip-mi355x.so ./oracle/_ref/test-backend-ops test -o MUL_MAT -b MI355X0 ;;
+        tboid) run tboid 900 env GGML_BACKEND_PATH=$PWD/ggml-gfx906_amd/libggml-hip-mi355x.so ./oracle/_ref/test-backend-ops test -o MUL_MAT_ID -b MI355X0 ;;
+        bench) run bench 600 python bench.py ;;
+        prof)  run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python bench.py --no-extra --cpu-seconds 1 ;;
+        *) echo "unknown step $step" ;;
+    esac
+done

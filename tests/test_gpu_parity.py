@@ -1,0 +1,139 @@
+"""GPU parity: the MI355X kernels (through the C ABI of libggml-hip-mi355x.so) vs the oracle.
+
+Every case replays a golden record (tests/golden/manifest.json, produced by the reference's
+own ggml-cpu) on byte-identical inputs and checks, like test-backend-ops does
+(tests/test-backend-ops.cpp:1173-1213 of the reference):
+  * NMSE <= 5e-4 against the reference CPU output (the MUL_MAT / MUL_MAT_ID bar, :3106-3108),
+  * and against the CPU oracle recomputed here on the same bytes,
+  * no NaN/Inf, and 1024-float sentinels on both sides of dst left untouched.
+Dequantization must be bit-exact with the reference's dequantize_row_*.
+"""
+import numpy as np
+import pytest
+
+import golden_cases as G
+import qref
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+SENT = 1024
+SENT_VAL = np.float32(-8675309.0)
+
+
+@pytest.fixture(scope="module")
+def mm():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import mi355x_qmm as M
+    M.build()
+    assert M.device_count() >= 1, "no gfx950 device visible"
+    return M
+
+
+def dev_bytes(buf: np.ndarray):
+    t = torch.from_numpy(np.ascontiguousarray(buf).view(np.uint8).copy()).cuda()
+    return t
+
+
+def guarded_out(nel: int):
+    host = np.full(nel + 2 * SENT, SENT_VAL, np.float32)
+    return torch.from_numpy(host).cuda()
+
+
+def check_guard(out_dev, nel: int) -> np.ndarray:
+    host = out_dev.cpu().numpy()
+    assert np.all(host[:SENT] == SENT_VAL), "write before dst"
+    assert np.all(host[SENT + nel:] == SENT_VAL), "write after dst"
+    return host[SENT:SENT + nel]
+
+
+def run_mul_mat(M, a: G.Operand, b: G.Operand, out_ne):
+    da, db = dev_bytes(a.buf), dev_bytes(b.buf)
+    nel = int(np.prod(out_ne))
+    dout = guarded_out(nel)
+    A = M.tensor(a.type, da.data_ptr(), a.ne, a.nb)
+    B = M.tensor(qref.F32, db.data_ptr(), b.ne, b.nb)
+    D = M.tensor(qref.F32, dout.data_ptr() + 4 * SENT, out_ne, qref.contiguous_nb(qref.F32, out_ne))
+    M.mul_mat(A, B, D)
+    torch.cuda.synchronize()
+    return check_guard(dout, nel)
+
+
+MM = [r for r in G.manifest() if r["kind"] == "mul_mat"]
+MMID = [r for r in G.manifest() if r["kind"] == "mul_mat_id"]
+
+
+@pytest.mark.parametrize("r", MM, ids=lambda r: r["name"])
+def test_mul_mat_vs_reference(mm, r):
+    a, b, out_ne = G.mul_mat_operands(r)
+    got = run_mul_mat(mm, a, b, out_ne)
+    want = G.load_bin(r["name"] + ".out.f32", np.float32)
+    assert np.all(np.isfinite(got))
+    e_ref = qref.nmse(got[: want.size], want)
+    assert e_ref <= 5e-4, f"nmse vs reference CPU {e_ref:.3e}"
+    if r["m"] * r["n"] * r["k"] <= 4096 * 4096 * 8:
+        e_orc = qref.nmse(got, G.oracle_mul_mat(a, b, out_ne))
+        assert e_orc <= 5e-4, f"nmse vs oracle {e_orc:.3e}"
+
+
+@pytest.mark.parametrize("r", MMID, ids=lambda r: r["name"])
+def test_mul_mat_id_vs_reference(mm, r):
+    a, b, ids, out_ne = G.mul_mat_id_operands(r)
+    da, db, di = dev_bytes(a.buf), dev_bytes(b.buf), dev_bytes(ids.buf)
+    nel = int(np.prod(out_ne))
+    dout = guarded_out(nel)
+    A = mm.tensor(a.type, da.data_ptr(), a.ne, a.nb)
+    B = mm.tensor(qref.F32, db.data_ptr(), b.ne, b.nb)
+    I = mm.tensor(qref.I32, di.data_ptr(), ids.ne, ids.nb)
+    D = mm.tensor(qref.F32, dout.data_ptr() + 4 * SENT, out_ne, qref.contiguous_nb(qref.F32, out_ne))
+    mm.mul_mat_id(A, B, I, D)
+    torch.cuda.synchronize()
+    got = check_guard(dout, nel)
+    want = G.load_bin(r["name"] + ".out.f32", np.float32)
+    assert qref.nmse(got, want) <= 5e-4
+    assert qref.nmse(got, G.oracle_mul_mat_id(a, b, ids, out_ne)) <= 5e-4
+
+
+QUANT = [r for r in G.manifest() if r["kind"] == "quant"]
+
+
+@pytest.mark.parametrize("r", QUANT, ids=lambda r: r["name"])
+def test_dequantize_bit_exact(mm, r):
+    q = G.load_bin(r["name"] + ".q", np.uint8)
+    want = G.load_bin(r["name"] + ".deq.f32", np.float32)
+    dq = dev_bytes(q)
+    out = torch.empty(r["n"], dtype=torch.float32, device="cuda")
+    mm.dequantize(r["type_id"], dq.data_ptr(), out.data_ptr(), r["n"])
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("t", qref.HOT_TYPES, ids=lambda t: qref.NAMES[t])
+@pytest.mark.parametrize("n", [0, 1, 3, 8, 9, 17])
+def test_edge_shapes(mm, t, n):
+    """empty batch, ragged columns and ragged K (K % 64 == 32 for the 32-block types)."""
+    K = 32 * 3 if qref.BLCK[t] == 32 else 512
+    N = 37
+    w = qref.quantize(t, qref.fill_uniform(N * K, 11), n_per_row=K)
+    x = qref.fill_uniform(max(n, 1) * K, 12)[: n * K]
+    a = G.Operand(t, w, [K, N, 1, 1], qref.contiguous_nb(t, [K, N, 1, 1]))
+    b = G.Operand(qref.F32, x if n else np.zeros(1, np.float32), [K, n, 1, 1], qref.contiguous_nb(qref.F32, [K, n, 1, 1]))
+    out_ne = [N, n, 1, 1]
+    got = run_mul_mat(mm, a, b, out_ne)
+    if n:
+        want = G.oracle_mul_mat(a, b, out_ne)
+        assert qref.nmse(got, want) <= 5e-4
+
+
+def test_rejects_bad_shapes(mm):
+    t = qref.Q4_K
+    w = torch.zeros(144 * 4, dtype=torch.uint8, device="cuda")
+    x = torch.zeros(256 * 2, dtype=torch.float32, device="cuda")
+    d = torch.zeros(8, dtype=torch.float32, device="cuda")
+    A = mm.tensor(t, w.data_ptr(), [256, 4, 1, 1], qref.contiguous_nb(t, [256, 4]))
+    B = mm.tensor(qref.F32, x.data_ptr(), [128, 4, 1, 1], qref.contiguous_nb(qref.F32, [128, 4]))   # K mismatch
+    D = mm.tensor(qref.F32, d.data_ptr(), [4, 2, 1, 1], qref.contiguous_nb(qref.F32, [4, 2]))
+    with pytest.raises(mm.Mi355xError):
+        mm.mul_mat(A, B, D)
