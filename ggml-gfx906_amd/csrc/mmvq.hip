@@ -52,43 +52,53 @@ __device__ inline void quantize_x_to_lds(const MmArgs &a, const uint8_t *xcol0, 
                                          int Kpad, int8_t *xq, float *xd, float *xs) {
     const int nslots = Kpad / 64;
     const int nblk = Kpad / 32;
+    const int total = NC * nblk;
     const int sub = threadIdx.x & 7;            // 8 lanes per 32-block, 4 values each
-    for (int b = threadIdx.x >> 3; b < NC * nblk; b += MMVQ_THREADS / 8) {
-        const int m = b / nblk, kb = b - m * nblk;
-        const int k0 = kb * 32 + sub * 4;
-        float v[4] = {0.f, 0.f, 0.f, 0.f};
-        if (k0 < a.K) {
-            const float *src = reinterpret_cast<const float *>(xcol0 + (int64_t)m * col_stride) + k0;
-            if (a.x_aligned16) {
-                const float4 t = *reinterpret_cast<const float4 *>(src);
-                v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-            } else {
-                v[0] = src[0]; v[1] = src[1]; v[2] = src[2]; v[3] = src[3];
+    constexpr int U = 4;                        // blocks in flight per lane group
+    constexpr int STRIDE = MMVQ_THREADS / 8;
+    for (int base = threadIdx.x >> 3; base < total; base += STRIDE * U) {
+        float4 v[U];
+        // issue every load of this round before any arithmetic (one L2/MALL latency per round)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int b = base + u * STRIDE;
+            v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (b < total) {
+                const int m = b / nblk, kb = b - m * nblk;
+                const int k0 = kb * 32 + sub * 4;
+                if (k0 < a.K) {
+                    const float *src = reinterpret_cast<const float *>(xcol0 + (int64_t)m * col_stride) + k0;
+                    if (a.x_aligned16) v[u] = *reinterpret_cast<const float4 *>(src);
+                    else v[u] = make_float4(src[0], src[1], src[2], src[3]);
+                }
             }
         }
-        float amax = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
-        amax = fmaxf(amax, __shfl_xor(amax, 1));
-        amax = fmaxf(amax, __shfl_xor(amax, 2));
-        amax = fmaxf(amax, __shfl_xor(amax, 4));
-        const float d = amax / 127.f;
-        const float id = amax > 0.f ? 127.f / amax : 0.f;
-        int q[4], qs = 0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            q[i] = (int)rintf(v[i] * id);
-            qs += q[i];
-        }
-        const uint32_t packed = (uint32_t)(q[0] & 0xff) | ((uint32_t)(q[1] & 0xff) << 8) |
-                                ((uint32_t)(q[2] & 0xff) << 16) | ((uint32_t)(q[3] & 0xff) << 24);
-        int s, j;
-        SlotMap<T>::place(kb * 2 + (sub >> 2), s, j);
-        *reinterpret_cast<uint32_t *>(xq + (size_t)m * Kpad + (size_t)(j * nslots + s) * 16 + (sub & 3) * 4) = packed;
-        qs += __shfl_xor(qs, 1);
-        qs += __shfl_xor(qs, 2);
-        qs += __shfl_xor(qs, 4);
-        if (sub == 0) {
-            xd[m * nblk + kb] = d;
-            xs[m * nblk + kb] = d * (float)qs;
+        for (int u = 0; u < U; ++u) {
+            const int b = base + u * STRIDE;
+            if (b >= total) break;              // uniform across the 8-lane group
+            const int m = b / nblk, kb = b - m * nblk;
+            float amax = fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w)));
+            amax = fmaxf(amax, __shfl_xor(amax, 1));
+            amax = fmaxf(amax, __shfl_xor(amax, 2));
+            amax = fmaxf(amax, __shfl_xor(amax, 4));
+            const float d = amax / 127.f;
+            const float id = amax > 0.f ? 127.f / amax : 0.f;
+            const int q0 = (int)rintf(v[u].x * id), q1 = (int)rintf(v[u].y * id);
+            const int q2 = (int)rintf(v[u].z * id), q3 = (int)rintf(v[u].w * id);
+            int qs = q0 + q1 + q2 + q3;
+            const uint32_t packed = (uint32_t)(q0 & 0xff) | ((uint32_t)(q1 & 0xff) << 8) |
+                                    ((uint32_t)(q2 & 0xff) << 16) | ((uint32_t)(q3 & 0xff) << 24);
+            int s, j;
+            SlotMap<T>::place(kb * 2 + (sub >> 2), s, j);
+            *reinterpret_cast<uint32_t *>(xq + (size_t)m * Kpad + (size_t)(j * nslots + s) * 16 + (sub & 3) * 4) = packed;
+            qs += __shfl_xor(qs, 1);
+            qs += __shfl_xor(qs, 2);
+            qs += __shfl_xor(qs, 4);
+            if (sub == 0) {
+                xd[m * nblk + kb] = d;
+                xs[m * nblk + kb] = d * (float)qs;
+            }
         }
     }
 }
