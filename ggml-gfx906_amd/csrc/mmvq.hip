@@ -47,58 +47,79 @@ template <> struct SlotMap<T_Q6_K> {
 //   xd : f32  [NC][Kpad/32] block scale d = amax / 127
 //   xs : f32  [NC][Kpad/32] d * sum(q)   (for the k-quant min terms)
 // ------------------------------------------------------------------------------------------
-template <int T, int NC>
-__device__ inline void quantize_x_to_lds(const MmArgs &a, const uint8_t *xcol0, int64_t col_stride,
-                                         int Kpad, int8_t *xq, float *xd, float *xs) {
-    const int nslots = Kpad / 64;
-    const int nblk = Kpad / 32;
+// Work split: 4 lanes per 32-block (8 values each, DPP reductions inside the quad); one
+// "round" = XR_U blocks per lane quad = 64 * XR_U blocks per workgroup.
+constexpr int XR_U = 4;
+constexpr int XR_STRIDE = MMVQ_THREADS / 4;
+
+struct XRound {
+    float4 v[XR_U][2];
+};
+
+template <int NC, bool XA>
+__device__ __forceinline__ void xround_load(const MmArgs &a, const uint8_t *xcol0, int64_t col_stride, int nblk,
+                                            int base, XRound &r) {
     const int total = NC * nblk;
-    const int sub = threadIdx.x & 7;            // 8 lanes per 32-block, 4 values each
-    constexpr int U = 4;                        // blocks in flight per lane group
-    constexpr int STRIDE = MMVQ_THREADS / 8;
-    for (int base = threadIdx.x >> 3; base < total; base += STRIDE * U) {
-        float4 v[U];
-        // issue every load of this round before any arithmetic (one L2/MALL latency per round)
+    const int sub = threadIdx.x & 3;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int b = base + u * STRIDE;
-            v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (b < total) {
-                const int m = b / nblk, kb = b - m * nblk;
-                const int k0 = kb * 32 + sub * 4;
-                if (k0 < a.K) {
-                    const float *src = reinterpret_cast<const float *>(xcol0 + (int64_t)m * col_stride) + k0;
-                    if (a.x_aligned16) v[u] = *reinterpret_cast<const float4 *>(src);
-                    else v[u] = make_float4(src[0], src[1], src[2], src[3]);
+    for (int u = 0; u < XR_U; ++u) {
+        const int b = base + u * XR_STRIDE;
+        r.v[u][0] = r.v[u][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (b < total) {
+            const int m = b / nblk, kb = b - m * nblk;
+            const int k0 = kb * 32 + sub * 8;
+            if (k0 < a.K) {
+                const float *src = reinterpret_cast<const float *>(xcol0 + (int64_t)m * col_stride) + k0;
+                if constexpr (XA) {
+                    r.v[u][0] = reinterpret_cast<const float4 *>(src)[0];
+                    r.v[u][1] = reinterpret_cast<const float4 *>(src)[1];
+                } else {
+                    r.v[u][0] = make_float4(src[0], src[1], src[2], src[3]);
+                    r.v[u][1] = make_float4(src[4], src[5], src[6], src[7]);
                 }
             }
         }
+    }
+}
+
+template <int T, int NC>
+__device__ __forceinline__ void xround_store(int nblk, int Kpad, int base, const XRound &r, int8_t *xq, float *xd,
+                                             float *xs) {
+    const int nslots = Kpad / 64;
+    const int total = NC * nblk;
+    const int sub = threadIdx.x & 3;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int b = base + u * STRIDE;
-            if (b >= total) break;              // uniform across the 8-lane group
-            const int m = b / nblk, kb = b - m * nblk;
-            float amax = fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w)));
-            amax = fmaxf(amax, __shfl_xor(amax, 1));
-            amax = fmaxf(amax, __shfl_xor(amax, 2));
-            amax = fmaxf(amax, __shfl_xor(amax, 4));
-            const float d = amax / 127.f;
-            const float id = amax > 0.f ? 127.f / amax : 0.f;
-            const int q0 = (int)rintf(v[u].x * id), q1 = (int)rintf(v[u].y * id);
-            const int q2 = (int)rintf(v[u].z * id), q3 = (int)rintf(v[u].w * id);
-            int qs = q0 + q1 + q2 + q3;
-            const uint32_t packed = (uint32_t)(q0 & 0xff) | ((uint32_t)(q1 & 0xff) << 8) |
-                                    ((uint32_t)(q2 & 0xff) << 16) | ((uint32_t)(q3 & 0xff) << 24);
-            int s, j;
-            SlotMap<T>::place(kb * 2 + (sub >> 2), s, j);
-            *reinterpret_cast<uint32_t *>(xq + (size_t)m * Kpad + (size_t)(j * nslots + s) * 16 + (sub & 3) * 4) = packed;
-            qs += __shfl_xor(qs, 1);
-            qs += __shfl_xor(qs, 2);
-            qs += __shfl_xor(qs, 4);
-            if (sub == 0) {
-                xd[m * nblk + kb] = d;
-                xs[m * nblk + kb] = d * (float)qs;
-            }
+    for (int u = 0; u < XR_U; ++u) {
+        const int b = base + u * XR_STRIDE;
+        if (b >= total) break;                  // uniform across the 4-lane group
+        const int m = b / nblk, kb = b - m * nblk;
+        const float f[8] = {r.v[u][0].x, r.v[u][0].y, r.v[u][0].z, r.v[u][0].w,
+                            r.v[u][1].x, r.v[u][1].y, r.v[u][1].z, r.v[u][1].w};
+        float amax = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(f[i]));
+        amax = fmaxf(amax, dpp_f<DPP_XOR1>(amax));
+        amax = fmaxf(amax, dpp_f<DPP_XOR2>(amax));
+        const float d = amax * (1.0f / 127.f);
+        const float id = amax > 0.f ? 127.f * __builtin_amdgcn_rcpf(amax) : 0.f;
+        uint32_t w0 = 0, w1 = 0;
+        int qs = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int q = max(-127, min(127, (int)rintf(f[i] * id)));
+            qs += q;
+            if (i < 4) w0 |= (uint32_t)(q & 0xff) << (8 * i);
+            else w1 |= (uint32_t)(q & 0xff) << (8 * (i - 4));
+        }
+        int s, j;
+        SlotMap<T>::place(kb * 2 + (sub >> 1), s, j);
+        *reinterpret_cast<uint2 *>(xq + (size_t)m * Kpad + (size_t)(j * nslots + s) * 16 + (sub & 1) * 8) = make_uint2(w0, w1);
+        float fs = (float)qs;
+        fs += dpp_f<DPP_XOR1>(fs);
+        fs += dpp_f<DPP_XOR2>(fs);
+        if (sub == 0) {
+            xd[m * nblk + kb] = d;
+            xs[m * nblk + kb] = d * fs;
         }
     }
 }
@@ -111,10 +132,11 @@ template <int T> struct Frag;
 // Q4_0: slot = blocks 2s, 2s+1 (36 contiguous bytes)
 template <> struct Frag<T_Q4_0> {
     uint32_t D[9];
+    template <bool RAG>
     __device__ inline void load(const uint8_t *row, int s, int nblk) {
         const uint8_t *p = row + (size_t)s * 36;
         ld16(p, D);
-        if (2 * s + 1 < nblk) {
+        if (!RAG || 2 * s + 1 < nblk) {
             ld16(p + 16, D + 4);
             D[8] = ld4(p + 32);
         } else {                     // ragged tail: K % 64 == 32, second block absent
@@ -144,11 +166,12 @@ template <> struct Frag<T_Q4_0> {
 // Q8_0: slot = blocks 2s, 2s+1 (68 contiguous bytes)
 template <> struct Frag<T_Q8_0> {
     uint32_t D[17];
+    template <bool RAG>
     __device__ inline void load(const uint8_t *row, int s, int nblk) {
         const uint8_t *p = row + (size_t)s * 68;
         ld16(p, D);
         ld16(p + 16, D + 4);
-        if (2 * s + 1 < nblk) {
+        if (!RAG || 2 * s + 1 < nblk) {
             ld16(p + 32, D + 8);
             ld16(p + 48, D + 12);
             D[16] = ld4(p + 64);
@@ -175,6 +198,7 @@ template <> struct Frag<T_Q8_0> {
 template <> struct Frag<T_Q4_K> {
     uint32_t H[4], Q[8];
     int c;
+    template <bool RAG>
     __device__ inline void load(const uint8_t *row, int s, int) {
         const uint8_t *p = row + (size_t)(s >> 2) * 144;
         c = s & 3;
@@ -203,6 +227,7 @@ template <> struct Frag<T_Q4_K> {
 template <> struct Frag<T_Q5_K> {
     uint32_t H[4], QH[8], Q[8];
     int c;
+    template <bool RAG>
     __device__ inline void load(const uint8_t *row, int s, int) {
         const uint8_t *p = row + (size_t)(s >> 2) * 176;
         c = s & 3;
@@ -242,6 +267,7 @@ template <> struct Frag<T_Q6_K> {
     uint32_t L0[4], L1[4], QH[4], SC[2];
     uint16_t dh;
     int p;
+    template <bool RAG>
     __device__ inline void load(const uint8_t *row, int s, int) {
         const uint8_t *b = row + (size_t)(s >> 2) * 210;
         const int h = (s >> 1) & 1;
@@ -296,32 +322,45 @@ template <int x> struct Log2 { static constexpr int v = 1 + Log2<x / 2>::v; };
 template <> struct Log2<1> { static constexpr int v = 0; };
 constexpr int pow2ceil(int x) { return x <= 1 ? 1 : 2 * pow2ceil((x + 1) / 2); }
 
+template <int V, int STEP>
+__device__ __forceinline__ void butterfly_step(float (&v)[V], int lane) {
+    constexpr int HALF = V >> (STEP + 1);
+    constexpr int DIST = 32 >> STEP;
+    const bool upper = (lane & DIST) != 0;
+#pragma unroll
+    for (int i = 0; i < HALF; ++i) {
+        const float send = upper ? v[i] : v[i + HALF];
+        const float keep = upper ? v[i + HALF] : v[i];
+        v[i] = keep + xchg<DIST>(send);
+    }
+}
+
 template <int V>
 __device__ inline float wave_reduce_transpose(float (&v)[V]) {
     constexpr int LV = Log2<V>::v;
     const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int step = 0; step < LV; ++step) {
-        const int half = V >> (step + 1);
-        const int dist = 32 >> step;
-        const bool upper = (lane & dist) != 0;
-#pragma unroll
-        for (int i = 0; i < half; ++i) {
-            const float send = upper ? v[i] : v[i + half];
-            const float keep = upper ? v[i + half] : v[i];
-            v[i] = keep + __shfl_xor(send, dist);
-        }
-    }
+    if constexpr (LV > 0) butterfly_step<V, 0>(v, lane);
+    if constexpr (LV > 1) butterfly_step<V, 1>(v, lane);
+    if constexpr (LV > 2) butterfly_step<V, 2>(v, lane);
+    if constexpr (LV > 3) butterfly_step<V, 3>(v, lane);
+    if constexpr (LV > 4) butterfly_step<V, 4>(v, lane);
+    if constexpr (LV > 5) butterfly_step<V, 5>(v, lane);
     float r = v[0];
-#pragma unroll
-    for (int dist = 32 >> LV; dist >= 1; dist >>= 1) r += __shfl_xor(r, dist);
+    if constexpr (LV <= 0) r += xchg<32>(r);
+    if constexpr (LV <= 1) r += xchg<16>(r);
+    if constexpr (LV <= 2) r += xchg<8>(r);
+    if constexpr (LV <= 3) r += xchg<4>(r);
+    if constexpr (LV <= 4) r += xchg<2>(r);
+    if constexpr (LV <= 5) r += xchg<1>(r);
     return r;
 }
 
 // ------------------------------------------------------------------------------------------
 // the kernel
+//   RAG : K % 64 == 32 (only possible for the 32-block types): last slot holds one block
+//   XA  : src1 rows and strides are 16-byte aligned (float4 activation loads)
 // ------------------------------------------------------------------------------------------
-template <int T, int NC, int RPW, bool IDS>
+template <int T, int NC, int RPW, bool IDS, bool RAG, bool XA>
 __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr int NX = XdCount<T>::n;
@@ -341,52 +380,61 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
     const uint8_t *wmat;
     const uint8_t *xcol0;
     uint8_t *dcol0;
-    int64_t xstride, dstride;
     if constexpr (IDS) {
         // one (expert slot e, token t) pair per blockIdx.y, NC == 1
         const int e = blockIdx.y % a.n_used, t = blockIdx.y / a.n_used;
-        const int ex = *reinterpret_cast<const int32_t *>(reinterpret_cast<const uint8_t *>(a.ids) + e * a.ids_nb0 + t * a.ids_nb1);
-        if (ex < 0 || ex >= a.n_expert) return;   // host validates; never index out of bounds
+        int ex = *reinterpret_cast<const int32_t *>(reinterpret_cast<const uint8_t *>(a.ids) + e * a.ids_nb0 + t * a.ids_nb1);
+        ex = min(max(ex, 0), a.n_expert - 1);     // host validates ids; never index out of bounds
         wmat = a.w + (int64_t)ex * a.nb02;
         xcol0 = a.x + (int64_t)(e % a.ne11_b) * a.nb11 + (int64_t)t * a.nb12;
         dcol0 = a.dst + (int64_t)e * a.nb1 + (int64_t)t * a.nb2;
-        xstride = a.nb11;
-        dstride = a.nb1;
     } else {
         const int i12 = blockIdx.y % a.ne12, i13 = blockIdx.y / a.ne12;
         wmat = a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03;
         xcol0 = a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13 + (int64_t)blockIdx.z * NC * a.nb11;
         dcol0 = a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3 + (int64_t)blockIdx.z * NC * a.nb1;
-        xstride = a.nb11;
-        dstride = a.nb1;
     }
 
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const int row0 = (blockIdx.x * MMVQ_WAVES + wave) * RPW;
 
-    // ---- issue the first slot's weight loads for all RPW rows before touching LDS
-    Frag<T> f[RPW];
+    // ---- activation loads first (L2/MALL hits), then the weight stream, so the quantization
+    // below waits only for the activations (vmcnt is in-order) while the weights stay in flight.
+    XRound xr;
+    const int xbase0 = threadIdx.x >> 2;
+    xround_load<NC, XA>(a, xcol0, a.nb11, nxblk, xbase0, xr);
+
+    // Row and slot indices are clamped (not predicated) so the weight loads are straight-line
+    // code: out-of-range lanes/rows read valid memory and their results are discarded.
+    const uint8_t *rowp[RPW];
 #pragma unroll
-    for (int r = 0; r < RPW; ++r) {
-        if (row0 + r < a.N && lane < nslots) f[r].load(wmat + (int64_t)(row0 + r) * a.nb01, lane, nblk);
-        else f[r].zero();
+    for (int r = 0; r < RPW; ++r) rowp[r] = wmat + (int64_t)min(row0 + r, a.N - 1) * a.nb01;
+    Frag<T> f[RPW];
+    {
+        const int s0 = min(lane, nslots - 1);
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) f[r].template load<RAG>(rowp[r], s0, nblk);
     }
 
-    quantize_x_to_lds<T, NC>(a, xcol0, xstride, Kpad, xq, xd, xs);
+    xround_store<T, NC>(nxblk, Kpad, xbase0, xr, xq, xd, xs);
+    for (int base = xbase0 + XR_STRIDE * XR_U; base < NC * nxblk; base += XR_STRIDE * XR_U) {
+        xround_load<NC, XA>(a, xcol0, a.nb11, nxblk, base, xr);
+        xround_store<T, NC>(nxblk, Kpad, base, xr, xq, xd, xs);
+    }
     __syncthreads();
 
     float acc[V];
 #pragma unroll
     for (int i = 0; i < V; ++i) acc[i] = 0.f;
 
-    for (int s = lane; s < nslots; s += WAVE) {
-        if (s != lane) {
+    for (int it = 0; it * WAVE < nslots; ++it) {
+        const int s_raw = lane + it * WAVE;
+        const int s = min(s_raw, nslots - 1);
+        const float live = s_raw < nslots ? 1.f : 0.f;
+        if (it > 0) {
 #pragma unroll
-            for (int r = 0; r < RPW; ++r) {
-                if (row0 + r < a.N) f[r].load(wmat + (int64_t)(row0 + r) * a.nb01, s, nblk);
-                else f[r].zero();
-            }
+            for (int r = 0; r < RPW; ++r) f[r].template load<RAG>(rowp[r], s, nblk);
         }
         // x block indices of this slot
         int xb0;
@@ -408,7 +456,7 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
                 sx[i] = xs[m * nxblk + xb0 + i];
             }
 #pragma unroll
-            for (int r = 0; r < RPW; ++r) acc[r * NC + m] += f[r].dot(X, dx, sx);
+            for (int r = 0; r < RPW; ++r) acc[r * NC + m] += live * f[r].dot(X, dx, sx);
         }
     }
 
@@ -417,7 +465,7 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
     const int idx = lane >> SHIFT;
     if ((lane & ((1 << SHIFT) - 1)) == 0 && idx < RPW * NC) {
         const int r = idx / NC, m = idx % NC;
-        if (row0 + r < a.N) reinterpret_cast<float *>(dcol0 + (int64_t)m * dstride)[row0 + r] = sum;
+        if (row0 + r < a.N) reinterpret_cast<float *>(dcol0 + (int64_t)m * a.nb1)[row0 + r] = sum;
     }
 }
 
@@ -429,32 +477,45 @@ size_t mmvq_lds_bytes(int K, int nc) {
     return (size_t)nc * Kpad + 2 * sizeof(float) * (size_t)nc * (Kpad / 32);
 }
 
-template <int T, int NC, int RPW, bool IDS>
-static hipError_t launch_one(const MmArgs &a, int grid_y, int grid_z, hipStream_t st) {
+template <int T, int NC, int RPW, bool IDS, bool RAG, bool XA>
+static hipError_t launch_one(const MmArgs &a, int grid_x_rows, int grid_y, int grid_z, hipStream_t st) {
     const size_t lds = mmvq_lds_bytes(a.K, NC);
-    auto kern = mmvq_kernel<T, NC, RPW, IDS>;
+    auto kern = mmvq_kernel<T, NC, RPW, IDS, RAG, XA>;
     static bool attr_set = false;   // per-instantiation
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
     const int rows_per_wg = MMVQ_WAVES * RPW;
-    dim3 grid((a.N + rows_per_wg - 1) / rows_per_wg, grid_y, grid_z);
+    dim3 grid((grid_x_rows + rows_per_wg - 1) / rows_per_wg, grid_y, grid_z);
     hipLaunchKernelGGL(kern, grid, dim3(MMVQ_THREADS), lds, st, a);
     return hipGetLastError();
+}
+
+template <int T, int NC, int RPW, bool IDS>
+static hipError_t launch_flags(const MmArgs &a, int grid_y, int grid_z, hipStream_t st) {
+    const bool rag = (a.K % 64) != 0;
+    if constexpr (T == T_Q4_0 || T == T_Q8_0) {
+        if (rag) {
+            return a.x_aligned16 ? launch_one<T, NC, RPW, IDS, true, true>(a, a.N, grid_y, grid_z, st)
+                                 : launch_one<T, NC, RPW, IDS, true, false>(a, a.N, grid_y, grid_z, st);
+        }
+    }
+    return a.x_aligned16 ? launch_one<T, NC, RPW, IDS, false, true>(a, a.N, grid_y, grid_z, st)
+                         : launch_one<T, NC, RPW, IDS, false, false>(a, a.N, grid_y, grid_z, st);
 }
 
 template <int T, int RPW>
 static hipError_t launch_nc(const MmArgs &a, int nc, int grid_y, int grid_z, hipStream_t st) {
     switch (nc) {
-        case 1: return launch_one<T, 1, RPW, false>(a, grid_y, grid_z, st);
-        case 2: return launch_one<T, 2, RPW, false>(a, grid_y, grid_z, st);
-        case 3: return launch_one<T, 3, RPW, false>(a, grid_y, grid_z, st);
-        case 4: return launch_one<T, 4, RPW, false>(a, grid_y, grid_z, st);
-        case 5: return launch_one<T, 5, RPW, false>(a, grid_y, grid_z, st);
-        case 6: return launch_one<T, 6, RPW, false>(a, grid_y, grid_z, st);
-        case 7: return launch_one<T, 7, RPW, false>(a, grid_y, grid_z, st);
-        case 8: return launch_one<T, 8, RPW, false>(a, grid_y, grid_z, st);
+        case 1: return launch_flags<T, 1, RPW, false>(a, grid_y, grid_z, st);
+        case 2: return launch_flags<T, 2, RPW, false>(a, grid_y, grid_z, st);
+        case 3: return launch_flags<T, 3, RPW, false>(a, grid_y, grid_z, st);
+        case 4: return launch_flags<T, 4, RPW, false>(a, grid_y, grid_z, st);
+        case 5: return launch_flags<T, 5, RPW, false>(a, grid_y, grid_z, st);
+        case 6: return launch_flags<T, 6, RPW, false>(a, grid_y, grid_z, st);
+        case 7: return launch_flags<T, 7, RPW, false>(a, grid_y, grid_z, st);
+        case 8: return launch_flags<T, 8, RPW, false>(a, grid_y, grid_z, st);
         default: return hipErrorInvalidValue;
     }
 }
@@ -468,7 +529,7 @@ static hipError_t launch_type(const MmArgs &a, int nc, int grid_y, int grid_z, i
     }
 }
 
-// plain MUL_MAT, a.M <= 8 columns per launch group; columns split into groups of nc
+// plain MUL_MAT: a.M columns in groups of nc (a.M % nc == 0)
 hipError_t mmvq_launch(int type, const MmArgs &a, int nc, int rpw, hipStream_t st) {
     const int grid_y = a.ne12 * a.ne13;
     const int grid_z = a.M / nc;
@@ -487,11 +548,11 @@ hipError_t mmvq_id_launch(int type, const MmArgs &a, int rpw, hipStream_t st) {
     const int grid_y = a.n_used * a.n_tok;
     (void)rpw;
     switch (type) {
-        case T_Q4_0: return launch_one<T_Q4_0, 1, 2, true>(a, grid_y, 1, st);
-        case T_Q8_0: return launch_one<T_Q8_0, 1, 2, true>(a, grid_y, 1, st);
-        case T_Q4_K: return launch_one<T_Q4_K, 1, 2, true>(a, grid_y, 1, st);
-        case T_Q5_K: return launch_one<T_Q5_K, 1, 2, true>(a, grid_y, 1, st);
-        case T_Q6_K: return launch_one<T_Q6_K, 1, 2, true>(a, grid_y, 1, st);
+        case T_Q4_0: return launch_flags<T_Q4_0, 1, 2, true>(a, grid_y, 1, st);
+        case T_Q8_0: return launch_flags<T_Q8_0, 1, 2, true>(a, grid_y, 1, st);
+        case T_Q4_K: return launch_flags<T_Q4_K, 1, 2, true>(a, grid_y, 1, st);
+        case T_Q5_K: return launch_flags<T_Q5_K, 1, 2, true>(a, grid_y, 1, st);
+        case T_Q6_K: return launch_flags<T_Q6_K, 1, 2, true>(a, grid_y, 1, st);
         default: return hipErrorInvalidValue;
     }
 }

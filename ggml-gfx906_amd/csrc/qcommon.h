@@ -75,4 +75,56 @@ __device__ __forceinline__ void k4_scale_min_pair(const uint32_t S[3], int c, ui
     m1  = (mw >> (sh + 8)) & 0xff;
 }
 
+// ------------------------------------------------------------------------------------------
+// cross-lane exchange without the LDS pipe: DPP within rows of 16, permlane swaps across
+// rows / halves (gfx950 v_permlane16_swap / v_permlane32_swap). Each returns the value of
+// lane (lane ^ mask) for the listed partner pattern.
+//   xor1  quad_perm [1,0,3,2]        xor2  quad_perm [2,3,0,1]
+//   mir7  row_half_mirror (lane ^ 7 inside each 8)
+//   mir15 row_mirror      (lane ^ 15 inside each 16)
+//   sw16  lane ^ 16                    sw32  lane ^ 32
+// The mirrors flip the low bits too; reductions that only combine symmetric partial sums
+// (and the butterfly below, which consumes the bits from high to low) stay exact.
+// ------------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, dpp_u<CTRL>(__builtin_bit_cast(uint32_t, v)));
+}
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_MIR7 = 0x141, DPP_MIR15 = 0x140;
+
+__device__ __forceinline__ float swap16_f(float v) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, v);
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return __builtin_bit_cast(float, (threadIdx.x & 16) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float swap32_f(float v) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, v);
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return __builtin_bit_cast(float, (threadIdx.x & 32) ? r[0] : r[1]);
+}
+
+// partner value for butterfly distance D (D = 32, 16, 8, 4, 2, 1)
+template <int D> __device__ __forceinline__ float xchg(float v);
+template <> __device__ __forceinline__ float xchg<32>(float v) { return swap32_f(v); }
+template <> __device__ __forceinline__ float xchg<16>(float v) { return swap16_f(v); }
+template <> __device__ __forceinline__ float xchg<8>(float v) { return dpp_f<DPP_MIR15>(v); }
+template <> __device__ __forceinline__ float xchg<4>(float v) { return dpp_f<DPP_MIR7>(v); }
+template <> __device__ __forceinline__ float xchg<2>(float v) { return dpp_f<DPP_XOR2>(v); }
+template <> __device__ __forceinline__ float xchg<1>(float v) { return dpp_f<DPP_XOR1>(v); }
+
+// full 64-lane sum, result in every lane
+__device__ __forceinline__ float wave_sum(float v) {
+    v += xchg<1>(v);
+    v += xchg<2>(v);
+    v += xchg<4>(v);
+    v += xchg<8>(v);
+    v += xchg<16>(v);
+    v += xchg<32>(v);
+    return v;
+}
+
 }  // namespace mi355x
