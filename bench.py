@@ -1,23 +1,31 @@
 #!/usr/bin/env python3
 """bench.py — MI355X quantized MUL_MAT throughput (BASELINE.json metric) on 1..8 GPUs.
 
-Workload (N=1 headline, BASELINE.json configs[1]): Q4_0 mat-vec, K=4096, N=4096 rows, M=1
-column, HBM-cold. One *step* = one pass over a batch of L=64 distinct weight matrices
-(64 x 9.44 MB = 604 MB > 256 MB Infinity Cache, so every GEMV streams from HBM), issued as a
-captured hipGraph of 64 dependent-free launches on one stream. value = algorithmic bytes of
-all GEMVs of all ranks / max-over-ranks wall time of the timed steps (GB/s).
+Headline workload (N=1, BASELINE.json configs[1]): Q4_0 mat-vec, K=4096, N=4096 rows, M=1
+column, HBM-cold. One *step* = ONE GGML_OP_MUL_MAT over a stack of B=64 independent 4096x4096
+Q4_0 matrices, each with its own activation column (ggml's batched mat-vec: src0 ne02=64,
+src1 ne12=64) — 606 MB of weights per step, > 2x the 256 MB Infinity Cache, so every byte
+streams from HBM. value = algorithmic bytes of all steps of all ranks / max-over-ranks wall
+time of the timed steps (GB/s).
+
+Why batched: a single 9.5 MB GEMV is bounded by the launch, not by HBM — on MI355X an empty
+kernel already costs 1.4-1.6 us of device time and dependent launches on one stream issue
+every ~2.8 us (scripts/hbm_probe.hip); the per-matrix numbers are reported beside it
+(configs.*_single) so both regimes are visible.
 
 Multi-GPU (torchrun, one rank per GPU): every rank runs the same per-GPU workload on its own
-weights (weak scaling, no data-path collective — GEMV batches over independent matrices
-partition with no exchange); barriers + max-over-ranks timing use torch.distributed (RCCL).
+weights (weak scaling, no data-path collective — independent matrices partition with no
+exchange); barriers + max-over-ranks timing go through torch.distributed (RCCL).
 
 Extra fields on the single JSON line:
-  roofline      dominant kernel (the GEMV): algorithmic bytes per launch / its mean duration,
-                timed live with HIP events around each launch on the launch stream
+  roofline      the mat-vec kernel: algorithmic bytes per launch / mean launch duration
+                (HIP events around each launch on the launch stream)
   cpu_baseline  the reference's own ggml-cpu (oracle/_ref, built from the reference sources)
-                on a bounded sample of the same workload (falls back to the C oracle port)
+                on a bounded sample (Q4_0 4096x4096 mat-vec, rotated weights); falls back
+                to the C oracle port
   configs       the other BASELINE.json kernel configs (Q4_K north star, Q4_K/Q5_K/Q6_K
-                4096x11008, Q8_0 M=512), kernel-time GB/s, TFLOP/s and roofline fractions
+                4096x11008, Q8_0 M=512): GB/s, TFLOP/s, roofline fractions; *_single rows
+                are one matrix per launch
 """
 from __future__ import annotations
 
@@ -64,32 +72,31 @@ def alg_bytes(t: int, K: int, N: int, Mc: int) -> int:
     return M.row_size(t, K) * N + 4 * K * Mc + 4 * N * Mc
 
 
-class GemvSet:
-    """L device copies of one weight matrix + activations/outputs for one config."""
+class MatVecSet:
+    """`copies` device copies of a stacked weight tensor [K, N, batch] (quantized rows) plus
+    activations [K, M, batch] and outputs [N, M, batch]: one launch = one MUL_MAT over the
+    whole stack (ne02 = ne12 = batch), rotating over the copies."""
 
-    def __init__(self, torch, t: int, K: int, N: int, Mc: int, copies: int, seed: int = 1234):
-        self.torch, self.t, self.K, self.N, self.Mc, self.copies = torch, t, K, N, Mc, copies
-        host = synthetic_weights(t, N, K, seed)
-        base = torch.from_numpy(host.reshape(-1)).cuda()
-        self.w = [base] + [base.clone() for _ in range(copies - 1)]
+    def __init__(self, torch, t: int, K: int, N: int, Mc: int, batch: int, copies: int, seed: int = 1234):
+        self.torch, self.t, self.K, self.N, self.Mc, self.batch, self.copies = torch, t, K, N, Mc, batch, copies
+        host = synthetic_weights(t, N, K, seed)                       # one matrix, replicated on device
+        one = torch.from_numpy(host.reshape(-1)).cuda()
+        self.w = [one.repeat(batch) for _ in range(copies)]
         rng = np.random.default_rng(seed + 1)
-        self.x = torch.from_numpy(rng.uniform(-1, 1, size=(Mc, K)).astype(np.float32)).cuda()
-        self.y = torch.zeros((Mc, N), dtype=torch.float32, device="cuda")
-        self.B = M.tensor(M.F32, self.x.data_ptr(), [K, Mc, 1, 1], M.contiguous_nb(M.F32, [K, Mc]))
-        self.D = M.tensor(M.F32, self.y.data_ptr(), [N, Mc, 1, 1], M.contiguous_nb(M.F32, [N, Mc]))
-        self.A = [M.tensor(t, wi.data_ptr(), [K, N, 1, 1], M.contiguous_nb(t, [K, N])) for wi in self.w]
-        self.bytes = alg_bytes(t, K, N, Mc)
-        self.flops = 2.0 * K * N * Mc
+        self.x = torch.from_numpy(rng.uniform(-1, 1, size=(batch, Mc, K)).astype(np.float32)).cuda()
+        self.y = torch.zeros((batch, Mc, N), dtype=torch.float32, device="cuda")
+        nb_a = M.contiguous_nb(t, [K, N, batch])
+        self.A = [M.tensor(t, wi.data_ptr(), [K, N, batch, 1], nb_a) for wi in self.w]
+        self.B = M.tensor(M.F32, self.x.data_ptr(), [K, Mc, batch, 1], M.contiguous_nb(M.F32, [K, Mc, batch]))
+        self.D = M.tensor(M.F32, self.y.data_ptr(), [N, Mc, batch, 1], M.contiguous_nb(M.F32, [N, Mc, batch]))
+        self.bytes = alg_bytes(t, K, N, Mc) * batch
+        self.flops = 2.0 * K * N * Mc * batch
 
     def launch(self, i: int, stream=None) -> None:
         M.mul_mat(self.A[i % self.copies], self.B, self.D, stream)
 
-    def sweep(self) -> None:
-        for i in range(self.copies):
-            self.launch(i)
-
-    def kernel_time_us(self, reps: int) -> float:
-        """mean duration of one launch, HIP events around each launch on the launch stream"""
+    def launch_us(self, reps: int) -> float:
+        """mean device time of one launch: HIP events around each launch on its stream"""
         torch = self.torch
         st = torch.cuda.current_stream()
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
@@ -98,8 +105,37 @@ class GemvSet:
             self.launch(i)
             b.record(st)
         torch.cuda.synchronize()
-        ts = sorted(a.elapsed_time(b) * 1e3 for a, b in evs)
-        return float(np.mean(ts[: max(1, int(0.9 * len(ts)))]))   # drop the slowest 10 % (host jitter)
+        return float(np.mean([a.elapsed_time(b) * 1e3 for a, b in evs]))
+
+    def graph_period_us(self, n: int) -> float:
+        """per-launch period of n back-to-back launches captured in one hipGraph"""
+        torch = self.torch
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for i in range(n):
+                self.launch(i)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for i in range(n):
+                self.launch(i)
+        g.replay()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(5):
+            g.replay()
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) * 1e3 / (5 * n)
+
+
+def config_row(s: MatVecSet, us: float) -> dict:
+    gbs = s.bytes / (us * 1e-6) / 1e9
+    tf = s.flops / (us * 1e-6) / 1e12
+    return {"us": round(us, 3), "GB/s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+            "TFLOP/s": round(tf, 3)}
 
 
 def cpu_baseline(seconds: float) -> dict:
@@ -136,10 +172,9 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--copies", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-extra", action="store_true", help="skip the secondary configs")
-    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a hipGraph step")
     args = ap.parse_args()
 
     import torch
@@ -160,33 +195,19 @@ def main() -> None:
             dist.barrier()
         torch.cuda.synchronize()
 
-    # ---------------- headline: Q4_0 4096x4096 M=1, 64 rotated copies per step ----------------
-    g = GemvSet(torch, M.Q4_0, 4096, 4096, 1, args.copies)
-    g.sweep()
+    # ---------------- headline: one MUL_MAT over 64 stacked Q4_0 4096x4096 matrices ------------
+    BATCH = args.batch
+    g = MatVecSet(torch, M.Q4_0, 4096, 4096, 1, BATCH, 2)
+    for i in range(2):
+        g.launch(i)
     torch.cuda.synchronize()
-    graph = None
-    if not args.no_graph:
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            g.sweep()
-        torch.cuda.current_stream().wait_stream(s)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            g.sweep()
 
-    def step():
-        if graph is not None:
-            graph.replay()
-        else:
-            g.sweep()
-
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        g.launch(i)
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for i in range(args.steps):
+        g.launch(i)
     barrier()
     elapsed = time.perf_counter() - t0
     t_max = elapsed
@@ -195,29 +216,34 @@ def main() -> None:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt.item())
 
-    kernel_us = g.kernel_time_us(256)
-    launches = args.steps * args.copies
-    total_bytes = g.bytes * launches * world
-    value = total_bytes / t_max / 1e9
+    kernel_us = g.launch_us(max(8, args.steps))
+    value = g.bytes * args.steps * world / t_max / 1e9
     achieved = g.bytes / (kernel_us * 1e-6) / 1e9
 
     extra = {}
     if not args.no_extra and rank == 0:
-        for name, t, K, N, Mc, copies in (
-            ("q4_K_4096x4096_m1", M.Q4_K, 4096, 4096, 1, 64),
-            ("q4_K_4096x11008_m1", M.Q4_K, 4096, 11008, 1, 24),
-            ("q5_K_4096x11008_m1", M.Q5_K, 4096, 11008, 1, 24),
-            ("q6_K_4096x11008_m1", M.Q6_K, 4096, 11008, 1, 24),
-            ("q8_0_4096x4096_m512", M.Q8_0, 4096, 4096, 512, 24),
+        # single-matrix launches (launch-bound regime), 64 copies rotated for HBM-cold reads
+        single = MatVecSet(torch, M.Q4_0, 4096, 4096, 1, 1, 64)
+        extra["q4_0_4096x4096_m1_single"] = dict(config_row(single, single.launch_us(64)),
+                                                 graph_period_us=round(single.graph_period_us(64), 3))
+        del single
+        for name, t, K, N, Mc, batch in (
+            ("q4_K_4096x4096_m1_b64", M.Q4_K, 4096, 4096, 1, 64),
+            ("q4_K_4096x11008_m1_b24", M.Q4_K, 4096, 11008, 1, 24),
+            ("q5_K_4096x11008_m1_b24", M.Q5_K, 4096, 11008, 1, 24),
+            ("q6_K_4096x11008_m1_b24", M.Q6_K, 4096, 11008, 1, 24),
+            ("q8_0_4096x4096_m512", M.Q8_0, 4096, 4096, 512, 1),
         ):
-            s2 = GemvSet(torch, t, K, N, Mc, copies)
-            s2.sweep()
+            s2 = MatVecSet(torch, t, K, N, Mc, batch, 2 if batch > 1 else 24)
+            s2.launch(0)
             torch.cuda.synchronize()
-            us = s2.kernel_time_us(64 if Mc == 1 else 24)
-            gbs = s2.bytes / (us * 1e-6) / 1e9
-            tf = s2.flops / (us * 1e-6) / 1e12
-            extra[name] = {"kernel_us": round(us, 3), "GB/s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
-                           "TFLOP/s": round(tf, 2)}
+            extra[name] = config_row(s2, s2.launch_us(16))
+            if batch > 1:
+                one = MatVecSet(torch, t, K, N, Mc, 1, 64)
+                one.launch(0)
+                extra[name.rsplit("_b", 1)[0] + "_single"] = dict(config_row(one, one.launch_us(64)),
+                                                                  graph_period_us=round(one.graph_period_us(64), 3))
+                del one
             del s2
             torch.cuda.empty_cache()
 
@@ -235,15 +261,15 @@ def main() -> None:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "q4_0 x int8 (int32 block dots, fp32 scale accumulate)",
+            "dtype": "q4_0 weights x int8 activations (int32 block dots, fp32 scale accumulate)",
             "data": "synthetic (random quant bits, fp16 scales 0.01; x ~ U[-1,1])",
-            "config": {"workload": "configs[1]: Q4_0 mul_mat_vec K=4096 N=4096 M=1",
-                       "gemv_per_step": args.copies, "weight_copies": args.copies,
-                       "weight_bytes_per_gpu": g.bytes * args.copies, "graph": graph is not None,
-                       "parallelism": f"independent weight sets per GPU x{world}"},
+            "config": {"workload": f"configs[1]: Q4_0 mul_mat_vec K=4096 N=4096 M=1, {BATCH} independent "
+                                   f"matrices per MUL_MAT (ne02=ne12={BATCH})",
+                       "matrices_per_step": BATCH, "weight_bytes_per_step": g.bytes,
+                       "parallelism": f"independent weight stacks per GPU x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel_us": round(kernel_us, 3), "alg_bytes_per_launch": g.bytes,
+                         "launch_us": round(kernel_us, 3), "alg_bytes_per_launch": g.bytes,
                          "frac_of_measured_copy_bw": round(achieved / HBM_MEASURED_GBS, 4)},
             "cpu_baseline": cpu,
             "configs": extra,

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/ggml-mi355x.h"
@@ -48,12 +49,29 @@ int type_bytes(int t) {
 
 bool is_hot_quant(int t) { return type_blck(t) != 0; }
 
-// rows per wave for the mat-vec: enough workgroups to cover 256 CUs at least twice,
-// more rows per wave (fewer redundant activation quantizations) once N is large.
-static int pick_rpw(int N) {
-    if (N >= 16384) return 4;
-    if (N >= 4096) return 2;
+// rows per wave for the mat-vec. Every workgroup quantizes its column(s) of src1 once, so
+// more rows per workgroup amortize that; fewer rows give more workgroups. A single 4096-row
+// matrix needs all 512 workgroups of RPW=1 to cover 256 CUs twice; batched / taller problems
+// (rows x batch) switch to 2 and 4 rows per wave.
+static int pick_rpw(int64_t rows_total) {
+    if (rows_total >= 262144) return 4;
+    if (rows_total >= 16384) return 2;
     return 1;
+}
+
+// ------------------------------------------------------------------------------------------
+// diagnostics: GGML_MI355X_STAMPS=1 makes every mat-vec launch record per-workgroup
+// s_memrealtime stamps (start / activations in LDS / dots done / end) into a device buffer that
+// ggml_mi355x_debug_stamps() copies out. Off by default: kernels test one null pointer.
+// ------------------------------------------------------------------------------------------
+static unsigned long long *g_stamps = nullptr;
+static const size_t STAMP_SLOTS = 8 * 65536;
+
+static unsigned long long *stamps_buffer() {
+    static const bool on = getenv("GGML_MI355X_STAMPS") != nullptr;
+    if (!on) return nullptr;
+    if (!g_stamps && hipMalloc(&g_stamps, STAMP_SLOTS * sizeof(unsigned long long)) != hipSuccess) g_stamps = nullptr;
+    return g_stamps;
 }
 
 static bool aligned16(const void *p, int64_t s1, int64_t s2, int64_t s3) {
@@ -87,12 +105,15 @@ static MmArgs base_args(const TensorView &a, const TensorView &b, const TensorVi
     m.r2 = (int)(b.ne[2] / a.ne[2]);
     m.r3 = (int)(b.ne[3] / a.ne[3]);
     m.x_aligned16 = aligned16(b.data, m.nb11, m.nb12, m.nb13);
+    m.stamps = stamps_buffer();
+    static const int diag = getenv("GGML_MI355X_DIAG") ? atoi(getenv("GGML_MI355X_DIAG")) : 0;
+    m.diag = diag;
     return m;
 }
 
 // mat-vec over columns [c0, c0 + ncols) in groups of at most 8
 static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st) {
-    const int rpw = pick_rpw(m.N);
+    const int rpw = pick_rpw((int64_t)m.N * m.ne12 * m.ne13);
     while (ncols > 0) {
         int nc = std::min(ncols, 8);
         while (nc > 1 && mmvq_lds_bytes(m.K, nc) > LDS_LIMIT) --nc;
@@ -155,7 +176,7 @@ int mul_mat_id(const TensorView &as, const TensorView &b, const TensorView &ids,
     m.ne11_b = (int)b.ne[1];
     m.n_expert = (int)as.ne[2];
     m.x_aligned16 = aligned16(b.data, m.nb11, m.nb12, m.nb13);
-    const hipError_t e = mmvq_id_launch(as.type, m, pick_rpw(m.N), st);
+    const hipError_t e = mmvq_id_launch(as.type, m, 1, st);
     return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
 }
 
@@ -248,6 +269,13 @@ int ggml_mi355x_device_count(void) {
         if (hipGetDeviceProperties(&p, i) == hipSuccess && strncmp(p.gcnArchName, "gfx950", 6) == 0) ++good;
     }
     return good;
+}
+
+// diagnostics only (not in the public header): copy the last launch's workgroup stamps
+__attribute__((visibility("default"))) int ggml_mi355x_debug_stamps(unsigned long long *host, size_t n) {
+    if (!g_stamps) return -1;
+    if (n > STAMP_SLOTS) n = STAMP_SLOTS;
+    return hipMemcpy(host, g_stamps, n * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
 }
 
 const char *ggml_mi355x_strerror(int status) {

@@ -3,30 +3,34 @@
 // Replaces the reference's mul_mat_vec_q / quantize_q8_1 pair (src/ggml-cuda/mmvq.cu:139-226,
 // quantize.cu:4-48) with a CDNA4-first design:
 //
-//  * one 256-thread workgroup = 4 waves; each wave owns RPW consecutive weight rows;
+//  * one 512-thread workgroup = 8 waves; each wave owns RPW consecutive weight rows;
 //  * a lane owns a fixed 64-weight "slot" of K for every row it touches (Q4_0/Q8_0: two
-//    32-blocks; Q4_K/Q5_K: one 64-chunk of a super-block; Q6_K: a quarter of a 128-half),
-//    so the weight stream of a wave is a set of wide (dwordx4) loads from one row, issued for
-//    all RPW rows before any arithmetic, read straight to VGPRs (no LDS round trip);
+//    32-blocks; Q4_K/Q5_K: one 64-chunk of a super-block; Q6_K: a quarter of a 128-half), so
+//    a wave's weight stream is a handful of wide (dwordx4) loads per row, issued for all RPW
+//    rows up front, straight to VGPRs (no LDS round trip for the once-read weights);
 //  * src1 is quantized to int8 per 32-block (d = amax/127, round-to-nearest-even) once per
-//    workgroup, into LDS, in a slot-interleaved layout so lane s reads its 64 activations with
-//    4 conflict-free ds_read_b128; d and d*sum(q) per 32-block sit beside them;
-//  * integer block dots on v_dot4_i32_i8 (weights unpacked to signed int8 lanes), fp32 scale
-//    accumulation per block, exactly the reference's per-block arithmetic (ggml-cpu/quants.c);
-//  * cross-lane reduction by a butterfly transpose: RPW*NC partial sums per lane collapse to
-//    one value per lane in log2 steps of halving width, then the plain tail.
+//    workgroup into LDS, in a slot-interleaved layout so lane s reads its 64 activations with
+//    4 conflict-free ds_read_b128. Quantization is ~2 VALU per value: one FMA against the
+//    1.5*2^23 magic constant rounds and biases, v_perm_b32 packs bytes, v_dot4_u32_u8 sums;
+//  * beside the bytes sit d, d*sum(q) per 32-block and d*sum(q) per 16-run, so the zero-point
+//    terms of Q4_0 (q-8), Q6_K (q-32) and the Q4_K/Q5_K mins cost one FMA per block instead of
+//    a per-byte fix-up;
+//  * integer block dots on v_dot4_i32_i8, fp32 scale accumulation per block — the reference's
+//    per-block arithmetic (src/ggml-cpu/quants.c:115-758);
+//  * cross-lane reduction by a butterfly transpose on DPP / permlane swaps: RPW*NC partial
+//    sums per lane collapse to one value per lane without touching LDS.
 //
-// Templated on <type, NC columns, RPW rows per wave, IDS = MUL_MAT_ID routing>.
+// Templated on <type, NC columns, RPW rows per wave, IDS = MUL_MAT_ID routing, RAG, XA>.
 #include "qcommon.h"
 #include "qmm_args.h"
 
 namespace mi355x {
 
-constexpr int MMVQ_WAVES = 4;
+constexpr int MMVQ_WAVES = 8;
 constexpr int MMVQ_THREADS = MMVQ_WAVES * WAVE;
 
 // ------------------------------------------------------------------------------------------
-// slot geometry: K-chunk (16 activations) q  <->  (slot s, part j) with q = chunk_of(s, j)
+// slot geometry: K-chunk (16 activations) q  <->  (slot s, part j)
 // ------------------------------------------------------------------------------------------
 template <int T> struct SlotMap {
     // slot s covers activations [64 s, 64 s + 64): parts are consecutive 16-chunks
@@ -42,94 +46,94 @@ template <> struct SlotMap<T_Q6_K> {
 };
 
 // ------------------------------------------------------------------------------------------
-// activation quantization into LDS
-//   xq : int8 [NC][Kpad]   slot-interleaved: chunk (s, j) at (j * nslots + s) * 16
-//   xd : f32  [NC][Kpad/32] block scale d = amax / 127
-//   xs : f32  [NC][Kpad/32] d * sum(q)   (for the k-quant min terms)
+// activation quantization into LDS (per column m, Kpad = K rounded up to 64):
+//   xq  : int8 [Kpad]      slot-interleaved: chunk (s, j) at (j * nslots + s) * 16
+//   xd  : f32  [Kpad/32]   block scale d = amax / 127
+//   xs  : f32  [Kpad/32]   d * sum(q) over the 32-block
+//   x16 : f32  [Kpad/16]   d * sum(q) over each 16-run
+// Work split: 4 lanes per 32-block (8 values each, DPP inside the quad); a round covers
+// MMVQ_THREADS/4 blocks; loads of a round are issued before its arithmetic.
 // ------------------------------------------------------------------------------------------
-// Work split: 4 lanes per 32-block (8 values each, DPP reductions inside the quad); one
-// "round" = XR_U blocks per lane quad = 64 * XR_U blocks per workgroup.
-constexpr int XR_U = 4;
-constexpr int XR_STRIDE = MMVQ_THREADS / 4;
-
-struct XRound {
-    float4 v[XR_U][2];
+struct XSmem {
+    int8_t *xq;
+    float *xd, *xs, *x16;
 };
 
-template <int NC, bool XA>
-__device__ __forceinline__ void xround_load(const MmArgs &a, const uint8_t *xcol0, int64_t col_stride, int nblk,
-                                            int base, XRound &r) {
-    const int total = NC * nblk;
-    const int sub = threadIdx.x & 3;
-#pragma unroll
-    for (int u = 0; u < XR_U; ++u) {
-        const int b = base + u * XR_STRIDE;
-        r.v[u][0] = r.v[u][1] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (b < total) {
-            const int m = b / nblk, kb = b - m * nblk;
-            const int k0 = kb * 32 + sub * 8;
-            if (k0 < a.K) {
-                const float *src = reinterpret_cast<const float *>(xcol0 + (int64_t)m * col_stride) + k0;
-                if constexpr (XA) {
-                    r.v[u][0] = reinterpret_cast<const float4 *>(src)[0];
-                    r.v[u][1] = reinterpret_cast<const float4 *>(src)[1];
-                } else {
-                    r.v[u][0] = make_float4(src[0], src[1], src[2], src[3]);
-                    r.v[u][1] = make_float4(src[4], src[5], src[6], src[7]);
-                }
-            }
+__device__ __forceinline__ XSmem xsmem(uint8_t *smem, int Kpad, int nc) {
+    XSmem s;
+    s.xq = reinterpret_cast<int8_t *>(smem);
+    s.xd = reinterpret_cast<float *>(smem + (size_t)nc * Kpad);
+    s.xs = s.xd + nc * (Kpad / 32);
+    s.x16 = s.xs + nc * (Kpad / 32);
+    return s;
+}
+
+constexpr int XR_STRIDE = MMVQ_THREADS / 4;
+
+template <bool XA>
+__device__ __forceinline__ void xblock_load(const MmArgs &a, const uint8_t *xcol, int kb, float4 &v0, float4 &v1) {
+    const int k0 = kb * 32 + (threadIdx.x & 3) * 8;
+    v0 = v1 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (k0 < a.K && !(a.diag & 1)) {
+        const float *src = reinterpret_cast<const float *>(xcol) + k0;
+        if constexpr (XA) {
+            v0 = reinterpret_cast<const float4 *>(src)[0];
+            v1 = reinterpret_cast<const float4 *>(src)[1];
+        } else {
+            v0 = make_float4(src[0], src[1], src[2], src[3]);
+            v1 = make_float4(src[4], src[5], src[6], src[7]);
         }
     }
 }
 
-template <int T, int NC>
-__device__ __forceinline__ void xround_store(int nblk, int Kpad, int base, const XRound &r, int8_t *xq, float *xd,
-                                             float *xs) {
-    const int nslots = Kpad / 64;
-    const int total = NC * nblk;
+template <int T>
+__device__ __forceinline__ void xblock_store(int Kpad, int kb, const float4 &v0, const float4 &v1, int8_t *xq,
+                                             float *xd, float *xs, float *x16) {
     const int sub = threadIdx.x & 3;
-#pragma unroll
-    for (int u = 0; u < XR_U; ++u) {
-        const int b = base + u * XR_STRIDE;
-        if (b >= total) break;                  // uniform across the 4-lane group
-        const int m = b / nblk, kb = b - m * nblk;
-        const float f[8] = {r.v[u][0].x, r.v[u][0].y, r.v[u][0].z, r.v[u][0].w,
-                            r.v[u][1].x, r.v[u][1].y, r.v[u][1].z, r.v[u][1].w};
-        float amax = 0.f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(f[i]));
-        amax = fmaxf(amax, dpp_f<DPP_XOR1>(amax));
-        amax = fmaxf(amax, dpp_f<DPP_XOR2>(amax));
-        const float d = amax * (1.0f / 127.f);
-        const float id = amax > 0.f ? 127.f * __builtin_amdgcn_rcpf(amax) : 0.f;
-        uint32_t w0 = 0, w1 = 0;
-        int qs = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int q = max(-127, min(127, (int)rintf(f[i] * id)));
-            qs += q;
-            if (i < 4) w0 |= (uint32_t)(q & 0xff) << (8 * i);
-            else w1 |= (uint32_t)(q & 0xff) << (8 * (i - 4));
-        }
-        int s, j;
-        SlotMap<T>::place(kb * 2 + (sub >> 1), s, j);
-        *reinterpret_cast<uint2 *>(xq + (size_t)m * Kpad + (size_t)(j * nslots + s) * 16 + (sub & 1) * 8) = make_uint2(w0, w1);
-        float fs = (float)qs;
-        fs += dpp_f<DPP_XOR1>(fs);
-        fs += dpp_f<DPP_XOR2>(fs);
-        if (sub == 0) {
-            xd[m * nblk + kb] = d;
-            xs[m * nblk + kb] = d * fs;
-        }
+    float amax = fmaxf(fmaxf(fmaxf(fabsf(v0.x), fabsf(v0.y)), fmaxf(fabsf(v0.z), fabsf(v0.w))),
+                       fmaxf(fmaxf(fabsf(v1.x), fabsf(v1.y)), fmaxf(fabsf(v1.z), fabsf(v1.w))));
+    amax = fmaxf(amax, dpp_f<DPP_XOR1>(amax));
+    amax = fmaxf(amax, dpp_f<DPP_XOR2>(amax));
+    const float d = amax * (1.0f / 127.f);
+    const float id = amax > 0.f ? 127.f * __builtin_amdgcn_rcpf(amax) : 0.f;
+    // t = x*id + (1.5*2^23 + 128): the FMA rounds to nearest-even into the mantissa, so the
+    // low byte of t's bits is 128 + q with q in [-127, 127]
+    constexpr float MAGIC = 12582912.0f + 128.0f;
+    const uint32_t b0 = __builtin_bit_cast(uint32_t, __builtin_fmaf(v0.x, id, MAGIC));
+    const uint32_t b1 = __builtin_bit_cast(uint32_t, __builtin_fmaf(v0.y, id, MAGIC));
+    const uint32_t b2 = __builtin_bit_cast(uint32_t, __builtin_fmaf(v0.z, id, MAGIC));
+    const uint32_t b3 = __builtin_bit_cast(uint32_t, __builtin_fmaf(v0.w, id, MAGIC));
+    const uint32_t b4 = __builtin_bit_cast(uint32_t, __builtin_fmaf(v1.x, id, MAGIC));
+    const uint32_t b5 = __builtin_bit_cast(uint32_t, __builtin_fmaf(v1.y, id, MAGIC));
+    const uint32_t b6 = __builtin_bit_cast(uint32_t, __builtin_fmaf(v1.z, id, MAGIC));
+    const uint32_t b7 = __builtin_bit_cast(uint32_t, __builtin_fmaf(v1.w, id, MAGIC));
+    const uint32_t w0 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(b3, b2, 0x0c0c0400u), __builtin_amdgcn_perm(b1, b0, 0x0c0c0400u), 0x05040100u);
+    const uint32_t w1 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(b7, b6, 0x0c0c0400u), __builtin_amdgcn_perm(b5, b4, 0x0c0c0400u), 0x05040100u);
+    // biased bytes (128 + q): sum(q) = udot4(bytes, 1) - 4*128 per dword
+    const int qs = (int)__builtin_amdgcn_udot4(w0, 0x01010101u, __builtin_amdgcn_udot4(w1, 0x01010101u, 0u, false), false) - 1024;
+    int s, j;
+    SlotMap<T>::place(kb * 2 + (sub >> 1), s, j);
+    const int nslots = Kpad / 64;
+    *reinterpret_cast<uint2 *>(xq + (size_t)(j * nslots + s) * 16 + (sub & 1) * 8) = make_uint2(w0 ^ 0x80808080u, w1 ^ 0x80808080u);
+    float fs = (float)qs;
+    fs += dpp_f<DPP_XOR1>(fs);              // 16-run sum (lane pairs 0-1 / 2-3)
+    if ((sub & 1) == 0) x16[kb * 2 + (sub >> 1)] = d * fs;
+    fs += dpp_f<DPP_XOR2>(fs);              // 32-block sum
+    if (sub == 0) {
+        xd[kb] = d;
+        xs[kb] = d * fs;
     }
 }
 
 // ------------------------------------------------------------------------------------------
-// per-type weight fragment: load (raw bytes of one slot of one row) and dot with a column
+// per-type weight fragment: load (raw bytes of one slot of one row) and dot with a column.
+//   X  : 16 dwords = the slot's 64 int8 activations (parts j = 0..3)
+//   dx : block scales of the slot's 32-blocks (2, or 4 for Q6_K)
+//   sx : d*sum(q): per 32-block (Q4_0, Q4_K, Q5_K) or per 16-run (Q6_K)
 // ------------------------------------------------------------------------------------------
 template <int T> struct Frag;
 
-// Q4_0: slot = blocks 2s, 2s+1 (36 contiguous bytes)
+// Q4_0: slot = blocks 2s, 2s+1 (36 contiguous bytes); sum (q-8)*x = sum q*x - 8 sum x
 template <> struct Frag<T_Q4_0> {
     uint32_t D[9];
     template <bool RAG>
@@ -145,21 +149,20 @@ template <> struct Frag<T_Q4_0> {
         }
     }
     __device__ inline void zero() { for (int i = 0; i < 9; ++i) D[i] = 0; }
-    // X: 16 dwords of int8 activations (parts 0..3), xd: d of blocks 2s, 2s+1
-    __device__ inline float dot(const uint32_t X[16], const float xd[2], const float *) const {
+    __device__ inline float dot(const uint32_t X[16], const float *dx, const float *sx) const {
         const float d0 = h2f((uint16_t)(D[0] & 0xffff));
         const float d1 = h2f((uint16_t)(D[4] >> 16));
         int s0 = 0, s1 = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t q0 = align2(D[i + 1], D[i]);      // qs of block 0 at byte 2
-            s0 = dot4(sub8_bytes(q0 & 0x0f0f0f0fu), X[i], s0);
-            s0 = dot4(sub8_bytes((q0 >> 4) & 0x0f0f0f0fu), X[4 + i], s0);
+            s0 = dot4(q0 & 0x0f0f0f0fu, X[i], s0);
+            s0 = dot4((q0 >> 4) & 0x0f0f0f0fu, X[4 + i], s0);
             const uint32_t q1 = D[5 + i];                   // qs of block 1 at byte 20
-            s1 = dot4(sub8_bytes(q1 & 0x0f0f0f0fu), X[8 + i], s1);
-            s1 = dot4(sub8_bytes((q1 >> 4) & 0x0f0f0f0fu), X[12 + i], s1);
+            s1 = dot4(q1 & 0x0f0f0f0fu, X[8 + i], s1);
+            s1 = dot4((q1 >> 4) & 0x0f0f0f0fu, X[12 + i], s1);
         }
-        return (d0 * xd[0]) * (float)s0 + (d1 * xd[1]) * (float)s1;
+        return d0 * __builtin_fmaf(dx[0], (float)s0, -8.f * sx[0]) + d1 * __builtin_fmaf(dx[1], (float)s1, -8.f * sx[1]);
     }
 };
 
@@ -181,7 +184,7 @@ template <> struct Frag<T_Q8_0> {
         }
     }
     __device__ inline void zero() { for (int i = 0; i < 17; ++i) D[i] = 0; }
-    __device__ inline float dot(const uint32_t X[16], const float xd[2], const float *) const {
+    __device__ inline float dot(const uint32_t X[16], const float *dx, const float *) const {
         const float d0 = h2f((uint16_t)(D[0] & 0xffff));
         const float d1 = h2f((uint16_t)(D[8] >> 16));
         int s0 = 0, s1 = 0;
@@ -190,7 +193,7 @@ template <> struct Frag<T_Q8_0> {
             s0 = dot4(align2(D[i + 1], D[i]), X[i], s0);
             s1 = dot4(D[9 + i], X[8 + i], s1);
         }
-        return (d0 * xd[0]) * (float)s0 + (d1 * xd[1]) * (float)s1;
+        return (d0 * dx[0]) * (float)s0 + (d1 * dx[1]) * (float)s1;
     }
 };
 
@@ -207,7 +210,7 @@ template <> struct Frag<T_Q4_K> {
         ld16(p + 32 + 32 * c, Q + 4);
     }
     __device__ inline void zero() { for (int i = 0; i < 4; ++i) H[i] = 0; for (int i = 0; i < 8; ++i) Q[i] = 0; c = 0; }
-    __device__ inline float dot(const uint32_t X[16], const float xd[2], const float xs[2]) const {
+    __device__ inline float dot(const uint32_t X[16], const float *dx, const float *sx) const {
         const float d = h2f((uint16_t)(H[0] & 0xffff)), dmin = h2f((uint16_t)(H[0] >> 16));
         const uint32_t S[3] = {H[1], H[2], H[3]};
         uint32_t sc0, sc1, m0, m1;
@@ -218,8 +221,8 @@ template <> struct Frag<T_Q4_K> {
             s0 = dot4(Q[i] & 0x0f0f0f0fu, X[i], s0);
             s1 = dot4((Q[i] >> 4) & 0x0f0f0f0fu, X[8 + i], s1);
         }
-        return d * ((float)sc0 * xd[0] * (float)s0 + (float)sc1 * xd[1] * (float)s1) -
-               dmin * ((float)m0 * xs[0] + (float)m1 * xs[1]);
+        return d * ((float)sc0 * dx[0] * (float)s0 + (float)sc1 * dx[1] * (float)s1) -
+               dmin * ((float)m0 * sx[0] + (float)m1 * sx[1]);
     }
 };
 
@@ -242,7 +245,7 @@ template <> struct Frag<T_Q5_K> {
         for (int i = 0; i < 8; ++i) QH[i] = Q[i] = 0;
         c = 0;
     }
-    __device__ inline float dot(const uint32_t X[16], const float xd[2], const float xs[2]) const {
+    __device__ inline float dot(const uint32_t X[16], const float *dx, const float *sx) const {
         const float d = h2f((uint16_t)(H[0] & 0xffff)), dmin = h2f((uint16_t)(H[0] >> 16));
         const uint32_t S[3] = {H[1], H[2], H[3]};
         uint32_t sc0, sc1, m0, m1;
@@ -255,14 +258,14 @@ template <> struct Frag<T_Q5_K> {
             s0 = dot4(lo, X[i], s0);
             s1 = dot4(hi, X[8 + i], s1);
         }
-        return d * ((float)sc0 * xd[0] * (float)s0 + (float)sc1 * xd[1] * (float)s1) -
-               dmin * ((float)m0 * xs[0] + (float)m1 * xs[1]);
+        return d * ((float)sc0 * dx[0] * (float)s0 + (float)sc1 * dx[1] * (float)s1) -
+               dmin * ((float)m0 * sx[0] + (float)m1 * sx[1]);
     }
 };
 
 // Q6_K: slot = (super-block sb = s/4, half h = (s/2)%2, part p = s%2); lane handles
 // positions 128h + 16p + 32k + [0,16) for k = 0..3, i.e. ql[64h+16p..], ql[64h+32+16p..],
-// qh[32h+16p..] and scales 8h + p + 2k.
+// qh[32h+16p..] and scales 8h + p + 2k; sum (q-32)*x = sum q*x - 32 sum x per 16-run.
 template <> struct Frag<T_Q6_K> {
     uint32_t L0[4], L1[4], QH[4], SC[2];
     uint16_t dh;
@@ -284,8 +287,8 @@ template <> struct Frag<T_Q6_K> {
         dh = 0;
         p = 0;
     }
-    // xd: d of the four 32-blocks 4h + k
-    __device__ inline float dot(const uint32_t X[16], const float xd[4], const float *) const {
+    // dx: d of the four 32-blocks 4h + k; sx: d*sum(q) of the four 16-runs
+    __device__ inline float dot(const uint32_t X[16], const float *dx, const float *sx) const {
         int s[4] = {0, 0, 0, 0};
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -293,10 +296,10 @@ template <> struct Frag<T_Q6_K> {
             const uint32_t w1 = (L1[t] & 0x0f0f0f0fu) | ((QH[t] & 0x0c0c0c0cu) << 2);
             const uint32_t w2 = ((L0[t] >> 4) & 0x0f0f0f0fu) | (QH[t] & 0x30303030u);
             const uint32_t w3 = ((L1[t] >> 4) & 0x0f0f0f0fu) | ((QH[t] & 0xc0c0c0c0u) >> 2);
-            s[0] = dot4(sub32_bytes(w0), X[t], s[0]);
-            s[1] = dot4(sub32_bytes(w1), X[4 + t], s[1]);
-            s[2] = dot4(sub32_bytes(w2), X[8 + t], s[2]);
-            s[3] = dot4(sub32_bytes(w3), X[12 + t], s[3]);
+            s[0] = dot4(w0, X[t], s[0]);
+            s[1] = dot4(w1, X[4 + t], s[1]);
+            s[2] = dot4(w2, X[8 + t], s[2]);
+            s[3] = dot4(w3, X[12 + t], s[3]);
         }
         // scales sc[8h + p + 2k]: byte (p + 2k) of the 8 loaded scale bytes
         float acc = 0.f;
@@ -304,7 +307,7 @@ template <> struct Frag<T_Q6_K> {
         for (int k = 0; k < 4; ++k) {
             const int byte = p + 2 * k;
             const int8_t sc = (int8_t)((SC[byte >> 2] >> (8 * (byte & 3))) & 0xff);
-            acc += (float)sc * xd[k] * (float)s[k];
+            acc += (float)sc * __builtin_fmaf(dx[k], (float)s[k], -32.f * sx[k]);
         }
         return h2f(dh) * acc;
     }
@@ -315,8 +318,7 @@ template <> struct XdCount<T_Q6_K> { static constexpr int n = 4; };
 
 // ------------------------------------------------------------------------------------------
 // butterfly-transpose wave reduction: V (power of two, <= 64) partial sums per lane.
-// On return lane L holds the full sum of value index (L >> (6 - log2 V)), replicated over the
-// 64/V lanes that share those high bits.
+// On return lane L holds the full sum of value index (L >> (6 - log2 V)).
 // ------------------------------------------------------------------------------------------
 template <int x> struct Log2 { static constexpr int v = 1 + Log2<x / 2>::v; };
 template <> struct Log2<1> { static constexpr int v = 0; };
@@ -366,15 +368,11 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
     constexpr int NX = XdCount<T>::n;
     constexpr int V = pow2ceil(RPW * NC);
 
-    const int blck = QT<T>::blck;
     const int Kpad = (a.K + 63) & ~63;
     const int nslots = Kpad / 64;
-    const int nblk = a.K / blck;                  // quant blocks per row
+    const int nblk = a.K / QT<T>::blck;           // quant blocks per row
     const int nxblk = Kpad / 32;
-
-    int8_t *xq = reinterpret_cast<int8_t *>(smem);
-    float *xd = reinterpret_cast<float *>(smem + (size_t)NC * Kpad);
-    float *xs = xd + NC * nxblk;
+    const XSmem sm = xsmem(smem, Kpad, NC);
 
     // ---- which matrix / columns this workgroup serves
     const uint8_t *wmat;
@@ -398,12 +396,16 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const int row0 = (blockIdx.x * MMVQ_WAVES + wave) * RPW;
+    const bool stamp = a.stamps != nullptr && threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
+    if (stamp) { a.stamps[blockIdx.x * 8 + 0] = __builtin_amdgcn_s_memrealtime(); a.stamps[blockIdx.x * 8 + 4] = __builtin_amdgcn_s_memtime(); }
 
-    // ---- activation loads first (L2/MALL hits), then the weight stream, so the quantization
-    // below waits only for the activations (vmcnt is in-order) while the weights stay in flight.
-    XRound xr;
-    const int xbase0 = threadIdx.x >> 2;
-    xround_load<NC, XA>(a, xcol0, a.nb11, nxblk, xbase0, xr);
+    // ---- activation loads of the first round first (L2/MALL hits), then the weight stream,
+    // so the quantization waits only for the activations (vmcnt is in-order) while the weights
+    // stay in flight.
+    const int kb0 = threadIdx.x >> 2;
+    float4 xa[NC], xb[NC];
+#pragma unroll
+    for (int m = 0; m < NC; ++m) xblock_load<XA>(a, xcol0 + (int64_t)m * a.nb11, kb0, xa[m], xb[m]);
 
     // Row and slot indices are clamped (not predicated) so the weight loads are straight-line
     // code: out-of-range lanes/rows read valid memory and their results are discarded.
@@ -411,18 +413,31 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
 #pragma unroll
     for (int r = 0; r < RPW; ++r) rowp[r] = wmat + (int64_t)min(row0 + r, a.N - 1) * a.nb01;
     Frag<T> f[RPW];
-    {
+    if (!(a.diag & 2)) {
         const int s0 = min(lane, nslots - 1);
 #pragma unroll
         for (int r = 0; r < RPW; ++r) f[r].template load<RAG>(rowp[r], s0, nblk);
+    } else {
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) f[r].zero();
     }
 
-    xround_store<T, NC>(nxblk, Kpad, xbase0, xr, xq, xd, xs);
-    for (int base = xbase0 + XR_STRIDE * XR_U; base < NC * nxblk; base += XR_STRIDE * XR_U) {
-        xround_load<NC, XA>(a, xcol0, a.nb11, nxblk, base, xr);
-        xround_store<T, NC>(nxblk, Kpad, base, xr, xq, xd, xs);
+    if (kb0 < nxblk) {
+#pragma unroll
+        for (int m = 0; m < NC; ++m)
+            xblock_store<T>(Kpad, kb0, xa[m], xb[m], sm.xq + (size_t)m * Kpad, sm.xd + m * nxblk, sm.xs + m * nxblk,
+                            sm.x16 + m * 2 * nxblk);
+    }
+    for (int kb = kb0 + XR_STRIDE; kb < nxblk; kb += XR_STRIDE) {
+#pragma unroll
+        for (int m = 0; m < NC; ++m) {
+            xblock_load<XA>(a, xcol0 + (int64_t)m * a.nb11, kb, xa[m], xb[m]);
+            xblock_store<T>(Kpad, kb, xa[m], xb[m], sm.xq + (size_t)m * Kpad, sm.xd + m * nxblk, sm.xs + m * nxblk,
+                            sm.x16 + m * 2 * nxblk);
+        }
     }
     __syncthreads();
+    if (stamp) a.stamps[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
 
     float acc[V];
 #pragma unroll
@@ -436,14 +451,19 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
 #pragma unroll
             for (int r = 0; r < RPW; ++r) f[r].template load<RAG>(rowp[r], s, nblk);
         }
-        // x block indices of this slot
-        int xb0;
-        if constexpr (T == T_Q6_K) xb0 = 8 * (s >> 2) + 4 * ((s >> 1) & 1);
-        else xb0 = 2 * s;
+        // x block / 16-run indices of this slot
+        int xb0, x16b;
+        if constexpr (T == T_Q6_K) {
+            xb0 = 8 * (s >> 2) + 4 * ((s >> 1) & 1);
+            x16b = 16 * (s >> 2) + 8 * ((s >> 1) & 1) + (s & 1);
+        } else {
+            xb0 = 2 * s;
+            x16b = 0;
+        }
 #pragma unroll
         for (int m = 0; m < NC; ++m) {
             uint32_t X[16];
-            const int8_t *xm = xq + (size_t)m * Kpad;
+            const int8_t *xm = sm.xq + (size_t)m * Kpad;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const uint4 t4 = *reinterpret_cast<const uint4 *>(xm + (size_t)(j * nslots + s) * 16);
@@ -451,15 +471,20 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
             }
             float dx[NX], sx[NX];
 #pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                dx[i] = xd[m * nxblk + xb0 + i];
-                sx[i] = xs[m * nxblk + xb0 + i];
+            for (int i = 0; i < NX; ++i) dx[i] = sm.xd[m * nxblk + xb0 + i];
+            if constexpr (T == T_Q6_K) {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) sx[i] = sm.x16[m * 2 * nxblk + x16b + 2 * i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) sx[i] = sm.xs[m * nxblk + xb0 + i];
             }
 #pragma unroll
             for (int r = 0; r < RPW; ++r) acc[r * NC + m] += live * f[r].dot(X, dx, sx);
         }
     }
 
+    if (stamp) a.stamps[blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memrealtime();
     const float sum = wave_reduce_transpose<V>(acc);
     constexpr int SHIFT = 6 - Log2<V>::v;
     const int idx = lane >> SHIFT;
@@ -467,6 +492,7 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
         const int r = idx / NC, m = idx % NC;
         if (row0 + r < a.N) reinterpret_cast<float *>(dcol0 + (int64_t)m * a.nb1)[row0 + r] = sum;
     }
+    if (stamp) { a.stamps[blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime(); a.stamps[blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memtime(); }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -474,11 +500,13 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
 // ------------------------------------------------------------------------------------------
 size_t mmvq_lds_bytes(int K, int nc) {
     const int Kpad = (K + 63) & ~63;
-    return (size_t)nc * Kpad + 2 * sizeof(float) * (size_t)nc * (Kpad / 32);
+    return (size_t)nc * Kpad + sizeof(float) * (size_t)nc * (Kpad / 32) * 4;   // xq + xd + xs + x16
 }
 
+int mmvq_rows_per_wg(int rpw) { return MMVQ_WAVES * rpw; }
+
 template <int T, int NC, int RPW, bool IDS, bool RAG, bool XA>
-static hipError_t launch_one(const MmArgs &a, int grid_x_rows, int grid_y, int grid_z, hipStream_t st) {
+static hipError_t launch_one(const MmArgs &a, int grid_y, int grid_z, hipStream_t st) {
     const size_t lds = mmvq_lds_bytes(a.K, NC);
     auto kern = mmvq_kernel<T, NC, RPW, IDS, RAG, XA>;
     static bool attr_set = false;   // per-instantiation
@@ -487,7 +515,7 @@ static hipError_t launch_one(const MmArgs &a, int grid_x_rows, int grid_y, int g
         attr_set = true;
     }
     const int rows_per_wg = MMVQ_WAVES * RPW;
-    dim3 grid((grid_x_rows + rows_per_wg - 1) / rows_per_wg, grid_y, grid_z);
+    dim3 grid((a.N + rows_per_wg - 1) / rows_per_wg, grid_y, grid_z);
     hipLaunchKernelGGL(kern, grid, dim3(MMVQ_THREADS), lds, st, a);
     return hipGetLastError();
 }
@@ -497,12 +525,12 @@ static hipError_t launch_flags(const MmArgs &a, int grid_y, int grid_z, hipStrea
     const bool rag = (a.K % 64) != 0;
     if constexpr (T == T_Q4_0 || T == T_Q8_0) {
         if (rag) {
-            return a.x_aligned16 ? launch_one<T, NC, RPW, IDS, true, true>(a, a.N, grid_y, grid_z, st)
-                                 : launch_one<T, NC, RPW, IDS, true, false>(a, a.N, grid_y, grid_z, st);
+            return a.x_aligned16 ? launch_one<T, NC, RPW, IDS, true, true>(a, grid_y, grid_z, st)
+                                 : launch_one<T, NC, RPW, IDS, true, false>(a, grid_y, grid_z, st);
         }
     }
-    return a.x_aligned16 ? launch_one<T, NC, RPW, IDS, false, true>(a, a.N, grid_y, grid_z, st)
-                         : launch_one<T, NC, RPW, IDS, false, false>(a, a.N, grid_y, grid_z, st);
+    return a.x_aligned16 ? launch_one<T, NC, RPW, IDS, false, true>(a, grid_y, grid_z, st)
+                         : launch_one<T, NC, RPW, IDS, false, false>(a, grid_y, grid_z, st);
 }
 
 template <int T, int RPW>
@@ -548,11 +576,11 @@ hipError_t mmvq_id_launch(int type, const MmArgs &a, int rpw, hipStream_t st) {
     const int grid_y = a.n_used * a.n_tok;
     (void)rpw;
     switch (type) {
-        case T_Q4_0: return launch_flags<T_Q4_0, 1, 2, true>(a, grid_y, 1, st);
-        case T_Q8_0: return launch_flags<T_Q8_0, 1, 2, true>(a, grid_y, 1, st);
-        case T_Q4_K: return launch_flags<T_Q4_K, 1, 2, true>(a, grid_y, 1, st);
-        case T_Q5_K: return launch_flags<T_Q5_K, 1, 2, true>(a, grid_y, 1, st);
-        case T_Q6_K: return launch_flags<T_Q6_K, 1, 2, true>(a, grid_y, 1, st);
+        case T_Q4_0: return launch_flags<T_Q4_0, 1, 1, true>(a, grid_y, 1, st);
+        case T_Q8_0: return launch_flags<T_Q8_0, 1, 1, true>(a, grid_y, 1, st);
+        case T_Q4_K: return launch_flags<T_Q4_K, 1, 1, true>(a, grid_y, 1, st);
+        case T_Q5_K: return launch_flags<T_Q5_K, 1, 1, true>(a, grid_y, 1, st);
+        case T_Q6_K: return launch_flags<T_Q6_K, 1, 1, true>(a, grid_y, 1, st);
         default: return hipErrorInvalidValue;
     }
 }

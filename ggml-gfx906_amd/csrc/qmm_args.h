@@ -29,6 +29,9 @@ struct MmArgs {
     int ne11_b;            // b->ne[1]
     int n_expert;          // as->ne[2]
     int x_aligned16;       // src1 rows / strides are 16-byte aligned
+    // diagnostics (GGML_MI355X_STAMPS): per-workgroup s_memrealtime stamps, or nullptr
+    unsigned long long *stamps;
+    int diag;              // diagnostics: bit0 = skip activation loads, bit1 = skip weight loads
 };
 
 }  // namespace mi355x

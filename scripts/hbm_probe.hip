@@ -1,0 +1,111 @@
+// scripts/hbm_probe.hip — measurement probe (not product code): how fast can one launch
+// stream B bytes from HBM on MI355X, as a function of B and the grid shape? Gives the floor
+// a GEMV of the same byte count can reach. Rotates over enough buffers to stay HBM-cold.
+//   hipcc --offload-arch=gfx950 -O3 scripts/hbm_probe.hip -o scripts/hbm_probe && scripts/hbm_probe
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                       \
+    do {                                                                            \
+        hipError_t e = (x);                                                         \
+        if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } \
+    } while (0)
+
+// each workgroup streams `per_wg` bytes with dwordx4 loads, UNROLL loads in flight per lane
+template <int UNROLL>
+__global__ void stream_read(const uint4 *__restrict__ p, size_t per_wg_vec, uint32_t *out) {
+    const uint4 *base = p + (size_t)blockIdx.x * per_wg_vec;
+    uint32_t acc = 0;
+    for (size_t i = threadIdx.x; i < per_wg_vec; i += (size_t)blockDim.x * UNROLL) {
+        uint4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const size_t j = i + (size_t)u * blockDim.x;
+            v[u] = j < per_wg_vec ? base[j] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    if (acc == 0x12345678u) out[blockIdx.x] = acc;   // keep the loads alive
+}
+
+__global__ void empty_kernel(uint32_t *out) {
+    if (threadIdx.x == 12345) out[0] = 1;
+}
+
+int main(int argc, char **argv) {
+    {
+        uint32_t *o;
+        CK(hipMalloc(&o, 64));
+        hipEvent_t a, b;
+        CK(hipEventCreate(&a));
+        CK(hipEventCreate(&b));
+        for (int th : {64, 256, 512, 1024}) {
+            for (int wgs : {256, 512, 1024, 2048, 4096}) {
+                for (int i = 0; i < 64; ++i) hipLaunchKernelGGL(empty_kernel, dim3(wgs), dim3(th), 0, 0, o);
+                CK(hipDeviceSynchronize());
+                CK(hipEventRecord(a, 0));
+                for (int i = 0; i < 512; ++i) hipLaunchKernelGGL(empty_kernel, dim3(wgs), dim3(th), 0, 0, o);
+                CK(hipEventRecord(b, 0));
+                CK(hipEventSynchronize(b));
+                float ms;
+                CK(hipEventElapsedTime(&ms, a, b));
+                printf("empty kernel threads=%4d wgs=%5d waves=%6d  back-to-back %6.2f us/launch\n", th, wgs, wgs * th / 64, ms * 1e3 / 512);
+            }
+        }
+        if (argc > 1) return 0;
+    }
+    const size_t sizes[] = {9469952 / 16 * 16, 25362432, 37748736, 100663296};
+    const int threads_opts[] = {256, 512};
+    const int wg_opts[] = {256, 512, 1024, 2048};
+    uint32_t *out;
+    CK(hipMalloc(&out, 1 << 20));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (size_t bytes : sizes) {
+        const int copies = (int)std::max<size_t>(4, (size_t)(700ull << 20) / bytes);
+        std::vector<uint4 *> bufs(copies);
+        for (auto &b : bufs) {
+            CK(hipMalloc(&b, bytes));
+            CK(hipMemset(b, 1, bytes));
+        }
+        for (int th : threads_opts) {
+            for (int wgs : wg_opts) {
+                const size_t per_wg_vec = bytes / 16 / wgs;
+                auto launch = [&](int i) {
+                    hipLaunchKernelGGL(stream_read<4>, dim3(wgs), dim3(th), 0, 0, bufs[i % copies], per_wg_vec, out);
+                };
+                for (int i = 0; i < copies; ++i) launch(i);
+                CK(hipDeviceSynchronize());
+                // per-launch duration with events around single launches (median of 64)
+                std::vector<float> ts;
+                for (int i = 0; i < 64; ++i) {
+                    CK(hipEventRecord(e0, 0));
+                    launch(i);
+                    CK(hipEventRecord(e1, 0));
+                    CK(hipEventSynchronize(e1));
+                    float ms;
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    ts.push_back(ms * 1e3f);
+                }
+                std::sort(ts.begin(), ts.end());
+                // back-to-back throughput over 256 launches
+                CK(hipEventRecord(e0, 0));
+                for (int i = 0; i < 256; ++i) launch(i);
+                CK(hipEventRecord(e1, 0));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                const double b2b_us = ms * 1e3 / 256;
+                printf("bytes=%10zu threads=%d wgs=%5d  single median %7.2f us (%6.0f GB/s)   back-to-back %7.2f us/launch (%6.0f GB/s)\n",
+                       bytes, th, wgs, ts[32], bytes / (ts[32] * 1e-6) / 1e9, b2b_us, bytes / (b2b_us * 1e-6) / 1e9);
+            }
+        }
+        for (auto &b : bufs) CK(hipFree(b));
+    }
+    return 0;
+}
