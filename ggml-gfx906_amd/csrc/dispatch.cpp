@@ -21,6 +21,8 @@ namespace mi355x {
 hipError_t mmvq_launch(int type, const MmArgs &a, int nc, int rpw, hipStream_t st);
 hipError_t mmvq_id_launch(int type, const MmArgs &a, int rpw, hipStream_t st);
 size_t mmvq_lds_bytes(int K, int nc);
+bool mmvq_has_nc(int nc);
+bool mmvq_bigk(int K);
 hipError_t dequant_launch(int type, const void *src, float *dst, int64_t n, hipStream_t st);
 hipError_t mmq_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
 bool mmq_supported(int type, const MmArgs &a);
@@ -54,9 +56,7 @@ bool is_hot_quant(int t) { return type_blck(t) != 0; }
 // matrix needs all 512 workgroups of RPW=1 to cover 256 CUs twice; batched / taller problems
 // (rows x batch) switch to 2 and 4 rows per wave.
 static int pick_rpw(int64_t rows_total) {
-    if (rows_total >= 262144) return 4;
-    if (rows_total >= 16384) return 2;
-    return 1;
+    return rows_total >= 16384 ? 2 : 1;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -115,8 +115,8 @@ static MmArgs base_args(const TensorView &a, const TensorView &b, const TensorVi
 static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st) {
     const int rpw = pick_rpw((int64_t)m.N * m.ne12 * m.ne13);
     while (ncols > 0) {
-        int nc = std::min(ncols, 8);
-        while (nc > 1 && mmvq_lds_bytes(m.K, nc) > LDS_LIMIT) --nc;
+        int nc = mmvq_bigk(m.K) ? 1 : std::min(ncols, 8);
+        while (nc > 1 && (!mmvq_has_nc(nc) || mmvq_lds_bytes(m.K, nc) > LDS_LIMIT)) --nc;
         MmArgs g = m;
         g.x = m.x + (int64_t)c0 * m.nb11;
         g.dst = m.dst + (int64_t)c0 * m.nb1;

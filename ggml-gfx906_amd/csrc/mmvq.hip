@@ -21,6 +21,8 @@
 //    sums per lane collapse to one value per lane without touching LDS.
 //
 // Templated on <type, NC columns, RPW rows per wave, IDS = MUL_MAT_ID routing, RAG, XA>.
+#include <algorithm>
+
 #include "qcommon.h"
 #include "qmm_args.h"
 
@@ -70,20 +72,24 @@ __device__ __forceinline__ XSmem xsmem(uint8_t *smem, int Kpad, int nc) {
 
 constexpr int XR_STRIDE = MMVQ_THREADS / 4;
 
+// Branch-free: the address is clamped into the row and out-of-range values are zeroed by a
+// select, so every lane issues the same loads. (A load under a branch makes the compiler's
+// in-order vmcnt bookkeeping ambiguous and it then waits for ALL outstanding loads — which
+// would include the weight stream.)
 template <bool XA>
 __device__ __forceinline__ void xblock_load(const MmArgs &a, const uint8_t *xcol, int kb, float4 &v0, float4 &v1) {
     const int k0 = kb * 32 + (threadIdx.x & 3) * 8;
-    v0 = v1 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (k0 < a.K && !(a.diag & 1)) {
-        const float *src = reinterpret_cast<const float *>(xcol) + k0;
-        if constexpr (XA) {
-            v0 = reinterpret_cast<const float4 *>(src)[0];
-            v1 = reinterpret_cast<const float4 *>(src)[1];
-        } else {
-            v0 = make_float4(src[0], src[1], src[2], src[3]);
-            v1 = make_float4(src[4], src[5], src[6], src[7]);
-        }
+    const float *src = reinterpret_cast<const float *>(xcol) + min(k0, a.K - 8);
+    if constexpr (XA) {
+        v0 = reinterpret_cast<const float4 *>(src)[0];
+        v1 = reinterpret_cast<const float4 *>(src)[1];
+    } else {
+        v0 = make_float4(src[0], src[1], src[2], src[3]);
+        v1 = make_float4(src[4], src[5], src[6], src[7]);
     }
+    const bool in = k0 < a.K;
+    v0.x = in ? v0.x : 0.f; v0.y = in ? v0.y : 0.f; v0.z = in ? v0.z : 0.f; v0.w = in ? v0.w : 0.f;
+    v1.x = in ? v1.x : 0.f; v1.y = in ? v1.y : 0.f; v1.z = in ? v1.z : 0.f; v1.w = in ? v1.w : 0.f;
 }
 
 template <int T>
@@ -270,15 +276,38 @@ template <> struct Frag<T_Q6_K> {
     uint32_t L0[4], L1[4], QH[4], SC[2];
     uint16_t dh;
     int p;
+    // a super-block starts 2-byte aligned when sb is odd; 2-byte-misaligned 16-B loads stream
+    // ~16 % slower on MI355X (scripts/hbm_probe.hip), 4-byte aligned ones at full rate, so
+    // every piece is loaded from its 4-byte-aligned floor and funnel-shifted into place.
+    __device__ static inline void ld16_a4(const uint8_t *p, uint32_t *o) {
+        const uintptr_t ip = reinterpret_cast<uintptr_t>(p);
+        const uint8_t *pa = reinterpret_cast<const uint8_t *>(ip & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(ip & 3);
+        const uint4 w = *reinterpret_cast<const uint4 *>(pa);    // 4-B aligned dwordx4
+        const uint32_t w4 = *reinterpret_cast<const uint32_t *>(pa + 16);
+        o[0] = __builtin_amdgcn_alignbyte(w.y, w.x, sh);
+        o[1] = __builtin_amdgcn_alignbyte(w.z, w.y, sh);
+        o[2] = __builtin_amdgcn_alignbyte(w.w, w.z, sh);
+        o[3] = __builtin_amdgcn_alignbyte(w4, w.w, sh);
+    }
     template <bool RAG>
     __device__ inline void load(const uint8_t *row, int s, int) {
         const uint8_t *b = row + (size_t)(s >> 2) * 210;
         const int h = (s >> 1) & 1;
         p = s & 1;
-        ld16(b + 64 * h + 16 * p, L0);
-        ld16(b + 64 * h + 32 + 16 * p, L1);
-        ld16(b + 128 + 32 * h + 16 * p, QH);
-        ld8(b + 192 + 8 * h, SC);
+        ld16_a4(b + 64 * h + 16 * p, L0);
+        ld16_a4(b + 64 * h + 32 + 16 * p, L1);
+        ld16_a4(b + 128 + 32 * h + 16 * p, QH);
+        {
+            const uintptr_t ip = reinterpret_cast<uintptr_t>(b + 192 + 8 * h);
+            const uint8_t *pa = reinterpret_cast<const uint8_t *>(ip & ~(uintptr_t)3);
+            const uint32_t sh = (uint32_t)(ip & 3);
+            const uint2 w = *reinterpret_cast<const uint2 *>(pa);
+            uint32_t w2 = 0;
+            if (sh) w2 = *reinterpret_cast<const uint32_t *>(pa + 8);   // never past the block end
+            SC[0] = __builtin_amdgcn_alignbyte(w.y, w.x, sh);
+            SC[1] = __builtin_amdgcn_alignbyte(w2, w.y, sh);
+        }
         dh = ld2(b + 208);
     }
     __device__ inline void zero() {
@@ -361,12 +390,20 @@ __device__ inline float wave_reduce_transpose(float (&v)[V]) {
 // the kernel
 //   RAG : K % 64 == 32 (only possible for the 32-block types): last slot holds one block
 //   XA  : src1 rows and strides are 16-byte aligned (float4 activation loads)
+//
+// Work: blockIdx.y selects the matrix / column group (batch entry, or (expert, token) for
+// MUL_MAT_ID); the workgroup quantizes that column group into LDS ONCE, then walks row groups
+// g = blockIdx.x, blockIdx.x + gridDim.x, ... (8 waves x RPW rows each). Each unit of work
+// = (row group, 64-slot iteration of K); the weights of unit u+1 are in flight while unit u
+// is computed (two register buffers), so a workgroup keeps HBM busy across its whole life and
+// the activation quantization is amortized over every row it covers.
 // ------------------------------------------------------------------------------------------
-template <int T, int NC, int RPW, bool IDS, bool RAG, bool XA>
+template <int T, int NC, int RPW, bool IDS, bool RAG, bool XA, bool BIGK>
 __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr int NX = XdCount<T>::n;
     constexpr int V = pow2ceil(RPW * NC);
+    constexpr int ROWS_PER_GROUP = MMVQ_WAVES * RPW;
 
     const int Kpad = (a.K + 63) & ~63;
     const int nslots = Kpad / 64;
@@ -395,45 +432,58 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
 
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const int row0 = (blockIdx.x * MMVQ_WAVES + wave) * RPW;
+    const int n_groups = (a.N + ROWS_PER_GROUP - 1) / ROWS_PER_GROUP;
+    const int n_it = (nslots + WAVE - 1) / WAVE;
+    const int my_groups = (n_groups - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int n_units = my_groups * n_it;
     const bool stamp = a.stamps != nullptr && threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
     if (stamp) { a.stamps[blockIdx.x * 8 + 0] = __builtin_amdgcn_s_memrealtime(); a.stamps[blockIdx.x * 8 + 4] = __builtin_amdgcn_s_memtime(); }
 
-    // ---- activation loads of the first round first (L2/MALL hits), then the weight stream,
-    // so the quantization waits only for the activations (vmcnt is in-order) while the weights
-    // stay in flight.
+    // unit u -> first row of this wave and K slot of this lane (slot clamped: straight-line
+    // loads; dead lanes / rows read valid memory and are masked out of the sums)
+    auto unit_row0 = [&](int u) { return ((int)blockIdx.x + (u / n_it) * (int)gridDim.x) * ROWS_PER_GROUP + wave * RPW; };
+    auto unit_slot = [&](int u) { return lane + (u % n_it) * WAVE; };
+    auto load_unit = [&](Frag<T> (&f)[RPW], int u) {
+        const int r0 = unit_row0(u);
+        const int s = min(unit_slot(u), nslots - 1);
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) f[r].template load<RAG>(wmat + (int64_t)min(r0 + r, a.N - 1) * a.nb01, s, nblk);
+    };
+
+    // ---- activation loads of the first round first (L2/MALL hits), then the weight stream of
+    // unit 0, so the quantization waits only for the activations (vmcnt is in-order) while the
+    // weights stay in flight.
+    // up to two rounds (K <= 8192) are preloaded; BIGK kernels loop over the rest
     const int kb0 = threadIdx.x >> 2;
-    float4 xa[NC], xb[NC];
+    constexpr int PRE = BIGK ? 1 : 2;
+    float4 xa[NC][PRE], xb[NC][PRE];
 #pragma unroll
-    for (int m = 0; m < NC; ++m) xblock_load<XA>(a, xcol0 + (int64_t)m * a.nb11, kb0, xa[m], xb[m]);
+    for (int m = 0; m < NC; ++m)
+#pragma unroll
+        for (int r = 0; r < PRE; ++r) xblock_load<XA>(a, xcol0 + (int64_t)m * a.nb11, kb0 + r * XR_STRIDE, xa[m][r], xb[m][r]);
 
-    // Row and slot indices are clamped (not predicated) so the weight loads are straight-line
-    // code: out-of-range lanes/rows read valid memory and their results are discarded.
-    const uint8_t *rowp[RPW];
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) rowp[r] = wmat + (int64_t)min(row0 + r, a.N - 1) * a.nb01;
-    Frag<T> f[RPW];
-    if (!(a.diag & 2)) {
-        const int s0 = min(lane, nslots - 1);
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) f[r].template load<RAG>(rowp[r], s0, nblk);
-    } else {
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) f[r].zero();
-    }
+    Frag<T> fa[RPW], fb[RPW];
+    load_unit(fa, 0);
+    __builtin_amdgcn_sched_barrier(0);
 
-    if (kb0 < nxblk) {
 #pragma unroll
-        for (int m = 0; m < NC; ++m)
-            xblock_store<T>(Kpad, kb0, xa[m], xb[m], sm.xq + (size_t)m * Kpad, sm.xd + m * nxblk, sm.xs + m * nxblk,
-                            sm.x16 + m * 2 * nxblk);
+    for (int r = 0; r < PRE; ++r) {
+        const int kb = kb0 + r * XR_STRIDE;
+        if (kb < nxblk) {
+#pragma unroll
+            for (int m = 0; m < NC; ++m)
+                xblock_store<T>(Kpad, kb, xa[m][r], xb[m][r], sm.xq + (size_t)m * Kpad, sm.xd + m * nxblk,
+                                sm.xs + m * nxblk, sm.x16 + m * 2 * nxblk);
+        }
     }
-    for (int kb = kb0 + XR_STRIDE; kb < nxblk; kb += XR_STRIDE) {
+    if constexpr (BIGK) {
+        for (int kb = kb0 + XR_STRIDE; kb < nxblk; kb += XR_STRIDE) {
 #pragma unroll
-        for (int m = 0; m < NC; ++m) {
-            xblock_load<XA>(a, xcol0 + (int64_t)m * a.nb11, kb, xa[m], xb[m]);
-            xblock_store<T>(Kpad, kb, xa[m], xb[m], sm.xq + (size_t)m * Kpad, sm.xd + m * nxblk, sm.xs + m * nxblk,
-                            sm.x16 + m * 2 * nxblk);
+            for (int m = 0; m < NC; ++m) {
+                xblock_load<XA>(a, xcol0 + (int64_t)m * a.nb11, kb, xa[m][0], xb[m][0]);
+                xblock_store<T>(Kpad, kb, xa[m][0], xb[m][0], sm.xq + (size_t)m * Kpad, sm.xd + m * nxblk,
+                                sm.xs + m * nxblk, sm.x16 + m * 2 * nxblk);
+            }
         }
     }
     __syncthreads();
@@ -443,15 +493,10 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
 #pragma unroll
     for (int i = 0; i < V; ++i) acc[i] = 0.f;
 
-    for (int it = 0; it * WAVE < nslots; ++it) {
-        const int s_raw = lane + it * WAVE;
+    auto compute_unit = [&](const Frag<T> (&f)[RPW], int u) {
+        const int s_raw = unit_slot(u);
         const int s = min(s_raw, nslots - 1);
         const float live = s_raw < nslots ? 1.f : 0.f;
-        if (it > 0) {
-#pragma unroll
-            for (int r = 0; r < RPW; ++r) f[r].template load<RAG>(rowp[r], s, nblk);
-        }
-        // x block / 16-run indices of this slot
         int xb0, x16b;
         if constexpr (T == T_Q6_K) {
             xb0 = 8 * (s >> 2) + 4 * ((s >> 1) & 1);
@@ -482,17 +527,35 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
 #pragma unroll
             for (int r = 0; r < RPW; ++r) acc[r * NC + m] += live * f[r].dot(X, dx, sx);
         }
-    }
+        // last K iteration of this row group: reduce across the wave and store
+        if (u % n_it == n_it - 1) {
+            const float sum = wave_reduce_transpose<V>(acc);
+            constexpr int SHIFT = 6 - Log2<V>::v;
+            const int idx = lane >> SHIFT;
+            const int r0 = unit_row0(u);
+            if ((lane & ((1 << SHIFT) - 1)) == 0 && idx < RPW * NC) {
+                const int r = idx / NC, m = idx % NC;
+                if (r0 + r < a.N) reinterpret_cast<float *>(dcol0 + (int64_t)m * a.nb1)[r0 + r] = sum;
+            }
+#pragma unroll
+            for (int i = 0; i < V; ++i) acc[i] = 0.f;
+        }
+    };
 
-    if (stamp) a.stamps[blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memrealtime();
-    const float sum = wave_reduce_transpose<V>(acc);
-    constexpr int SHIFT = 6 - Log2<V>::v;
-    const int idx = lane >> SHIFT;
-    if ((lane & ((1 << SHIFT) - 1)) == 0 && idx < RPW * NC) {
-        const int r = idx / NC, m = idx % NC;
-        if (row0 + r < a.N) reinterpret_cast<float *>(dcol0 + (int64_t)m * a.nb1)[row0 + r] = sum;
+    // prefetches are unconditional (clamped to the last unit: a repeat of addresses already
+    // in flight, served on-chip) so the load stream never sits under a branch
+    // sched_barrier pins each prefetch ahead of the compute that follows it (left alone, the
+    // scheduler sinks the loads below the compute to save registers and the overlap is lost)
+    for (int u = 0; u < n_units; u += 2) {
+        load_unit(fb, min(u + 1, n_units - 1));
+        __builtin_amdgcn_sched_barrier(0);
+        compute_unit(fa, u);
+        if (u + 1 >= n_units) break;
+        load_unit(fa, min(u + 2, n_units - 1));
+        __builtin_amdgcn_sched_barrier(0);
+        compute_unit(fb, u + 1);
     }
-    if (stamp) { a.stamps[blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime(); a.stamps[blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memtime(); }
+    if (stamp) { a.stamps[blockIdx.x * 8 + 2] = a.stamps[blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime(); a.stamps[blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memtime(); }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -505,32 +568,51 @@ size_t mmvq_lds_bytes(int K, int nc) {
 
 int mmvq_rows_per_wg(int rpw) { return MMVQ_WAVES * rpw; }
 
-template <int T, int NC, int RPW, bool IDS, bool RAG, bool XA>
+constexpr int64_t MMVQ_TARGET_WGS = 1024;
+
+template <int T, int NC, int RPW, bool IDS, bool RAG, bool XA, bool BIGK>
 static hipError_t launch_one(const MmArgs &a, int grid_y, int grid_z, hipStream_t st) {
     const size_t lds = mmvq_lds_bytes(a.K, NC);
-    auto kern = mmvq_kernel<T, NC, RPW, IDS, RAG, XA>;
+    auto kern = mmvq_kernel<T, NC, RPW, IDS, RAG, XA, BIGK>;
     static bool attr_set = false;   // per-instantiation
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    const int rows_per_wg = MMVQ_WAVES * RPW;
-    dim3 grid((a.N + rows_per_wg - 1) / rows_per_wg, grid_y, grid_z);
+    const int rows_per_group = MMVQ_WAVES * RPW;
+    const int n_groups = (a.N + rows_per_group - 1) / rows_per_group;
+    // enough workgroups to fill 256 CUs ~4 deep; beyond that each workgroup walks more groups
+    const int64_t others = (int64_t)grid_y * grid_z;
+    const int want = (int)std::max<int64_t>(1, (MMVQ_TARGET_WGS + others - 1) / others);
+    dim3 grid(std::min(n_groups, want), grid_y, grid_z);
     hipLaunchKernelGGL(kern, grid, dim3(MMVQ_THREADS), lds, st, a);
     return hipGetLastError();
 }
 
+// K > 8192 (activations need more than two preloaded quantization rounds)
+static bool is_bigk(const MmArgs &a) { return ((a.K + 63) & ~63) / 32 > 2 * XR_STRIDE; }
+
 template <int T, int NC, int RPW, bool IDS>
 static hipError_t launch_flags(const MmArgs &a, int grid_y, int grid_z, hipStream_t st) {
     const bool rag = (a.K % 64) != 0;
+    if (is_bigk(a)) {
+        if constexpr (NC == 1) {
+            if constexpr (T == T_Q4_0 || T == T_Q8_0) {
+                if (rag) return launch_one<T, 1, RPW, IDS, true, false, true>(a, grid_y, grid_z, st);
+            }
+            return a.x_aligned16 ? launch_one<T, 1, RPW, IDS, false, true, true>(a, grid_y, grid_z, st)
+                                 : launch_one<T, 1, RPW, IDS, false, false, true>(a, grid_y, grid_z, st);
+        }
+        return hipErrorInvalidValue;   // host splits big-K launches into single columns
+    }
     if constexpr (T == T_Q4_0 || T == T_Q8_0) {
         if (rag) {
-            return a.x_aligned16 ? launch_one<T, NC, RPW, IDS, true, true>(a, grid_y, grid_z, st)
-                                 : launch_one<T, NC, RPW, IDS, true, false>(a, grid_y, grid_z, st);
+            return a.x_aligned16 ? launch_one<T, NC, RPW, IDS, true, true, false>(a, grid_y, grid_z, st)
+                                 : launch_one<T, NC, RPW, IDS, true, false, false>(a, grid_y, grid_z, st);
         }
     }
-    return a.x_aligned16 ? launch_one<T, NC, RPW, IDS, false, true>(a, grid_y, grid_z, st)
-                         : launch_one<T, NC, RPW, IDS, false, false>(a, grid_y, grid_z, st);
+    return a.x_aligned16 ? launch_one<T, NC, RPW, IDS, false, true, false>(a, grid_y, grid_z, st)
+                         : launch_one<T, NC, RPW, IDS, false, false, false>(a, grid_y, grid_z, st);
 }
 
 template <int T, int RPW>
@@ -540,9 +622,6 @@ static hipError_t launch_nc(const MmArgs &a, int nc, int grid_y, int grid_z, hip
         case 2: return launch_flags<T, 2, RPW, false>(a, grid_y, grid_z, st);
         case 3: return launch_flags<T, 3, RPW, false>(a, grid_y, grid_z, st);
         case 4: return launch_flags<T, 4, RPW, false>(a, grid_y, grid_z, st);
-        case 5: return launch_flags<T, 5, RPW, false>(a, grid_y, grid_z, st);
-        case 6: return launch_flags<T, 6, RPW, false>(a, grid_y, grid_z, st);
-        case 7: return launch_flags<T, 7, RPW, false>(a, grid_y, grid_z, st);
         case 8: return launch_flags<T, 8, RPW, false>(a, grid_y, grid_z, st);
         default: return hipErrorInvalidValue;
     }
@@ -550,12 +629,13 @@ static hipError_t launch_nc(const MmArgs &a, int nc, int grid_y, int grid_z, hip
 
 template <int T>
 static hipError_t launch_type(const MmArgs &a, int nc, int grid_y, int grid_z, int rpw, hipStream_t st) {
-    switch (rpw) {
-        case 1: return launch_nc<T, 1>(a, nc, grid_y, grid_z, st);
-        case 2: return launch_nc<T, 2>(a, nc, grid_y, grid_z, st);
-        default: return launch_nc<T, 4>(a, nc, grid_y, grid_z, st);
-    }
+    if (rpw <= 1) return launch_nc<T, 1>(a, nc, grid_y, grid_z, st);
+    return launch_nc<T, 2>(a, nc, grid_y, grid_z, st);
 }
+
+// column-group widths that have kernels (dispatch.cpp splits M into these)
+bool mmvq_has_nc(int nc) { return nc == 1 || nc == 2 || nc == 3 || nc == 4 || nc == 8; }
+bool mmvq_bigk(int K) { MmArgs a{}; a.K = K; return is_bigk(a); }
 
 // plain MUL_MAT: a.M columns in groups of nc (a.M % nc == 0)
 hipError_t mmvq_launch(int type, const MmArgs &a, int nc, int rpw, hipStream_t st) {

@@ -32,6 +32,26 @@ __global__ void stream_read(const uint4 *__restrict__ p, size_t per_wg_vec, uint
     if (acc == 0x12345678u) out[blockIdx.x] = acc;   // keep the loads alive
 }
 
+struct __attribute__((packed, aligned(2))) u4a2 { uint32_t v[4]; };
+
+// same stream, but every 16-byte load is shifted by `off` bytes (2 = Q6_K-like misalignment)
+__global__ void stream_read_off(const uint8_t *__restrict__ p, size_t per_wg_vec, int off, uint32_t *out) {
+    const uint8_t *base = p + (size_t)blockIdx.x * per_wg_vec * 16 + off;
+    uint32_t acc = 0;
+    for (size_t i = threadIdx.x; i < per_wg_vec - 1; i += (size_t)blockDim.x * 4) {
+        u4a2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const size_t j = i + (size_t)u * blockDim.x;
+            if (j < per_wg_vec - 1) v[u] = *reinterpret_cast<const u4a2 *>(base + j * 16);
+            else v[u] = u4a2{{0, 0, 0, 0}};
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc ^= v[u].v[0] ^ v[u].v[1] ^ v[u].v[2] ^ v[u].v[3];
+    }
+    if (acc == 0x12345678u) out[blockIdx.x] = acc;
+}
+
 __global__ void empty_kernel(uint32_t *out) {
     if (threadIdx.x == 12345) out[0] = 1;
 }
@@ -56,7 +76,32 @@ int main(int argc, char **argv) {
                 printf("empty kernel threads=%4d wgs=%5d waves=%6d  back-to-back %6.2f us/launch\n", th, wgs, wgs * th / 64, ms * 1e3 / 512);
             }
         }
-        if (argc > 1) return 0;
+        if (argc > 1 && argv[1][0] == 'e') return 0;
+    }
+    if (argc > 1 && argv[1][0] == 'a') {
+        const size_t bytes = 603979776;   // 576 MiB
+        uint8_t *buf;
+        uint32_t *o;
+        CK(hipMalloc(&buf, bytes + 64));
+        CK(hipMalloc(&o, 1 << 20));
+        CK(hipMemset(buf, 1, bytes + 64));
+        hipEvent_t a, b;
+        CK(hipEventCreate(&a));
+        CK(hipEventCreate(&b));
+        for (int off : {0, 2, 4, 8, 0}) {
+            const int wgs = 4096;
+            const size_t per = bytes / 16 / wgs;
+            hipLaunchKernelGGL(stream_read_off, dim3(wgs), dim3(256), 0, 0, buf, per, off, o);
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(a, 0));
+            for (int i = 0; i < 10; ++i) hipLaunchKernelGGL(stream_read_off, dim3(wgs), dim3(256), 0, 0, buf, per, off, o);
+            CK(hipEventRecord(b, 0));
+            CK(hipEventSynchronize(b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            printf("576 MiB stream, 16-B loads at offset %d: %.0f GB/s\n", off, bytes * 10 / (ms * 1e-3) / 1e9);
+        }
+        return 0;
     }
     const size_t sizes[] = {9469952 / 16 * 16, 25362432, 37748736, 100663296};
     const int threads_opts[] = {256, 512};

@@ -24,18 +24,19 @@ t = {v: k for k, v in M.NAMES.items()}[tname]
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 N = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
 Mc = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+BATCH = int(sys.argv[5]) if len(sys.argv) > 5 else 1
 
 L = M.lib()
 L.ggml_mi355x_debug_stamps.argtypes = [C.c_void_p, C.c_size_t]
-g = bench.GemvSet(torch, t, K, N, Mc, 64)
-g.sweep()
+g = bench.MatVecSet(torch, t, K, N, Mc, BATCH, 64 if BATCH == 1 else 2)
+g.launch(0)
 torch.cuda.synchronize()
-rows_per_wg = 8 * (4 if N >= 65536 else 2 if N >= 8192 else 1)
-nwg = (N + rows_per_wg - 1) // rows_per_wg
+rows_per_wg = 8 * (2 if N * BATCH >= 16384 else 1)
+nwg = min((N + rows_per_wg - 1) // rows_per_wg, max(1, (1024 + BATCH - 1) // BATCH))
 buf = np.zeros(8 * nwg, np.uint64)
 spans, xs, ds, es, starts, clk = [], [], [], [], [], []
 for i in range(16):
-    for j in range(63):          # keep the GPU busy: measure a launch inside a back-to-back run
+    for j in range(63 if BATCH == 1 else 3):   # measure a launch inside a back-to-back run
         g.launch(i + j)
     torch.cuda.synchronize()
     L.ggml_mi355x_debug_stamps(buf.ctypes.data, buf.size)
@@ -47,8 +48,8 @@ for i in range(16):
     xs.append(np.median((s[:, 1] - s[:, 0]) * 10))
     ds.append(np.median((s[:, 2] - s[:, 1]) * 10))
     es.append(np.median((s[:, 3] - s[:, 2]) * 10))
-print(f"{tname} K={K} N={N} M={Mc}: workgroups={nwg}")
+print(f"{tname} K={K} N={N} M={Mc} batch={BATCH}: workgroups(x)={nwg}")
 print(f"  kernel span (first start -> last end) ns: median {np.median(spans):.0f}  min {np.min(spans):.0f}")
 print(f"  start offsets ns (median, max over WGs): {np.median(starts, axis=0)}")
 print(f"  shader clock during the workgroup (memtime/realtime): {np.median(clk):.2f} GHz")
-print(f"  per-WG median ns: start->x_ready {np.median(xs):.0f}  x_ready->dots_done {np.median(ds):.0f}  dots_done->end {np.median(es):.0f}")
+print(f"  per-WG median ns: start->x_ready {np.median(xs):.0f}  x_ready->end {np.median(ds):.0f}")
