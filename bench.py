@@ -138,6 +138,16 @@ def config_row(s: MatVecSet, us: float) -> dict:
             "TFLOP/s": round(tf, 3)}
 
 
+def measured_traffic(key: str):
+    """HBM bytes per launch from the committed rocprofv3 --pmc FETCH_SIZE run (profiles/traffic.json),
+    corrected as MI355X_MICROARCH.md prescribes; None when absent."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+            return json.load(f)[key]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_baseline(seconds: float) -> dict:
     """Reference ggml-cpu (oracle/_ref) on the host cores, bounded sample of the same config."""
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
@@ -268,7 +278,9 @@ def main() -> None:
                        "matrices_per_step": BATCH, "weight_bytes_per_step": g.bytes,
                        "parallelism": f"independent weight stacks per GPU x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": measured_traffic("q4_0_4096x4096_m1_b64") if BATCH == 64 else None,
+                         "traffic_source": "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE, x2 gfx950 correction)",
                          "launch_us": round(kernel_us, 3), "alg_bytes_per_launch": g.bytes,
                          "frac_of_measured_copy_bw": round(achieved / HBM_MEASURED_GBS, 4)},
             "cpu_baseline": cpu,

@@ -29,7 +29,9 @@ for step in "$@"; do
         tbo)   run tbo 900 env GGML_BACKEND_PATH=$PWD/ggml-gfx906_amd/libggml-hip-mi355x.so ./oracle/_ref/test-backend-ops test -o MUL_MAT -b MI355X0 ;;
         tboid) run tboid 900 env GGML_BACKEND_PATH=$PWD/ggml-gfx906_amd/libggml-hip-mi355x.so ./oracle/_ref/test-backend-ops test -o MUL_MAT_ID -b MI355X0 ;;
         bench) run bench 600 python bench.py ;;
-        prof)  run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python bench.py --no-extra --cpu-seconds 1 ;;
+        prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --no-extra --cpu-seconds 1 ;;
+        pmc)   run pmc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/pmc -o pmc -- python bench.py --no-extra --cpu-seconds 1 --steps 5 --warmup 1 ;;
+        pmcw)  run pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/pmcw -o pmcw -- python bench.py --no-extra --cpu-seconds 1 --steps 5 --warmup 1 ;;
         *) echo "unknown step $step" ;;
     esac
 done
