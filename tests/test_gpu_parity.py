@@ -137,3 +137,62 @@ def test_rejects_bad_shapes(mm):
     D = mm.tensor(qref.F32, d.data_ptr(), [4, 2, 1, 1], qref.contiguous_nb(qref.F32, [4, 2]))
     with pytest.raises(mm.Mi355xError):
         mm.mul_mat(A, B, D)
+
+
+# ------------------------------------------------------------------------------------------
+# mat-mat (ne11 > 8) path: MFMA tiles of 64 weight rows x 128 tokens x 64 K
+# ------------------------------------------------------------------------------------------
+MMQ_SHAPES = [  # (N, M, K-multiplier) around the tile edges
+    (37, 9, 1), (64, 127, 2), (65, 128, 1), (200, 129, 2), (128, 300, 3),
+]
+
+
+@pytest.mark.parametrize("t", qref.HOT_TYPES, ids=lambda t: qref.NAMES[t])
+@pytest.mark.parametrize("shape", MMQ_SHAPES, ids=lambda s: f"n{s[0]}_m{s[1]}_k{s[2]}")
+def test_mmq_tile_edges(mm, t, shape):
+    N, M_, km = shape
+    K = (96 if qref.BLCK[t] == 32 else 256) * km   # K % 64 == 32 for the 32-block types
+    w = qref.quantize(t, qref.fill_uniform(N * K, 21), n_per_row=K)
+    x = qref.fill_uniform(M_ * K, 22)
+    a = G.Operand(t, w, [K, N, 1, 1], qref.contiguous_nb(t, [K, N, 1, 1]))
+    b = G.Operand(qref.F32, x, [K, M_, 1, 1], qref.contiguous_nb(qref.F32, [K, M_, 1, 1]))
+    out_ne = [N, M_, 1, 1]
+    got = run_mul_mat(mm, a, b, out_ne)
+    assert qref.nmse(got, G.oracle_mul_mat(a, b, out_ne)) <= 5e-4
+
+
+@pytest.mark.parametrize("t", [qref.Q4_0, qref.Q6_K], ids=lambda t: qref.NAMES[t])
+def test_mmq_broadcast_and_strided_rows(mm, t):
+    """weights [K,N,2,1] broadcast over activations [K,M,4,3] whose rows are padded (nb11 > 4K)."""
+    K, N, M_ = 512, 96, 40
+    w = qref.quantize(t, qref.fill_uniform(N * K * 2, 31), n_per_row=K)
+    pad = 24
+    xs = qref.fill_uniform((K + pad) * M_ * 12, 32)
+    a = G.Operand(t, w, [K, N, 2, 1], qref.contiguous_nb(t, [K, N, 2, 1]))
+    nb1 = 4 * (K + pad)
+    b = G.Operand(qref.F32, xs, [K, M_, 4, 3], [4, nb1, nb1 * M_, nb1 * M_ * 4])
+    out_ne = [N, M_, 4, 3]
+    got = run_mul_mat(mm, a, b, out_ne)
+    assert qref.nmse(got, G.oracle_mul_mat(a, b, out_ne)) <= 5e-4
+
+
+@pytest.mark.parametrize("scale", [1e-6, 3e4, 1e7])
+def test_mmq_activation_range(mm, scale):
+    """activations far outside the f16 range go through the per-token power-of-two prescale.
+
+    Checked against the exact product (bit-exact dequantized weights x activations in float64):
+    at these magnitudes the reference's own Q8_0 activation blocks underflow / overflow their fp16
+    scale (d = amax/127 stored as fp16), so ggml-cpu is not a usable oracle here.
+    """
+    t, K, N, M_ = qref.Q8_0, 256, 64, 33
+    w = qref.quantize(t, qref.fill_uniform(N * K, 41), n_per_row=K)
+    x = (qref.fill_uniform(M_ * K, 42) * np.float32(scale)).astype(np.float32)
+    x[5 * K + 7] *= 50.0          # one outlier token
+    a = G.Operand(t, w, [K, N, 1, 1], qref.contiguous_nb(t, [K, N, 1, 1]))
+    b = G.Operand(qref.F32, x, [K, M_, 1, 1], qref.contiguous_nb(qref.F32, [K, M_, 1, 1]))
+    out_ne = [N, M_, 1, 1]
+    got = run_mul_mat(mm, a, b, out_ne)
+    assert np.all(np.isfinite(got))
+    wf = qref.dequantize(t, w, N * K).reshape(N, K).astype(np.float64)
+    exact = (x.reshape(M_, K).astype(np.float64) @ wf.T).reshape(-1)
+    assert qref.nmse(got.astype(np.float64), exact) <= 1e-5
