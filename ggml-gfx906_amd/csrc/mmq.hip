@@ -34,7 +34,7 @@ typedef float float16v __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // SROA-friendly 16-B register
 
 constexpr int MQ_BK = 64;        // K per step = one 128-B LDS row of f16
-constexpr int MQ_THREADS = 256;
+constexpr int MQ_THREADS = 512;
 
 __device__ __forceinline__ h2v as_h2(uint32_t u) { return __builtin_bit_cast(h2v, u); }
 __device__ __forceinline__ uint32_t as_u(h2v v) { return __builtin_bit_cast(uint32_t, v); }
@@ -59,144 +59,153 @@ __device__ __forceinline__ void bytes_f16(uint32_t b, uint32_t &lo, uint32_t &hi
     hi = __builtin_amdgcn_perm(0x64646464u, b, 0x04030402u);
 }
 
-// 16 byte codes in c[4] -> 16 f16 weights (c - bias) * d, packed in o[8]; one rounding
-template <int BIAS>
-__device__ __forceinline__ void emit_scaled(const uint32_t c[4], h2v d, uint32_t o[8]) {
-    const h2v bias = splat_h2(1024.f + BIAS);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        uint32_t lo, hi;
-        bytes_f16(c[i], lo, hi);
-        o[2 * i] = as_u((as_h2(lo) - bias) * d);
-        o[2 * i + 1] = as_u((as_h2(hi) - bias) * d);
-    }
-}
-
-// 16 byte codes -> c * d1 - m1 (affine K-quant form)
-__device__ __forceinline__ void emit_affine(const uint32_t c[4], h2v d1, h2v m1, uint32_t o[8]) {
-    const h2v bias = splat_h2(1024.f);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        uint32_t lo, hi;
-        bytes_f16(c[i], lo, hi);
-        o[2 * i] = as_u(__builtin_elementwise_fma(as_h2(lo) - bias, d1, -m1));
-        o[2 * i + 1] = as_u(__builtin_elementwise_fma(as_h2(hi) - bias, d1, -m1));
-    }
-}
-
 // ------------------------------------------------------------------------------------------
-// 16-weight dequant units: raw registers loaded ahead (load), decoded at LDS-store time (emit).
+// 8-weight dequant units: raw registers loaded ahead through a buffer resource (32-bit offsets,
+// out-of-range reads return zero), decoded at LDS-store time (emit -> one 16-B f16 chunk).
 // Formulas restate src/ggml-quants.c dequantize_row_* (:307, :401, :1352, :1554, :1762).
 // ------------------------------------------------------------------------------------------
-template <int T> struct Deq16;
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void pin(u32x2 &v) { asm volatile("" : "+v"(v)); }
 
-template <> struct Deq16<T_Q4_0> {
-    uint32_t q[4], d;
+__device__ __forceinline__ u32x4 bl128(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+__device__ __forceinline__ u32x2 bl64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+}
+__device__ __forceinline__ uint32_t bl16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+}
+__device__ __forceinline__ uint32_t bl8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+}
+
+// 8 byte codes (2 dwords) -> 8 f16 weights (c - bias) * d; one rounding of the exact product
+template <int BIAS>
+__device__ __forceinline__ u32x4 emit8_scaled(uint32_t c0, uint32_t c1, h2v d) {
+    const h2v bias = splat_h2(1024.f + BIAS);
+    uint32_t l0, h0, l1, h1;
+    bytes_f16(c0, l0, h0);
+    bytes_f16(c1, l1, h1);
+    return u32x4{as_u((as_h2(l0) - bias) * d), as_u((as_h2(h0) - bias) * d), as_u((as_h2(l1) - bias) * d),
+                 as_u((as_h2(h1) - bias) * d)};
+}
+// 8 byte codes -> c * d1 - m1 (K-quant affine form)
+__device__ __forceinline__ u32x4 emit8_affine(uint32_t c0, uint32_t c1, h2v d1, h2v m1) {
+    const h2v bias = splat_h2(1024.f);
+    uint32_t l0, h0, l1, h1;
+    bytes_f16(c0, l0, h0);
+    bytes_f16(c1, l1, h1);
+    auto f = [&](uint32_t v) { return as_u(__builtin_elementwise_fma(as_h2(v) - bias, d1, -m1)); };
+    return u32x4{f(l0), f(h0), f(l1), f(h1)};
+}
+
+template <int T> struct Deq8;
+
+template <> struct Deq8<T_Q4_0> {
+    u32x2 q;
+    uint32_t d;
     int sh;
-    __device__ __forceinline__ void pin_all() { pin(q); pin(d); }
-    __device__ __forceinline__ void load(const uint8_t *row, int k0) {
-        const uint8_t *b = row + (k0 >> 5) * 18;
-        d = ld2(b);
-        ld16(b + 2, q);
+    __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, uint32_t row, int k0) {
+        const uint32_t b = row + (uint32_t)(k0 >> 5) * 18;
+        d = bl16(r, b);
+        q = bl64(r, b + 2 + (k0 & 15));
         sh = (k0 & 16) ? 4 : 0;
     }
-    __device__ __forceinline__ void emit(uint32_t o[8]) const {
-        uint32_t c[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) c[i] = (q[i] >> sh) & 0x0F0F0F0Fu;
-        emit_scaled<8>(c, splat_h2(h2f((uint16_t)d)), o);
-    }
-};
-
-template <> struct Deq16<T_Q8_0> {
-    uint32_t q[4], d;
     __device__ __forceinline__ void pin_all() { pin(q); pin(d); }
-    __device__ __forceinline__ void load(const uint8_t *row, int k0) {
-        const uint8_t *b = row + (k0 >> 5) * 34;
-        d = ld2(b);
-        ld16(b + 2 + (k0 & 16), q);
-    }
-    __device__ __forceinline__ void emit(uint32_t o[8]) const {
-        uint32_t c[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) c[i] = q[i] ^ 0x80808080u;   // int8 -> 128 + q
-        emit_scaled<128>(c, splat_h2(h2f((uint16_t)d)), o);
+    __device__ __forceinline__ u32x4 emit() const {
+        return emit8_scaled<8>((q[0] >> sh) & 0x0F0F0F0Fu, (q[1] >> sh) & 0x0F0F0F0Fu, splat_h2(h2f((uint16_t)d)));
     }
 };
 
-template <> struct Deq16<T_Q4_K> {
-    uint32_t q[4], dm, S[3];
+template <> struct Deq8<T_Q8_0> {
+    u32x2 q;
+    uint32_t d;
+    __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, uint32_t row, int k0) {
+        const uint32_t b = row + (uint32_t)(k0 >> 5) * 34;
+        d = bl16(r, b);
+        q = bl64(r, b + 2 + (k0 & 31));
+    }
+    __device__ __forceinline__ void pin_all() { pin(q); pin(d); }
+    __device__ __forceinline__ u32x4 emit() const {   // int8 -> 128 + q
+        return emit8_scaled<128>(q[0] ^ 0x80808080u, q[1] ^ 0x80808080u, splat_h2(h2f((uint16_t)d)));
+    }
+};
+
+// Q4_K / Q5_K header: d, dmin (fp16) and the 12 packed 6-bit scale/min bytes -> (d*sc, dmin*m)
+// of sub-block j (get_scale_min_k4, src/ggml-quants.c:703-710)
+__device__ __forceinline__ void k4_sub_scale(const u32x4 &hd, int j, h2v &d1, h2v &m1) {
+    const uint32_t S[3] = {hd[1], hd[2], hd[3]};
+    uint32_t sc0, sc1, m0, m1v;
+    k4_scale_min_pair(S, j >> 1, sc0, sc1, m0, m1v);
+    const bool hi = j & 1;
+    d1 = splat_h2(h2f((uint16_t)hd[0]) * (float)(hi ? sc1 : sc0));
+    m1 = splat_h2(h2f((uint16_t)(hd[0] >> 16)) * (float)(hi ? m1v : m0));
+}
+
+template <> struct Deq8<T_Q4_K> {
+    u32x4 hd;
+    u32x2 q;
     int j;
-    __device__ __forceinline__ void pin_all() { pin(q); pin(dm); pin(S); }
-    __device__ __forceinline__ void load(const uint8_t *row, int k0) {
-        const uint8_t *b = row + (k0 >> 8) * 144;
-        const int w = k0 & 255, c = w >> 6;
+    __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, uint32_t row, int k0) {
+        const uint32_t b = row + (uint32_t)(k0 >> 8) * 144;
+        const int w = k0 & 255;
         j = w >> 5;
-        dm = ld4(b);
-        S[0] = ld4(b + 4); S[1] = ld4(b + 8); S[2] = ld4(b + 12);
-        ld16(b + 16 + 32 * c + (w & 31), q);
+        hd = bl128(r, b);
+        q = bl64(r, b + 16 + 32 * (w >> 6) + (w & 31));
     }
-    __device__ __forceinline__ void emit(uint32_t o[8]) const {
-        uint32_t sc0, sc1, m0, m1;
-        k4_scale_min_pair(S, j >> 1, sc0, sc1, m0, m1);
-        const bool hi = j & 1;
-        const float d1 = h2f((uint16_t)dm) * (float)(hi ? sc1 : sc0);
-        const float mm = h2f((uint16_t)(dm >> 16)) * (float)(hi ? m1 : m0);
-        const int sh = hi ? 4 : 0;
-        uint32_t c[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) c[i] = (q[i] >> sh) & 0x0F0F0F0Fu;
-        emit_affine(c, splat_h2(d1), splat_h2(mm), o);
+    __device__ __forceinline__ void pin_all() { pin(hd); pin(q); }
+    __device__ __forceinline__ u32x4 emit() const {
+        h2v d1, m1;
+        k4_sub_scale(hd, j, d1, m1);
+        const int sh = (j & 1) * 4;
+        return emit8_affine((q[0] >> sh) & 0x0F0F0F0Fu, (q[1] >> sh) & 0x0F0F0F0Fu, d1, m1);
     }
 };
 
-template <> struct Deq16<T_Q5_K> {
-    uint32_t q[4], h[4], dm, S[3];
+template <> struct Deq8<T_Q5_K> {
+    u32x4 hd;
+    u32x2 q, h;
     int j;
-    __device__ __forceinline__ void pin_all() { pin(q); pin(h); pin(dm); pin(S); }
-    __device__ __forceinline__ void load(const uint8_t *row, int k0) {
-        const uint8_t *b = row + (k0 >> 8) * 176;
-        const int w = k0 & 255, c = w >> 6;
+    __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, uint32_t row, int k0) {
+        const uint32_t b = row + (uint32_t)(k0 >> 8) * 176;
+        const int w = k0 & 255;
         j = w >> 5;
-        dm = ld4(b);
-        S[0] = ld4(b + 4); S[1] = ld4(b + 8); S[2] = ld4(b + 12);
-        ld16(b + 16 + (w & 31), h);
-        ld16(b + 48 + 32 * c + (w & 31), q);
+        hd = bl128(r, b);
+        h = bl64(r, b + 16 + (w & 31));
+        q = bl64(r, b + 48 + 32 * (w >> 6) + (w & 31));
     }
-    __device__ __forceinline__ void emit(uint32_t o[8]) const {
-        uint32_t sc0, sc1, m0, m1;
-        k4_scale_min_pair(S, j >> 1, sc0, sc1, m0, m1);
-        const bool hi = j & 1;
-        const float d1 = h2f((uint16_t)dm) * (float)(hi ? sc1 : sc0);
-        const float mm = h2f((uint16_t)(dm >> 16)) * (float)(hi ? m1 : m0);
-        const int sh = hi ? 4 : 0;
-        uint32_t c[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) c[i] = ((q[i] >> sh) & 0x0F0F0F0Fu) | (((h[i] >> j) & 0x01010101u) << 4);
-        emit_affine(c, splat_h2(d1), splat_h2(mm), o);
+    __device__ __forceinline__ void pin_all() { pin(hd); pin(q); pin(h); }
+    __device__ __forceinline__ u32x4 emit() const {
+        h2v d1, m1;
+        k4_sub_scale(hd, j, d1, m1);
+        const int sh = (j & 1) * 4;
+        const uint32_t c0 = ((q[0] >> sh) & 0x0F0F0F0Fu) | (((h[0] >> j) & 0x01010101u) << 4);
+        const uint32_t c1 = ((q[1] >> sh) & 0x0F0F0F0Fu) | (((h[1] >> j) & 0x01010101u) << 4);
+        return emit8_affine(c0, c1, d1, m1);
     }
 };
 
-template <> struct Deq16<T_Q6_K> {
-    uint32_t ql[4], qh[4], d;
+template <> struct Deq8<T_Q6_K> {
+    u32x2 ql, qh;
+    uint32_t d, sc;
     int k;
-    __device__ __forceinline__ void pin_all() { pin(ql); pin(qh); pin(d); }
-    __device__ __forceinline__ void load(const uint8_t *row, int k0) {
-        const uint8_t *b = row + (k0 >> 8) * 210;
-        const int w = k0 & 255, hh = w >> 7, r = w & 127, l0 = r & 31;
-        k = r >> 5;
-        ld16(b + 64 * hh + l0 + 32 * (k & 1), ql);
-        ld16(b + 128 + 32 * hh + l0, qh);
-        const uint32_t sc = b[192 + 8 * hh + (l0 >> 4) + 2 * k];   // int8 scale of these 16
-        d = (uint32_t)ld2(b + 208) | (sc << 16);
+    __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, uint32_t row, int k0) {
+        const uint32_t b = row + (uint32_t)(k0 >> 8) * 210;
+        const int w = k0 & 255, hh = w >> 7, rr = w & 127, l = rr & 31;
+        k = rr >> 5;
+        ql = bl64(r, b + 64 * hh + l + 32 * (k & 1));
+        qh = bl64(r, b + 128 + 32 * hh + l);
+        sc = bl8(r, b + 192 + 8 * hh + (l >> 4) + 2 * k);   // int8 scale of this 16-group
+        d = bl16(r, b + 208);
     }
-    __device__ __forceinline__ void emit(uint32_t o[8]) const {
-        const float ds = h2f((uint16_t)d) * (float)(int8_t)(d >> 16);
+    __device__ __forceinline__ void pin_all() { pin(ql); pin(qh); pin(d); pin(sc); }
+    __device__ __forceinline__ u32x4 emit() const {
+        const float ds = h2f((uint16_t)d) * (float)(int8_t)sc;
         const int sh = (k >> 1) * 4, hs = 2 * k;
-        uint32_t c[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) c[i] = ((ql[i] >> sh) & 0x0F0F0F0Fu) | (((qh[i] >> hs) & 0x03030303u) << 4);
-        emit_scaled<32>(c, splat_h2(ds), o);
+        const uint32_t c0 = ((ql[0] >> sh) & 0x0F0F0F0Fu) | (((qh[0] >> hs) & 0x03030303u) << 4);
+        const uint32_t c1 = ((ql[1] >> sh) & 0x0F0F0F0Fu) | (((qh[1] >> hs) & 0x03030303u) << 4);
+        return emit8_scaled<32>(c0, c1, splat_h2(ds));
     }
 };
 
@@ -204,22 +213,27 @@ template <> struct Deq16<T_Q6_K> {
 // activations: f32 (strided) -> f16 [slice][M][Kpad]; per-token power-of-two prescale puts the
 // largest |x| in (2^13, 2^14] (no f16 overflow, no subnormals); xinv[slice][M] undoes it
 // ------------------------------------------------------------------------------------------
-// one wave per token: float4 loads (scalar when src1 rows are not 16-B aligned), 8-B stores
+// one workgroup per token (K spread over 256 threads, 4 float4 loads in flight per thread);
+// scalar loads when src1 rows are not 16-B aligned; 8-B stores
 __global__ __launch_bounds__(256) void mmq_convert_x(const MmArgs a, _Float16 *x16, float *xinv, int Kpad) {
-    const int lane = threadIdx.x & 63;
-    const int tok = blockIdx.x * 4 + (threadIdx.x >> 6), slice = blockIdx.y;
-    if (tok >= a.M) return;   // whole wave; no barriers below
+    const int tok = blockIdx.x, slice = blockIdx.y;
     const int i12 = slice % a.ne12, i13 = slice / a.ne12;
     const float *src = reinterpret_cast<const float *>(a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13 +
                                                        (int64_t)tok * a.nb11);
     auto ld4f = [&](int k) -> float4 {
+        if (k >= a.K) return make_float4(0.f, 0.f, 0.f, 0.f);   // K % 4 == 0
         if (a.x_aligned16) return *reinterpret_cast<const float4 *>(src + k);
         return make_float4(src[k], src[k + 1], src[k + 2], src[k + 3]);
     };
+    const int t4 = threadIdx.x * 4;
     float amax = 0.f;
-    for (int k = lane * 4; k < a.K; k += 256) {   // K % 32 == 0
-        const float4 v = ld4f(k);
-        amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    for (int k0 = 0; k0 < a.K; k0 += 4096) {
+        float4 v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = ld4f(k0 + 1024 * i + t4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v[i].x), fabsf(v[i].y)), fmaxf(fabsf(v[i].z), fabsf(v[i].w))));
     }
     amax = fmaxf(amax, xchg<1>(amax));
     amax = fmaxf(amax, xchg<2>(amax));
@@ -227,175 +241,248 @@ __global__ __launch_bounds__(256) void mmq_convert_x(const MmArgs a, _Float16 *x
     amax = fmaxf(amax, xchg<8>(amax));
     amax = fmaxf(amax, xchg<16>(amax));
     amax = fmaxf(amax, xchg<32>(amax));
+    __shared__ float red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+    __syncthreads();
+    amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
     const int e = amax > 0.f ? (int)ceilf(log2f(amax)) - 14 : 0;
     const float s = ldexpf(1.f, -e);
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
     _Float16 *dst = x16 + ((int64_t)slice * a.M + tok) * Kpad;
-    for (int k = lane * 4; k < Kpad; k += 256) {
-        const float4 v = k < a.K ? ld4f(k) : make_float4(0.f, 0.f, 0.f, 0.f);
-        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-        *reinterpret_cast<h4 *>(dst + k) = h4{(_Float16)(v.x * s), (_Float16)(v.y * s), (_Float16)(v.z * s), (_Float16)(v.w * s)};
+    for (int k0 = 0; k0 < Kpad; k0 += 4096) {
+        float4 v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = ld4f(k0 + 1024 * i + t4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int k = k0 + 1024 * i + t4;
+            if (k < Kpad)
+                *reinterpret_cast<h4 *>(dst + k) =
+                    h4{(_Float16)(v[i].x * s), (_Float16)(v[i].y * s), (_Float16)(v[i].z * s), (_Float16)(v[i].w * s)};
+        }
     }
-    if (lane == 0) xinv[(int64_t)slice * a.M + tok] = ldexpf(1.f, e);
+    if (threadIdx.x == 0) xinv[(int64_t)slice * a.M + tok] = ldexpf(1.f, e);
 }
 
 // byte offset of 16-B chunk c of LDS row r (128-B rows, XOR swizzle over row pairs)
 __device__ __forceinline__ int swz(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 
 // ------------------------------------------------------------------------------------------
-// the tile kernel
+// the tile kernel: 8 waves (two per SIMD, so one wave's dequant VALU overlaps the other's
+// MFMAs), wave grid (BM/32) x (8/(BM/32)), wave tile 32 weight rows x TN*32 tokens.
+//
+// Per K-step (BK = 64) of phase s:
+//   1. weight units of step s+2 -> registers (buffer loads, 2 register slots)
+//   2. activations of step s+2 -> LDS X ring slot (s+2)%3 by LDS-DMA (buffer_load ... lds):
+//      no VGPR round trip and no ds_write issue cost (the ds_write path, ~80 B/clk/CU, was the
+//      bottleneck of register staging); the 16-B XOR swizzle is applied on the source address
+//   3. MFMAs of step s from W slot s%2 and X slot s%3
+//   4. decode the weight units of step s+1 (loaded one phase ago) into W slot (s+1)%2
+//   5. s_waitcnt vmcnt(<this phase's loads>) retires the DMA of step s+1, then one barrier
 // ------------------------------------------------------------------------------------------
-template <int T, int BM, int BN>
+constexpr uint32_t RSRC_W3 = 0x00020000u;   // raw buffer, dword3 for gfx9-class descriptors
+
+template <int T> struct LoadsPerUnit;   // VMEM instructions one Deq8<T>::load issues
+template <> struct LoadsPerUnit<T_Q4_0> { static constexpr int n = 2; };
+template <> struct LoadsPerUnit<T_Q8_0> { static constexpr int n = 2; };
+template <> struct LoadsPerUnit<T_Q4_K> { static constexpr int n = 2; };
+template <> struct LoadsPerUnit<T_Q5_K> { static constexpr int n = 3; };
+template <> struct LoadsPerUnit<T_Q6_K> { static constexpr int n = 4; };
+
+template <int N> __device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+typedef __attribute__((address_space(3))) void *lds_ptr_t;
+
+// 16 B per lane from the buffer straight into LDS at lds_dst + 16 * lane (lds_dst wave-uniform).
+// (A plain device function: used directly inside the kernel's lambdas, this builtin makes the
+// ROCm 7.2 host pass drop the kernel's launch stub.)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_dst, uint32_t voff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds_dst, 16, voff, 0, 0, 0);
+}
+
+template <int T, int BM, int BN, bool STAMP = false>
 __global__ __launch_bounds__(MQ_THREADS) void mmq_kernel(const MmArgs a, const _Float16 *__restrict__ x16,
-                                                         const float *__restrict__ xinv, int Kpad) {
-    constexpr int U = BM / 64;          // 16-weight units per thread per step
-    constexpr int V = BN / 32;          // 16-B activation chunks per thread per step
-    constexpr int TM = BM / 64;         // MFMA tiles per wave along weight rows
-    constexpr int TN = BN / 64;         // MFMA tiles per wave along tokens
-    constexpr int BUF = (BM + BN) * 128;
-    __shared__ __align__(16) uint8_t lds[2 * BUF];
+                                                         const float *__restrict__ xinv, int Kpad, uint32_t w_extent) {
+    constexpr int WGM = BM / 32;                 // waves along weight rows
+    constexpr int WGN = 8 / WGM;                 // waves along tokens
+    constexpr int TN = BN / WGN / 32;            // MFMA tiles per wave along tokens
+    constexpr int U = BM / 64;                   // 8-weight units per thread per step
+    constexpr int V = BN / 64;                   // 1-KiB activation pieces per wave per step
+    constexpr int WB = BM * 128, XB = BN * 128;  // bytes of one W / X slot
+    constexpr int VM_PHASE = U * LoadsPerUnit<T>::n + V;   // VMEM ops one wave issues per phase
+    static_assert(WGM * WGN == 8 && TN >= 1 && U >= 1 && V >= 1, "tile shape");
+    __shared__ __align__(16) uint8_t lds[2 * WB + 3 * XB];   // one array: see the .s traps in the guide
+    uint8_t *const wslot = lds;
+    uint8_t *const xslot = lds + 2 * WB;
 
     const int slice = blockIdx.z;
     const int i12 = slice % a.ne12, i13 = slice / a.ne12;
     const uint8_t *wmat = a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03;
     const _Float16 *xs = x16 + (int64_t)slice * a.M * Kpad;
     uint8_t *dmat = a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3;
+    // rows past N and tokens past M read as zeros (buffer range check)
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void *)wmat, 0, w_extent, RSRC_W3);
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)xs, 0, (uint32_t)a.M * (uint32_t)Kpad * 2u, RSRC_W3);
 
     const int wrow0 = blockIdx.x * BM;
     const int tok0 = blockIdx.y * BN;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
-    const int wm = wave & 1, wn = wave >> 1;
+    const int wm = wave % WGM, wn = wave / WGM;
     const int nsteps = Kpad / MQ_BK;
+    // diagnostic build only (GGML_MI355X_STAMPS): per-wave s_memtime cycles spent in each phase
+    uint64_t st_seg[5] = {0, 0, 0, 0, 0}, st_t = 0, st_start = 0;
+    auto stamp = [&](int seg) {
+        if constexpr (STAMP) {
+            __builtin_amdgcn_sched_barrier(0);
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            if (seg >= 0) st_seg[seg] += t - st_t;
+            st_t = t;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    stamp(-1);
+    st_start = st_t;
 
-    // staging roles (dead rows / tokens are clamped: they only feed outputs that are not stored)
-    const uint8_t *w_row[U];
+    uint32_t w_row[U];
     int w_r[U], w_c[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int g = tid + MQ_THREADS * u;
-        w_r[u] = g >> 2;
-        w_c[u] = (g & 3) * 16;
-        w_row[u] = wmat + (int64_t)min(wrow0 + w_r[u], a.N - 1) * a.nb01;
+        w_r[u] = g >> 3;
+        w_c[u] = (g & 7) * 8;
+        w_row[u] = (uint32_t)(wrow0 + w_r[u]) * (uint32_t)a.nb01;
     }
-    const u32x4 *x_src[V];
-    int x_r[V], x_c[V];
+    // activation pieces: wave piece p = wave + 8v covers tile rows 8p..8p+7; lane -> (row, LDS
+    // chunk lane&7) fetching the global chunk that the swizzle maps there
+    uint32_t x_off[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-        const int g = tid + MQ_THREADS * v;
-        x_r[v] = g >> 3;
-        x_c[v] = g & 7;
-        x_src[v] = reinterpret_cast<const u32x4 *>(xs + (int64_t)min(tok0 + x_r[v], a.M - 1) * Kpad) + x_c[v];
+        const int r = 8 * (wave + 8 * v) + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        x_off[v] = ((uint32_t)(tok0 + r) * (uint32_t)Kpad + (uint32_t)c * 8u) * 2u;
     }
 
-    // one ring slot: raw weight units + activation chunks of one K-step
-    auto load = [&](Deq16<T> (&w)[U], u32x4 (&x)[V], int step) {
+    auto load_w = [&](Deq8<T> (&w)[U], int step) {
         const int k0 = step * MQ_BK;
+        // the K tail of the 32-block types re-reads the row's last unit: finite weights times
+        // the zero-padded activations contribute exactly 0
 #pragma unroll
-        for (int v = 0; v < V; ++v) x[v] = x_src[v][k0 / 8];
-#pragma unroll
-        for (int u = 0; u < U; ++u) w[u].load(w_row[u], min(k0 + w_c[u], a.K - 16));
+        for (int u = 0; u < U; ++u) w[u].load(wr, w_row[u], min(k0 + w_c[u], a.K - 8));
     };
-    auto store = [&](Deq16<T> (&w)[U], u32x4 (&x)[V], int step, int buf) {
-        const int k0 = step * MQ_BK;
+    auto dma_x = [&](int step, int slot) {
+        const uint32_t k2 = (uint32_t)step * MQ_BK * 2u;
 #pragma unroll
-        for (int v = 0; v < V; ++v) pin(x[v]);
+        for (int v = 0; v < V; ++v)
+            dma16(xr, xslot + slot * XB + (wave + 8 * v) * 1024, x_off[v] + k2);
+    };
+    auto store_w = [&](Deq8<T> (&w)[U], int slot) {
 #pragma unroll
         for (int u = 0; u < U; ++u) w[u].pin_all();
-        uint8_t *W = lds + buf * BUF;
-        uint8_t *X = W + BM * 128;
+        uint8_t *W = wslot + slot * WB;
 #pragma unroll
-        for (int v = 0; v < V; ++v) *reinterpret_cast<u32x4 *>(X + swz(x_r[v], x_c[v])) = x[v];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            uint32_t o[8];
-            w[u].emit(o);
-            if (k0 + w_c[u] >= a.K) {   // ragged K tail (32-block types): zero weights
-#pragma unroll
-                for (int i = 0; i < 8; ++i) o[i] = 0;
-            }
-            *reinterpret_cast<u32x4 *>(W + swz(w_r[u], w_c[u] / 8)) = u32x4{o[0], o[1], o[2], o[3]};
-            *reinterpret_cast<u32x4 *>(W + swz(w_r[u], w_c[u] / 8 + 1)) = u32x4{o[4], o[5], o[6], o[7]};
-        }
+        for (int u = 0; u < U; ++u)
+            *reinterpret_cast<u32x4 *>(W + swz(w_r[u], w_c[u] / 8)) = w[u].emit();
     };
 
-    float16v acc[TM][TN];
+    float16v acc[TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
 
     const int fr = lane & 31, fh = lane >> 5;
-    auto compute = [&](int buf) {
-        const uint8_t *W = lds + buf * BUF;
-        const uint8_t *X = W + BM * 128;
+    auto compute = [&](int wsl, int xsl) {
+        const uint8_t *W = wslot + wsl * WB;
+        const uint8_t *X = xslot + xsl * XB;
 #pragma unroll
         for (int ks = 0; ks < MQ_BK / 16; ++ks) {
             const int c = 2 * ks + fh;
-            half8 bw[TM], ax[TN];
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-                bw[i] = *reinterpret_cast<const half8 *>(W + swz(wm * (BM / 2) + 32 * i + fr, c));
+            const half8 bw = *reinterpret_cast<const half8 *>(W + swz(wm * 32 + fr, c));
+            half8 ax[TN];
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                ax[j] = *reinterpret_cast<const half8 *>(X + swz(wn * (BN / 2) + 32 * j + fr, c));
+                ax[j] = *reinterpret_cast<const half8 *>(X + swz(wn * (TN * 32) + 32 * j + fr, c));
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax[j], bw[i], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax[j], bw, acc[j], 0, 0, 0);
         }
     };
+    auto barrier = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's ds_writes landed
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
 
-    // 2-deep register ring: loads for step s+2 are issued before the MFMAs of step s and
-    // written to LDS after those of step s+1. Loads and stores are unconditional (clamped step)
-    // so the compiler keeps counted vmcnt waits instead of draining the ring.
-    Deq16<T> wa[U], wb[U];
-    u32x4 xa[V], xb[V];
-    load(wa, xa, 0);
-    load(wb, xb, min(1, nsteps - 1));
-    store(wa, xa, 0, 0);
-    __syncthreads();
-    int s = 0;
-    // sched_barrier pins the phases: without it the scheduler hoists the decode of the slot just
-    // loaded into the current phase and waits vmcnt(0) for it, collapsing the ring to depth 1
+    Deq8<T> wa[U], wb[U];
+    // prologue: steps 0 and 1 in flight, step 0 decoded
+    load_w(wa, 0);
+    dma_x(0, 0);
+    load_w(wb, min(1, nsteps - 1));
+    dma_x(min(1, nsteps - 1), 1);
+    __builtin_amdgcn_sched_barrier(0);
+    store_w(wa, 0);
+    wait_vmcnt<VM_PHASE>();   // retires step 0's DMA
+    barrier();
+
+    // phase body; W register slot parity is static (loop unrolled by 2), X slots rotate by 3
+    auto phase = [&](Deq8<T> (&wnext)[U], Deq8<T> (&wdec)[U], int s, int xs0) {
+        const int xs1 = xs0 == 2 ? 0 : xs0 + 1, xs2 = xs1 == 2 ? 0 : xs1 + 1;
+        stamp(4);
+        load_w(wnext, min(s + 2, nsteps - 1));
+        dma_x(min(s + 2, nsteps - 1), xs2);
+        __builtin_amdgcn_sched_barrier(0);
+        stamp(0);
+        compute(s & 1, xs0);
+        __builtin_amdgcn_sched_barrier(0);
+        stamp(1);
+        store_w(wdec, (s + 1) & 1);
+        stamp(2);
+        wait_vmcnt<VM_PHASE>();   // retires step s+1's DMA (issued one phase ago)
+        stamp(3);
+        barrier();
+        return xs1;
+    };
+    int s = 0, xsl = 0;
     for (; s + 1 < nsteps; s += 2) {
-        load(wa, xa, min(s + 2, nsteps - 1));
-        __builtin_amdgcn_sched_barrier(0);
-        compute(0);
-        __builtin_amdgcn_sched_barrier(0);
-        store(wb, xb, s + 1, 1);
-        __syncthreads();
-        load(wb, xb, min(s + 3, nsteps - 1));
-        __builtin_amdgcn_sched_barrier(0);
-        compute(1);
-        __builtin_amdgcn_sched_barrier(0);
-        store(wa, xa, s + 2, 0);
-        __syncthreads();
+        xsl = phase(wa, wb, s, xsl);
+        xsl = phase(wb, wa, s + 1, xsl);
     }
-    if (s < nsteps) compute(0);   // odd step count: the last step sits in buffer 0
+    if (s < nsteps) compute(s & 1, xsl);   // odd step count: the last step
+    wait_vmcnt<0>();   // no LDS-DMA may still be landing when the workgroup's LDS is released
+    stamp(4);
+    if constexpr (STAMP) {
+        if (lane == 0 && a.stamps) {
+            const int g = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+            unsigned long long *o = a.stamps + ((size_t)g * 8 + wave) * 8;
+            o[0] = st_start;
+            for (int i = 0; i < 5; ++i) o[1 + i] = st_seg[i];
+            o[6] = st_t;
+            o[7] = nsteps;
+        }
+    }
 
-    // epilogue: lane holds weight row (lane & 31) of each B tile and 16 tokens of each A tile;
-    // token scales are read before any store (dst may alias nothing, but the compiler cannot know)
+    // epilogue: lane holds weight row (lane & 31) and 16 tokens of each A tile; token scales are
+    // read before any store (the compiler cannot prove dst does not alias them)
     float inv[TN][16];
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int tok = tok0 + wn * (BN / 2) + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * fh;
+            const int tok = tok0 + wn * (TN * 32) + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * fh;
             inv[j][r] = xinv[(int64_t)slice * a.M + min(tok, a.M - 1)];
         }
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-        const int orow = wrow0 + wm * (BM / 2) + 32 * i + fr;
-        if (orow >= a.N) continue;
+    const int orow = wrow0 + wm * 32 + fr;
+    if (orow < a.N) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int tok = tok0 + wn * (BN / 2) + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * fh;
-                if (tok < a.M) reinterpret_cast<float *>(dmat + (int64_t)tok * a.nb1)[orow] = acc[i][j][r] * inv[j][r];
+                const int tok = tok0 + wn * (TN * 32) + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * fh;
+                if (tok < a.M) reinterpret_cast<float *>(dmat + (int64_t)tok * a.nb1)[orow] = acc[j][r] * inv[j][r];
             }
         }
     }
@@ -404,15 +491,25 @@ __global__ __launch_bounds__(MQ_THREADS) void mmq_kernel(const MmArgs a, const _
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
+static int64_t row_bytes(int type, int K) { return (int64_t)K / type_blck(type) * type_bytes(type); }
+
+// buffer offsets are 32-bit: one weight matrix (plus a tile of rows past its end) and one
+// slice of converted activations must each stay below 4 GiB; larger problems use the mat-vec
 bool mmq_supported(int type, const MmArgs &a) {
-    (void)a;
-    return type == T_Q4_0 || type == T_Q8_0 || type == T_Q4_K || type == T_Q5_K || type == T_Q6_K;
+    if (!(type == T_Q4_0 || type == T_Q8_0 || type == T_Q4_K || type == T_Q5_K || type == T_Q6_K)) return false;
+    const int64_t kpad = (a.K + MQ_BK - 1) / MQ_BK * MQ_BK;
+    const int64_t w_span = (int64_t)(a.N + 128) * a.nb01 + row_bytes(type, a.K);
+    return a.nb01 >= row_bytes(type, a.K) && w_span < (1LL << 32) && (int64_t)(a.M + 128) * kpad * 2 < (1LL << 32);
 }
 
 template <int T, int BM, int BN>
 static void launch_tile(const MmArgs &a, const _Float16 *x16, const float *xinv, int Kpad, int slices, hipStream_t st) {
     const dim3 grid((a.N + BM - 1) / BM, (a.M + BN - 1) / BN, slices);
-    hipLaunchKernelGGL((mmq_kernel<T, BM, BN>), grid, dim3(MQ_THREADS), 0, st, a, x16, xinv, Kpad);
+    const uint32_t w_extent = (uint32_t)((int64_t)(a.N - 1) * a.nb01 + row_bytes(T, a.K));
+    if (a.stamps && (size_t)grid.x * grid.y * grid.z * 64 <= 8 * 65536)
+        hipLaunchKernelGGL((mmq_kernel<T, BM, BN, true>), grid, dim3(MQ_THREADS), 0, st, a, x16, xinv, Kpad, w_extent);
+    else
+        hipLaunchKernelGGL((mmq_kernel<T, BM, BN>), grid, dim3(MQ_THREADS), 0, st, a, x16, xinv, Kpad, w_extent);
 }
 
 template <int T>
@@ -425,7 +522,7 @@ static void launch_type(int tile, const MmArgs &a, const _Float16 *x16, const fl
     }
 }
 
-// tile shape: the largest tile that still gives every CU a workgroup; GGML_MI355X_MMQ_TILE
+// tile shape; GGML_MI355X_MMQ_TILE
 // (64x128 | 128x64 | 128x128) overrides it for measurements
 static int pick_tile(const MmArgs &a, int slices) {
     static const char *env = getenv("GGML_MI355X_MMQ_TILE");
@@ -435,8 +532,10 @@ static int pick_tile(const MmArgs &a, int slices) {
         if (!strcmp(env, "128x128")) return 2;
     }
     auto wgs = [&](int bm, int bn) { return (int64_t)((a.N + bm - 1) / bm) * ((a.M + bn - 1) / bn) * slices; };
+    // measured on MI355X (scripts/mmq_sweep.sh): 128x128 once it fills the chip, otherwise the
+    // 64-row tile (twice the workgroups) unless there are too few tokens for 128-token tiles
     if (wgs(128, 128) >= 256) return 2;
-    return a.M <= 64 ? 1 : (wgs(128, 64) >= 256 ? 1 : 0);
+    return a.M > 64 ? 0 : 1;
 }
 
 hipError_t mmq_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch) {
@@ -448,7 +547,7 @@ hipError_t mmq_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratc
     if (!buf) return hipErrorOutOfMemory;
     _Float16 *x16 = reinterpret_cast<_Float16 *>(buf);
     float *xinv = reinterpret_cast<float *>(buf + x16_bytes);
-    hipLaunchKernelGGL(mmq_convert_x, dim3((a.M + 3) / 4, slices), dim3(256), 0, st, a, x16, xinv, Kpad);
+    hipLaunchKernelGGL(mmq_convert_x, dim3(a.M, slices), dim3(256), 0, st, a, x16, xinv, Kpad);
     const int tile = pick_tile(a, slices);
     switch (type) {
         case T_Q4_0: launch_type<T_Q4_0>(tile, a, x16, xinv, Kpad, slices, st); break;

@@ -21,8 +21,9 @@ for sh in shapes:
     s = bench.MatVecSet(torch, TYPES[tn], int(K), int(N), int(Mc), 1, 24)
     s.launch(0)
     torch.cuda.synchronize()
-    us = s.launch_us(24)
+    ev_us = s.launch_us(24)
+    us = s.graph_period_us(24)   # back-to-back launches in one hipGraph: no host gaps
     print(f"tile={tile:8s} {sh:22s} {us:9.2f} us  {s.flops / us / 1e6:8.1f} TFLOP/s  "
-          f"{s.bytes / us / 1e3:8.1f} GB/s", flush=True)
+          f"{s.bytes / us / 1e3:8.1f} GB/s  (events {ev_us:.2f} us)", flush=True)
     del s
     torch.cuda.empty_cache()

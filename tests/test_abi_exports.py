@@ -36,6 +36,13 @@ def test_dynamic_symbol_table():
     assert not any(s.startswith("_ZN6mi355x") for s in exported)
 
 
+def test_no_unresolved_internal_symbols():
+    """every kernel launch stub and internal function is defined inside the library (a template
+    kernel whose host stub the compiler dropped would only fail at dlopen on the GPU box)"""
+    out = subprocess.run(["nm", "-D", "--undefined-only", M.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    assert "mi355x" not in out, [l for l in out.splitlines() if "mi355x" in l]
+
+
 def test_code_object_targets_gfx950_only():
     """every embedded device code object is for gfx950 (no other arch, no dual paths)"""
     import re
