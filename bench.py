@@ -43,6 +43,7 @@ sys.path.insert(0, os.path.join(ROOT, "ggml-gfx906_amd"))
 
 import mi355x_qmm as M  # noqa: E402
 
+MFMA_F16_PEAK_TFLOPS = 2500.0   # dense f16/bf16 MFMA peak, MI355X_MICROARCH.md (no sparsity)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 HBM_MEASURED_GBS = 6290.0      # float4 copy measured on MI355X (same guide)
 I8_PEAK_TOPS = 5000.0          # dense int8 / fp8 MFMA (no sparsity)
@@ -134,8 +135,12 @@ class MatVecSet:
 def config_row(s: MatVecSet, us: float) -> dict:
     gbs = s.bytes / (us * 1e-6) / 1e9
     tf = s.flops / (us * 1e-6) / 1e12
-    return {"us": round(us, 3), "GB/s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
-            "TFLOP/s": round(tf, 3)}
+    row = {"us": round(us, 3), "GB/s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+           "TFLOP/s": round(tf, 3)}
+    if s.Mc > 8:   # mat-mat path: f16 MFMA tiles, priced against the dense f16 peak
+        row.update(bound="mfma", mfma_frac_f16=round(tf / MFMA_F16_PEAK_TFLOPS, 4),
+                   graph_period_us=round(s.graph_period_us(16), 3))
+    return row
 
 
 def measured_traffic(key: str):
@@ -177,6 +182,27 @@ def cpu_baseline(seconds: float) -> dict:
             "us_per_mul_mat": round(per * 1e6, 2)}
 
 
+def launch_env():
+    """(world, rank, local_rank) as torch.distributed.run exports them; 1 process by default"""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def max_over_ranks(seconds: float, device) -> float:
+    """slowest rank's elapsed time (all ranks get it); `device` is cuda for RCCL, cpu for gloo"""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([seconds], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def job_gbps(bytes_per_step_per_rank: int, steps: int, world: int, t_max: float) -> float:
+    """whole-job throughput: every rank streams its own weight stacks (weak scaling, no data-path
+    collective), so the job moves world x bytes per step in the slowest rank's time"""
+    return bytes_per_step_per_rank * steps * world / t_max / 1e9
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -190,13 +216,14 @@ def main() -> None:
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = launch_env()
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    M.build()
+    if local == 0:
+        M.build()                      # one rank per node compiles (if stale); the others wait
+    if world > 1:
+        dist.barrier()
     if M.device_count() < 1:
         raise SystemExit("no gfx950 device visible: the MI355X backend cannot run")
 
@@ -220,14 +247,10 @@ def main() -> None:
         g.launch(i)
     barrier()
     elapsed = time.perf_counter() - t0
-    t_max = elapsed
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max = float(tt.item())
+    t_max = max_over_ranks(elapsed, torch.device("cuda", local)) if world > 1 else elapsed
 
     kernel_us = g.launch_us(max(8, args.steps))
-    value = g.bytes * args.steps * world / t_max / 1e9
+    value = job_gbps(g.bytes, args.steps, world, t_max)
     achieved = g.bytes / (kernel_us * 1e-6) / 1e9
 
     extra = {}
@@ -243,6 +266,7 @@ def main() -> None:
             ("q5_K_4096x11008_m1_b24", M.Q5_K, 4096, 11008, 1, 24),
             ("q6_K_4096x11008_m1_b24", M.Q6_K, 4096, 11008, 1, 24),
             ("q8_0_4096x4096_m512", M.Q8_0, 4096, 4096, 512, 1),
+            ("q4_K_4096x4096_m512", M.Q4_K, 4096, 4096, 512, 1),
         ):
             s2 = MatVecSet(torch, t, K, N, Mc, batch, 2 if batch > 1 else 24)
             s2.launch(0)

@@ -1,0 +1,56 @@
+"""Multi-process (gloo, world_size 2, CPU) coverage of bench.py's N>1 path: rank/world from the
+torch.distributed.run environment, the slowest-rank timing reduction and the weak-scaling
+aggregate. The GPU run uses the same functions over RCCL ("nccl")."""
+import os
+import socket
+
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank: int, world: int, port: int, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    w, r, l = bench.launch_env()
+    dist.init_process_group("gloo", rank=r, world_size=w)
+    elapsed = 0.5 + rank            # rank 1 is the slow one
+    t_max = bench.max_over_ranks(elapsed, torch.device("cpu"))
+    gbps = bench.job_gbps(606076928, 20, w, t_max)
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((r, w, l, t_max, gbps))
+
+
+def test_two_rank_timing_and_aggregate():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[0] for r in res] == [0, 1] and all(r[1] == 2 and r[2] == r[0] for r in res)
+    for r in res:
+        assert r[3] == pytest.approx(1.5)                           # max over ranks
+        assert r[4] == pytest.approx(606076928 * 20 * 2 / 1.5 / 1e9)  # both ranks' bytes / slowest time
+
+
+def test_single_process_defaults(monkeypatch):
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    assert bench.launch_env() == (1, 0, 0)
+    assert bench.job_gbps(1e9, 10, 1, 2.0) == pytest.approx(5.0)
