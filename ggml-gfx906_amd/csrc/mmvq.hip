@@ -22,6 +22,7 @@
 //
 // Templated on <type, NC columns, RPW rows per wave, IDS = MUL_MAT_ID routing, RAG, XA>.
 #include <algorithm>
+#include <cstdlib>
 
 #include "qcommon.h"
 #include "qmm_args.h"
@@ -303,8 +304,10 @@ template <> struct Frag<T_Q6_K> {
             const uint8_t *pa = reinterpret_cast<const uint8_t *>(ip & ~(uintptr_t)3);
             const uint32_t sh = (uint32_t)(ip & 3);
             const uint2 w = *reinterpret_cast<const uint2 *>(pa);
-            uint32_t w2 = 0;
-            if (sh) w2 = *reinterpret_cast<const uint32_t *>(pa + 8);   // never past the block end
+            // third dword only matters when misaligned (then it ends at byte 209 of the block);
+            // aligned blocks re-read the second one, so the load is unconditional (no branch
+            // around a load, which would force a vmcnt(0) drain) and never passes the block end
+            const uint32_t w2 = *reinterpret_cast<const uint32_t *>(pa + (sh ? 8 : 4));
             SC[0] = __builtin_amdgcn_alignbyte(w.y, w.x, sh);
             SC[1] = __builtin_amdgcn_alignbyte(w2, w.y, sh);
         }
@@ -568,7 +571,7 @@ size_t mmvq_lds_bytes(int K, int nc) {
 
 int mmvq_rows_per_wg(int rpw) { return MMVQ_WAVES * rpw; }
 
-constexpr int64_t MMVQ_TARGET_WGS = 1024;
+constexpr int64_t MMVQ_TARGET_WGS = 2048;   // two rounds of 4 resident 8-wave workgroups per CU (scripts/mmvq_sweep.sh)
 
 template <int T, int NC, int RPW, bool IDS, bool RAG, bool XA, bool BIGK>
 static hipError_t launch_one(const MmArgs &a, int grid_y, int grid_z, hipStream_t st) {
@@ -583,7 +586,10 @@ static hipError_t launch_one(const MmArgs &a, int grid_y, int grid_z, hipStream_
     const int n_groups = (a.N + rows_per_group - 1) / rows_per_group;
     // enough workgroups to fill 256 CUs ~4 deep; beyond that each workgroup walks more groups
     const int64_t others = (int64_t)grid_y * grid_z;
-    const int want = (int)std::max<int64_t>(1, (MMVQ_TARGET_WGS + others - 1) / others);
+    static const int64_t target = getenv("GGML_MI355X_MMVQ_WGS") ? atoll(getenv("GGML_MI355X_MMVQ_WGS")) : MMVQ_TARGET_WGS;
+    // floor, not ceil: a launch just above a multiple of the resident capacity (4 workgroups of
+    // 8 waves per CU = 1024) leaves a tail of workgroups that start only when others finish
+    const int want = (int)std::max<int64_t>(1, target / others);
     dim3 grid(std::min(n_groups, want), grid_y, grid_z);
     hipLaunchKernelGGL(kern, grid, dim3(MMVQ_THREADS), lds, st, a);
     return hipGetLastError();
