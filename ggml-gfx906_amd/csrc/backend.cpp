@@ -309,6 +309,10 @@ enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
             rc = mul_mat(tv(node->src[0]), tv(node->src[1]), tv(node), c->stream, c->scratch);
         } else if (node->op == GGMLABI_OP_MUL_MAT_ID) {
             rc = mul_mat_id(tv(node->src[0]), tv(node->src[1]), tv(node->src[2]), tv(node), c->stream, c->scratch);
+        } else if (node->op == GGMLABI_OP_GET_ROWS) {
+            rc = get_rows(tv(node->src[0]), tv(node->src[1]), tv(node), c->stream);
+        } else if (node->op == GGMLABI_OP_CPY) {
+            rc = quantize(tv(node->src[0]), tv(node), c->stream);   // node is the view of src[1]
         } else {
             fprintf(stderr, "[ggml-mi355x] unsupported op %d in graph (node %s)\n", node->op, node->name);
             return GGML_STATUS_FAILED;
@@ -411,6 +415,12 @@ bool dv_supports_op(ggml_backend_dev_t, const struct ggml_tensor *op) {
         case GGMLABI_OP_MUL_MAT_ID:
             return op->type == GGMLABI_TYPE_F32 && supports_mm_operands(op->src[0], op->src[1]) &&
                    op->src[2]->type == GGMLABI_TYPE_I32 && op->src[2]->ne[0] * op->src[2]->ne[1] <= 65535;
+        // GET_ROWS of the hot quant types / f32 (dequantized rows, bit-exact), like get_rows_cuda
+        case GGMLABI_OP_GET_ROWS:
+            return check_get_rows(tv(op->src[0]), tv(op->src[1]), tv(op)) == GGML_MI355X_OK;
+        // f32 -> Q4_0 / Q8_0 copies (the reference GPU's cpy_f32_q subset of these types)
+        case GGMLABI_OP_CPY:
+            return check_quantize(tv(op->src[0]), tv(op)) == GGML_MI355X_OK;
         default:
             return false;
     }

@@ -88,4 +88,129 @@ hipError_t dequant_launch(int type, const void *src, float *dst, int64_t n, hipS
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------
+// GET_ROWS: dst[i12][i11][i10][:] = dequantize_row(src0 row idx[i12][i11][i10] of matrix
+// (i11, i12)) — src/ggml-cpu/ops.cpp:5121-5163 (get_rows_q), src/ggml.c:3617-3637 (shapes).
+// Bit-exact: the same per-element formulas as dequantize_row_*. Out-of-range indices (the
+// reference asserts) are clamped so the kernel never reads outside src0.
+// ------------------------------------------------------------------------------------------
+struct RowsArgs {
+    const uint8_t *src; int64_t nb01, nb02, nb03, ne01;
+    const uint8_t *idx; int64_t nb10, nb11, nb12, ne10, ne11;
+    uint8_t *dst; int64_t nb1, nb2, nb3;
+    int64_t ne00;
+};
+
+template <int T>
+__global__ __launch_bounds__(256) void get_rows_kernel(const RowsArgs a) {
+    const int64_t row = blockIdx.y;                      // flattened (i10, i11, i12)
+    const int64_t i12 = row / (a.ne10 * a.ne11);
+    const int64_t i11 = (row - i12 * a.ne10 * a.ne11) / a.ne10;
+    const int64_t i10 = row - i12 * a.ne10 * a.ne11 - i11 * a.ne10;
+    int64_t i01 = *reinterpret_cast<const int32_t *>(a.idx + i10 * a.nb10 + i11 * a.nb11 + i12 * a.nb12);
+    i01 = i01 < 0 ? 0 : (i01 >= a.ne01 ? a.ne01 - 1 : i01);
+    const uint8_t *srow = a.src + i01 * a.nb01 + i11 * a.nb02 + i12 * a.nb03;
+    float *drow = reinterpret_cast<float *>(a.dst + i10 * a.nb1 + i11 * a.nb2 + i12 * a.nb3);
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.ne00) return;
+    if constexpr (T == T_F32) {
+        drow[i] = reinterpret_cast<const float *>(srow)[i];
+    } else {
+        const int64_t b = i / QT<T>::blck;
+        drow[i] = deq_one<T>(srow + b * QT<T>::bytes, (int)(i - b * QT<T>::blck));
+    }
+}
+
+hipError_t get_rows_launch(int type, const RowsArgs &a, int64_t nrows, hipStream_t st) {
+    const dim3 grid((unsigned)((a.ne00 + 255) / 256), (unsigned)nrows);
+    switch (type) {
+        case T_F32: hipLaunchKernelGGL(get_rows_kernel<T_F32>, grid, dim3(256), 0, st, a); break;
+        case T_Q4_0: hipLaunchKernelGGL(get_rows_kernel<T_Q4_0>, grid, dim3(256), 0, st, a); break;
+        case T_Q8_0: hipLaunchKernelGGL(get_rows_kernel<T_Q8_0>, grid, dim3(256), 0, st, a); break;
+        case T_Q4_K: hipLaunchKernelGGL(get_rows_kernel<T_Q4_K>, grid, dim3(256), 0, st, a); break;
+        case T_Q5_K: hipLaunchKernelGGL(get_rows_kernel<T_Q5_K>, grid, dim3(256), 0, st, a); break;
+        case T_Q6_K: hipLaunchKernelGGL(get_rows_kernel<T_Q6_K>, grid, dim3(256), 0, st, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// f32 -> Q4_0 / Q8_0 (GGML_OP_CPY into a quantized tensor; the reference GPU path is
+// cpy_f32_q, src/ggml-cuda/cpy.cu:66-94). One thread per 32-block, bit-exact with
+// quantize_row_q4_0_ref / quantize_row_q8_0_ref (src/ggml-quants.c:36-71, 199-222): the same
+// sequential max search, correctly rounded division, and separately rounded mul / add.
+// ------------------------------------------------------------------------------------------
+struct QuantArgs {
+    const uint8_t *src; int64_t nb01, nb02, nb03;        // f32 rows (nb00 == 4)
+    uint8_t *dst; int64_t nb1, nb2, nb3;                  // quantized rows (nb0 == block bytes)
+    int64_t ne0, ne1, ne2, ne3;
+};
+
+// fp32 -> fp16 bits, round to nearest even, sign of zero kept (GGML_FP32_TO_FP16)
+__device__ inline uint16_t f2h_rne(float f) {
+    const uint16_t h = __builtin_bit_cast(uint16_t, (_Float16)f);
+    return (uint16_t)(h | ((__builtin_bit_cast(uint32_t, f) >> 16) & 0x8000u));
+}
+
+template <int T>
+__global__ __launch_bounds__(256) void quantize_kernel(const QuantArgs a) {
+    const int64_t nb = a.ne0 / 32;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t nblocks = nb * a.ne1 * a.ne2 * a.ne3;
+    if (t >= nblocks) return;
+    int64_t r = t / nb;
+    const int64_t ib = t - r * nb;
+    const int64_t i1 = r % a.ne1; r /= a.ne1;
+    const int64_t i2 = r % a.ne2;
+    const int64_t i3 = r / a.ne2;
+    const float *x = reinterpret_cast<const float *>(a.src + i1 * a.nb01 + i2 * a.nb02 + i3 * a.nb03) + ib * 32;
+    uint8_t *y = a.dst + i1 * a.nb1 + i2 * a.nb2 + i3 * a.nb3 + ib * QT<T>::bytes;
+    float v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] = x[j];
+    if constexpr (T == T_Q4_0) {
+        float amax = 0.f, mx = 0.f;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            if (amax < fabsf(v[j])) { amax = fabsf(v[j]); mx = v[j]; }
+        }
+        // max / -8 is an exact power-of-two scaling: -(max * 0.125) rounds identically and keeps
+        // the -0.0 an all-zero block gets from the reference (d = 0.0f / -8)
+        const float d = -__fmul_rn(mx, 0.125f);
+        const float id = d != 0.f ? __fdiv_rn(1.f, d) : 0.f;
+        const uint16_t dh = f2h_rne(d);
+        y[0] = (uint8_t)(dh & 0xff);
+        y[1] = (uint8_t)(dh >> 8);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int xi0 = min(15, (int)(int8_t)(int)__fadd_rn(__fmul_rn(v[j], id), 8.5f));
+            const int xi1 = min(15, (int)(int8_t)(int)__fadd_rn(__fmul_rn(v[16 + j], id), 8.5f));
+            y[2 + j] = (uint8_t)(xi0 | (xi1 << 4));
+        }
+    } else {
+        float amax = 0.f;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(v[j]));
+        const float d = __fdiv_rn(amax, 127.f);
+        const float id = d != 0.f ? __fdiv_rn(1.f, d) : 0.f;
+        const uint16_t dh = f2h_rne(d);
+        y[0] = (uint8_t)(dh & 0xff);
+        y[1] = (uint8_t)(dh >> 8);
+#pragma unroll
+        for (int j = 0; j < 32; ++j) y[2 + j] = (uint8_t)(int8_t)roundf(__fmul_rn(v[j], id));
+    }
+}
+
+hipError_t quantize_launch(int type, const QuantArgs &a, hipStream_t st) {
+    const int64_t n = a.ne0 / 32 * a.ne1 * a.ne2 * a.ne3;
+    const dim3 grid((unsigned)((n + 255) / 256));
+    switch (type) {
+        case T_Q4_0: hipLaunchKernelGGL(quantize_kernel<T_Q4_0>, grid, dim3(256), 0, st, a); break;
+        case T_Q8_0: hipLaunchKernelGGL(quantize_kernel<T_Q8_0>, grid, dim3(256), 0, st, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 }  // namespace mi355x

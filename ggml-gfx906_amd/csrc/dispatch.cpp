@@ -25,6 +25,19 @@ bool mmvq_has_nc(int nc);
 bool mmvq_bigk(int K);
 hipError_t dequant_launch(int type, const void *src, float *dst, int64_t n, hipStream_t st);
 hipError_t mmq_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
+struct RowsArgs {
+    const uint8_t *src; int64_t nb01, nb02, nb03, ne01;
+    const uint8_t *idx; int64_t nb10, nb11, nb12, ne10, ne11;
+    uint8_t *dst; int64_t nb1, nb2, nb3;
+    int64_t ne00;
+};
+hipError_t get_rows_launch(int type, const RowsArgs &a, int64_t nrows, hipStream_t st);
+struct QuantArgs {
+    const uint8_t *src; int64_t nb01, nb02, nb03;
+    uint8_t *dst; int64_t nb1, nb2, nb3;
+    int64_t ne0, ne1, ne2, ne3;
+};
+hipError_t quantize_launch(int type, const QuantArgs &a, hipStream_t st);
 bool mmq_supported(int type, const MmArgs &a);
 
 static constexpr size_t LDS_LIMIT = 160 * 1024;
@@ -186,6 +199,58 @@ int dequantize(int type, const void *src, float *dst, int64_t n, hipStream_t st)
     return dequant_launch(type, src, dst, n, st) == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
 }
 
+// GET_ROWS (ggml_get_rows, reference src/ggml.c:3617-3637): a [ne00, ne01, ne02, ne03] hot type
+// or f32, rows [r, ne02, ne03] i32, dst [ne00, r, ne02, ne03] f32
+int check_get_rows(const TensorView &a, const TensorView &r, const TensorView &d) {
+    if (!(is_hot_quant(a.type) || a.type == T_F32) || r.type != T_I32 || d.type != T_F32) return GGML_MI355X_EINVAL;
+    const int blck = a.type == T_F32 ? 1 : type_blck(a.type);
+    if (a.ne[0] % blck != 0 || (int64_t)a.nb[0] != type_bytes(a.type) || r.nb[0] != 4 || d.nb[0] != 4) return GGML_MI355X_EINVAL;
+    if (a.ne[2] != r.ne[1] || a.ne[3] != r.ne[2] || r.ne[3] != 1) return GGML_MI355X_EINVAL;
+    if (d.ne[0] != a.ne[0] || d.ne[1] != r.ne[0] || d.ne[2] != r.ne[1] || d.ne[3] != r.ne[2]) return GGML_MI355X_EINVAL;
+    if (a.ne[1] <= 0 && r.ne[0] > 0) return GGML_MI355X_EINVAL;
+    if (r.ne[0] * r.ne[1] * r.ne[2] > 65535) return GGML_MI355X_EINVAL;   // grid.y
+    return GGML_MI355X_OK;
+}
+
+int get_rows(const TensorView &a, const TensorView &r, const TensorView &d, hipStream_t st) {
+    const int rc = check_get_rows(a, r, d);
+    if (rc != GGML_MI355X_OK) return rc;
+    const int64_t nrows = r.ne[0] * r.ne[1] * r.ne[2];
+    if (nrows == 0 || a.ne[0] == 0) return GGML_MI355X_OK;
+    RowsArgs g{};
+    g.src = static_cast<const uint8_t *>(a.data);
+    g.nb01 = (int64_t)a.nb[1]; g.nb02 = (int64_t)a.nb[2]; g.nb03 = (int64_t)a.nb[3]; g.ne01 = a.ne[1];
+    g.idx = static_cast<const uint8_t *>(r.data);
+    g.nb10 = (int64_t)r.nb[0]; g.nb11 = (int64_t)r.nb[1]; g.nb12 = (int64_t)r.nb[2];
+    g.ne10 = r.ne[0]; g.ne11 = r.ne[1];
+    g.dst = static_cast<uint8_t *>(d.data);
+    g.nb1 = (int64_t)d.nb[1]; g.nb2 = (int64_t)d.nb[2]; g.nb3 = (int64_t)d.nb[3];
+    g.ne00 = a.ne[0];
+    return get_rows_launch(a.type, g, nrows, st) == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
+}
+
+// f32 -> Q4_0 / Q8_0 (GGML_OP_CPY into a quantized tensor)
+int check_quantize(const TensorView &s, const TensorView &d) {
+    if (s.type != T_F32 || !(d.type == T_Q4_0 || d.type == T_Q8_0)) return GGML_MI355X_EINVAL;
+    for (int i = 0; i < 4; ++i)
+        if (s.ne[i] != d.ne[i]) return GGML_MI355X_EINVAL;
+    if (s.ne[0] % 32 != 0 || s.nb[0] != 4 || (int64_t)d.nb[0] != type_bytes(d.type)) return GGML_MI355X_EINVAL;
+    return GGML_MI355X_OK;
+}
+
+int quantize(const TensorView &s, const TensorView &d, hipStream_t st) {
+    const int rc = check_quantize(s, d);
+    if (rc != GGML_MI355X_OK) return rc;
+    if (s.ne[0] * s.ne[1] * s.ne[2] * s.ne[3] == 0) return GGML_MI355X_OK;
+    QuantArgs q{};
+    q.src = static_cast<const uint8_t *>(s.data);
+    q.nb01 = (int64_t)s.nb[1]; q.nb02 = (int64_t)s.nb[2]; q.nb03 = (int64_t)s.nb[3];
+    q.dst = static_cast<uint8_t *>(d.data);
+    q.nb1 = (int64_t)d.nb[1]; q.nb2 = (int64_t)d.nb[2]; q.nb3 = (int64_t)d.nb[3];
+    q.ne0 = s.ne[0]; q.ne1 = s.ne[1]; q.ne2 = s.ne[2]; q.ne3 = s.ne[3];
+    return quantize_launch(d.type, q, st) == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
+}
+
 // ------------------------------------------------------------------------------------------
 // scratch: grow-only device buffer, one per (device, stream) user
 // ------------------------------------------------------------------------------------------
@@ -252,6 +317,17 @@ int ggml_mi355x_mul_mat_id(const ggml_mi355x_tensor *as, const ggml_mi355x_tenso
 
 int ggml_mi355x_dequantize(int32_t type, const void *src, float *dst, int64_t n, void *stream) {
     return dequantize(type, src, dst, n, static_cast<hipStream_t>(stream));
+}
+
+int ggml_mi355x_get_rows(const ggml_mi355x_tensor *src0, const ggml_mi355x_tensor *rows, ggml_mi355x_tensor *dst,
+                         void *stream) {
+    if (!src0 || !rows || !dst) return GGML_MI355X_EINVAL;
+    return get_rows(view_of(src0), view_of(rows), view_of(dst), static_cast<hipStream_t>(stream));
+}
+
+int ggml_mi355x_quantize(const ggml_mi355x_tensor *src, ggml_mi355x_tensor *dst, void *stream) {
+    if (!src || !dst) return GGML_MI355X_EINVAL;
+    return quantize(view_of(src), view_of(dst), static_cast<hipStream_t>(stream));
 }
 
 int ggml_mi355x_supports_mul_mat(const ggml_mi355x_tensor *src0, const ggml_mi355x_tensor *src1) {

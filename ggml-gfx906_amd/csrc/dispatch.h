@@ -36,5 +36,9 @@ int mul_mat(const TensorView &a, const TensorView &b, const TensorView &d, hipSt
 int mul_mat_id(const TensorView &as, const TensorView &b, const TensorView &ids, const TensorView &d, hipStream_t st,
                Scratch &scratch);
 int dequantize(int type, const void *src, float *dst, int64_t n, hipStream_t st);
+int check_get_rows(const TensorView &a, const TensorView &rows, const TensorView &d);
+int get_rows(const TensorView &a, const TensorView &rows, const TensorView &d, hipStream_t st);
+int check_quantize(const TensorView &src, const TensorView &d);
+int quantize(const TensorView &src, const TensorView &d, hipStream_t st);
 
 }  // namespace mi355x

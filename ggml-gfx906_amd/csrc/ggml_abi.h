@@ -28,11 +28,13 @@ enum ggml_status { GGML_STATUS_ALLOC_FAILED = -2, GGML_STATUS_FAILED = -1, GGML_
 enum {
     GGMLABI_OP_NONE = 0,
     GGMLABI_OP_MUL_MAT = 28,
+    GGMLABI_OP_CPY = 33,
     GGMLABI_OP_MUL_MAT_ID = 29,
     GGMLABI_OP_RESHAPE = 35,
     GGMLABI_OP_VIEW = 36,
     GGMLABI_OP_PERMUTE = 37,
     GGMLABI_OP_TRANSPOSE = 38,
+    GGMLABI_OP_GET_ROWS = 39,
 };
 
 enum { GGMLABI_TYPE_F32 = 0, GGMLABI_TYPE_F16 = 1, GGMLABI_TYPE_I32 = 26 };

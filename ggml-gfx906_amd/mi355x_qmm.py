@@ -56,6 +56,8 @@ def lib():
         L.ggml_mi355x_mul_mat_id.argtypes = [P, P, P, P, C.c_void_p]
         L.ggml_mi355x_dequantize.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
         L.ggml_mi355x_supports_mul_mat.argtypes = [P, P]
+        L.ggml_mi355x_get_rows.argtypes = [P, P, P, C.c_void_p]
+        L.ggml_mi355x_quantize.argtypes = [P, P, C.c_void_p]
         L.ggml_mi355x_strerror.restype = C.c_char_p
         L.ggml_mi355x_strerror.argtypes = [C.c_int]
         L.ggml_backend_init.restype = C.c_void_p
@@ -109,6 +111,16 @@ def _stream_ptr(stream) -> int | None:
 
 def mul_mat(a: MmTensor, b: MmTensor, d: MmTensor, stream=None) -> None:
     _check(lib().ggml_mi355x_mul_mat(C.byref(a), C.byref(b), C.byref(d), _stream_ptr(stream)), "mul_mat")
+
+
+def get_rows(a: MmTensor, rows: MmTensor, d: MmTensor, stream=None) -> None:
+    """dst = get_rows(a, rows) (GGML_OP_GET_ROWS) on the device"""
+    _check(lib().ggml_mi355x_get_rows(C.byref(a), C.byref(rows), C.byref(d), _stream_ptr(stream)), "get_rows")
+
+
+def quantize(src: MmTensor, dst: MmTensor, stream=None) -> None:
+    """dst (Q4_0 / Q8_0) = quantize_row_*_ref(src f32) on the device (GGML_OP_CPY f32 -> q)"""
+    _check(lib().ggml_mi355x_quantize(C.byref(src), C.byref(dst), _stream_ptr(stream)), "quantize")
 
 
 def mul_mat_id(a: MmTensor, b: MmTensor, ids: MmTensor, d: MmTensor, stream=None) -> None:

@@ -95,6 +95,20 @@ GGML_MI355X_API int ggml_mi355x_mul_mat_id(const ggml_mi355x_tensor *as, const g
  * a multiple of the block size. */
 GGML_MI355X_API int ggml_mi355x_dequantize(int32_t type, const void *src, float *dst, int64_t n, void *stream);
 
+/* dst = get_rows(src0, rows) with GGML_OP_GET_ROWS semantics (ggml_get_rows, reference
+ * src/ggml.c:3617-3637; CPU src/ggml-cpu/ops.cpp:5121-5163): src0 [ne00, ne01, ne02, ne03] of a
+ * hot quant type or f32, rows [r, ne02, ne03] i32, dst [ne00, r, ne02, ne03] f32, each row the
+ * bit-exact dequantize_row_* of the selected src0 row. Replaces get_rows_cuda
+ * (src/ggml-cuda/getrows.cu). Indices outside [0, ne01) are clamped (the reference asserts). */
+GGML_MI355X_API int ggml_mi355x_get_rows(const ggml_mi355x_tensor *src0, const ggml_mi355x_tensor *rows,
+                                         ggml_mi355x_tensor *dst, void *stream);
+
+/* dst = src converted f32 -> Q4_0 or Q8_0 (GGML_OP_CPY into a quantized tensor), bit-exact with
+ * quantize_row_q4_0_ref / quantize_row_q8_0_ref (reference src/ggml-quants.c:36-71, 199-222).
+ * Same shapes, strided 4-d views with contiguous rows; ne0 a multiple of 32. Replaces
+ * ggml_cpy_f32_q4_0_cuda / ggml_cpy_f32_q8_0_cuda (src/ggml-cuda/cpy.cu). */
+GGML_MI355X_API int ggml_mi355x_quantize(const ggml_mi355x_tensor *src, ggml_mi355x_tensor *dst, void *stream);
+
 /* Same predicate the backend's supports_op uses for MUL_MAT / MUL_MAT_ID on these operands
  * (replaces the MUL_MAT arm of ggml_backend_cuda_device_supports_op, ggml-cuda.cu:3270-3330). */
 GGML_MI355X_API int ggml_mi355x_supports_mul_mat(const ggml_mi355x_tensor *src0, const ggml_mi355x_tensor *src1);
