@@ -39,6 +39,8 @@ struct QuantArgs {
 };
 hipError_t quantize_launch(int type, const QuantArgs &a, hipStream_t st);
 bool mmq_supported(int type, const MmArgs &a);
+bool mmq_id_supported(int type, const MmArgs &a);
+hipError_t mmq_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
 
 static constexpr size_t LDS_LIMIT = 160 * 1024;
 
@@ -165,8 +167,11 @@ int check_mul_mat_id(const TensorView &as, const TensorView &b, const TensorView
     return GGML_MI355X_OK;
 }
 
+// (slot, token) pairs from which the grouped MFMA path beats one mat-vec per pair
+static const int MMQ_ID_MIN_PAIRS = 64;
+
 int mul_mat_id(const TensorView &as, const TensorView &b, const TensorView &ids, const TensorView &d, hipStream_t st,
-               Scratch &) {
+               Scratch &scratch) {
     const int rc = check_mul_mat_id(as, b, ids, d);
     if (rc != GGML_MI355X_OK) return rc;
     if (ids.ne[0] == 0 || ids.ne[1] == 0 || as.ne[1] == 0) return GGML_MI355X_OK;
@@ -189,7 +194,9 @@ int mul_mat_id(const TensorView &as, const TensorView &b, const TensorView &ids,
     m.ne11_b = (int)b.ne[1];
     m.n_expert = (int)as.ne[2];
     m.x_aligned16 = aligned16(b.data, m.nb11, m.nb12, m.nb13);
-    const hipError_t e = mmvq_id_launch(as.type, m, 1, st);
+    static const int min_pairs = getenv("GGML_MI355X_MMQ_ID_MIN") ? atoi(getenv("GGML_MI355X_MMQ_ID_MIN")) : MMQ_ID_MIN_PAIRS;
+    const bool grouped = m.n_used * m.n_tok >= min_pairs && mmq_id_supported(as.type, m);
+    const hipError_t e = grouped ? mmq_id_launch(as.type, m, st, scratch) : mmvq_id_launch(as.type, m, 1, st);
     return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
 }
 

@@ -215,11 +215,29 @@ template <> struct Deq8<T_Q6_K> {
 // ------------------------------------------------------------------------------------------
 // one workgroup per token (K spread over 256 threads, 4 float4 loads in flight per thread);
 // scalar loads when src1 rows are not 16-B aligned; 8-B stores
-__global__ __launch_bounds__(256) void mmq_convert_x(const MmArgs a, _Float16 *x16, float *xinv, int Kpad) {
+// MUL_MAT_ID grouping (expert-sorted (slot, token) pairs), built on the device by moe_prep:
+//   offsets[e] .. offsets[e+1]  : sorted positions of expert e's pairs
+//   tile_off[e]                 : first token tile of expert e (prefix sum of ceil(count / BN))
+//   pos_pair[pos]               : pair index t * n_used + slot at sorted position pos
+struct MoeMap {
+    const int *offsets, *tile_off, *pos_pair;
+    int n_expert, n_used;
+};
+
+// pos_pair == nullptr: plain MUL_MAT (row tok of slice blockIdx.y); otherwise row pos of the
+// expert-sorted pair list, gathered from src1 column (slot % ne11, token)
+__global__ __launch_bounds__(256) void mmq_convert_x(const MmArgs a, _Float16 *x16, float *xinv, int Kpad,
+                                                     const int *pos_pair) {
     const int tok = blockIdx.x, slice = blockIdx.y;
-    const int i12 = slice % a.ne12, i13 = slice / a.ne12;
-    const float *src = reinterpret_cast<const float *>(a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13 +
-                                                       (int64_t)tok * a.nb11);
+    const float *src;
+    if (pos_pair) {
+        const int pair = pos_pair[tok];
+        const int slot = pair % a.n_used, t = pair / a.n_used;
+        src = reinterpret_cast<const float *>(a.x + (int64_t)(slot % a.ne11_b) * a.nb11 + (int64_t)t * a.nb12);
+    } else {
+        const int i12 = slice % a.ne12, i13 = slice / a.ne12;
+        src = reinterpret_cast<const float *>(a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13 + (int64_t)tok * a.nb11);
+    }
     auto ld4f = [&](int k) -> float4 {
         if (k >= a.K) return make_float4(0.f, 0.f, 0.f, 0.f);   // K % 4 == 0
         if (a.x_aligned16) return *reinterpret_cast<const float4 *>(src + k);
@@ -303,9 +321,10 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_dst
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds_dst, 16, voff, 0, 0, 0);
 }
 
-template <int T, int BM, int BN, bool STAMP = false>
+template <int T, int BM, int BN, bool STAMP = false, bool IDS = false>
 __global__ __launch_bounds__(MQ_THREADS) void mmq_kernel(const MmArgs a, const _Float16 *__restrict__ x16,
-                                                         const float *__restrict__ xinv, int Kpad, uint32_t w_extent) {
+                                                         const float *__restrict__ xinv, int Kpad, uint32_t w_extent,
+                                                         const MoeMap moe) {
     constexpr int WGM = BM / 32;                 // waves along weight rows
     constexpr int WGN = 8 / WGM;                 // waves along tokens
     constexpr int TN = BN / WGN / 32;            // MFMA tiles per wave along tokens
@@ -320,16 +339,39 @@ __global__ __launch_bounds__(MQ_THREADS) void mmq_kernel(const MmArgs a, const _
 
     const int slice = blockIdx.z;
     const int i12 = slice % a.ne12, i13 = slice / a.ne12;
-    const uint8_t *wmat = a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03;
-    const _Float16 *xs = x16 + (int64_t)slice * a.M * Kpad;
-    uint8_t *dmat = a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3;
-    // rows past N and tokens past M read as zeros (buffer range check)
+    const uint8_t *wmat;
+    const _Float16 *xs;
+    uint8_t *dmat;
+    int tok0, tok_end;   // token rows [tok0, tok_end) of xs feed this workgroup
+    if constexpr (IDS) {
+        // grid.y is an upper bound on the token tiles of all experts; tile -> expert by a search
+        // of the prefix sums (empty experts share their successor's start, so "last e with
+        // tile_off[e] <= tile" is the non-empty one)
+        const int tile = blockIdx.y;
+        if (tile >= moe.tile_off[moe.n_expert]) return;   // whole workgroup, before any barrier
+        int lo = 0, hi = moe.n_expert - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (moe.tile_off[mid] <= tile) lo = mid; else hi = mid - 1;
+        }
+        wmat = a.w + (int64_t)lo * a.nb02;
+        xs = x16;
+        dmat = a.dst;
+        tok0 = moe.offsets[lo] + (tile - moe.tile_off[lo]) * BN;
+        tok_end = moe.offsets[lo + 1];
+    } else {
+        wmat = a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03;
+        xs = x16 + (int64_t)slice * a.M * Kpad;
+        dmat = a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3;
+        tok0 = blockIdx.y * BN;
+        tok_end = a.M;
+    }
+    // rows past N and tokens past tok_end read as zeros (buffer range check)
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void *)wmat, 0, w_extent, RSRC_W3);
     const __amdgpu_buffer_rsrc_t xr =
-        __builtin_amdgcn_make_buffer_rsrc((void *)xs, 0, (uint32_t)a.M * (uint32_t)Kpad * 2u, RSRC_W3);
+        __builtin_amdgcn_make_buffer_rsrc((void *)xs, 0, (uint32_t)tok_end * (uint32_t)Kpad * 2u, RSRC_W3);
 
     const int wrow0 = blockIdx.x * BM;
-    const int tok0 = blockIdx.y * BN;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int wm = wave % WGM, wn = wave / WGM;
@@ -467,13 +509,14 @@ __global__ __launch_bounds__(MQ_THREADS) void mmq_kernel(const MmArgs a, const _
 
     // epilogue: lane holds weight row (lane & 31) and 16 tokens of each A tile; token scales are
     // read before any store (the compiler cannot prove dst does not alias them)
+    const float *xinv_s = IDS ? xinv : xinv + (int64_t)slice * a.M;
     float inv[TN][16];
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int tok = tok0 + wn * (TN * 32) + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * fh;
-            inv[j][r] = xinv[(int64_t)slice * a.M + min(tok, a.M - 1)];
+            inv[j][r] = xinv_s[min(tok, tok_end - 1)];
         }
     const int orow = wrow0 + wm * 32 + fr;
     if (orow < a.N) {
@@ -482,7 +525,16 @@ __global__ __launch_bounds__(MQ_THREADS) void mmq_kernel(const MmArgs a, const _
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int tok = tok0 + wn * (TN * 32) + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * fh;
-                if (tok < a.M) reinterpret_cast<float *>(dmat + (int64_t)tok * a.nb1)[orow] = acc[j][r] * inv[j][r];
+                if (tok < tok_end) {
+                    uint8_t *drow;
+                    if constexpr (IDS) {   // scatter back to dst[slot][token]
+                        const int pair = moe.pos_pair[tok];
+                        drow = dmat + (int64_t)(pair % moe.n_used) * a.nb1 + (int64_t)(pair / moe.n_used) * a.nb2;
+                    } else {
+                        drow = dmat + (int64_t)tok * a.nb1;
+                    }
+                    reinterpret_cast<float *>(drow)[orow] = acc[j][r] * inv[j][r];
+                }
             }
         }
     }
@@ -506,10 +558,11 @@ template <int T, int BM, int BN>
 static void launch_tile(const MmArgs &a, const _Float16 *x16, const float *xinv, int Kpad, int slices, hipStream_t st) {
     const dim3 grid((a.N + BM - 1) / BM, (a.M + BN - 1) / BN, slices);
     const uint32_t w_extent = (uint32_t)((int64_t)(a.N - 1) * a.nb01 + row_bytes(T, a.K));
+    const MoeMap none{};
     if (a.stamps && (size_t)grid.x * grid.y * grid.z * 64 <= 8 * 65536)
-        hipLaunchKernelGGL((mmq_kernel<T, BM, BN, true>), grid, dim3(MQ_THREADS), 0, st, a, x16, xinv, Kpad, w_extent);
+        hipLaunchKernelGGL((mmq_kernel<T, BM, BN, true>), grid, dim3(MQ_THREADS), 0, st, a, x16, xinv, Kpad, w_extent, none);
     else
-        hipLaunchKernelGGL((mmq_kernel<T, BM, BN>), grid, dim3(MQ_THREADS), 0, st, a, x16, xinv, Kpad, w_extent);
+        hipLaunchKernelGGL((mmq_kernel<T, BM, BN>), grid, dim3(MQ_THREADS), 0, st, a, x16, xinv, Kpad, w_extent, none);
 }
 
 template <int T>
@@ -547,7 +600,7 @@ hipError_t mmq_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratc
     if (!buf) return hipErrorOutOfMemory;
     _Float16 *x16 = reinterpret_cast<_Float16 *>(buf);
     float *xinv = reinterpret_cast<float *>(buf + x16_bytes);
-    hipLaunchKernelGGL(mmq_convert_x, dim3(a.M, slices), dim3(256), 0, st, a, x16, xinv, Kpad);
+    hipLaunchKernelGGL(mmq_convert_x, dim3(a.M, slices), dim3(256), 0, st, a, x16, xinv, Kpad, (const int *)nullptr);
     const int tile = pick_tile(a, slices);
     switch (type) {
         case T_Q4_0: launch_type<T_Q4_0>(tile, a, x16, xinv, Kpad, slices, st); break;
@@ -555,6 +608,81 @@ hipError_t mmq_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratc
         case T_Q4_K: launch_type<T_Q4_K>(tile, a, x16, xinv, Kpad, slices, st); break;
         case T_Q5_K: launch_type<T_Q5_K>(tile, a, x16, xinv, Kpad, slices, st); break;
         case T_Q6_K: launch_type<T_Q6_K>(tile, a, x16, xinv, Kpad, slices, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// MUL_MAT_ID on the MFMA tiles (prefill / many tokens): the (slot, token) pairs are grouped by
+// expert on the device (counting sort in LDS), their activation columns gathered into f16 rows
+// in that order, and every expert's rows run as token tiles of the same kernel; the epilogue
+// scatters each row back to dst[slot][token]. No host synchronisation: grid.y is the upper
+// bound ceil(P / BN) + n_expert and surplus workgroups exit at once. (Reference: the expert
+// grouping of ggml_compute_forward_mul_mat_id, src/ggml-cpu/ggml-cpu.c:1564-1579, and
+// ggml_cuda_mul_mat_id, src/ggml-cuda/ggml-cuda.cu:2092-2230.)
+// ------------------------------------------------------------------------------------------
+constexpr int MOE_MAX_EXPERTS = 1024;
+constexpr int MOE_BN = 64;                // token tile of the grouped path (128 x 64 tiles)
+
+__global__ __launch_bounds__(1024) void moe_prep(const MmArgs a, int *offsets, int *tile_off, int *pos_pair) {
+    __shared__ int cnt[MOE_MAX_EXPERTS], cur[MOE_MAX_EXPERTS];
+    const int E = a.n_expert, P = a.n_used * a.n_tok;
+    for (int e = threadIdx.x; e < E; e += 1024) cnt[e] = 0;
+    __syncthreads();
+    auto expert_of = [&](int p) {
+        const int slot = p % a.n_used, t = p / a.n_used;
+        const int ex = *reinterpret_cast<const int32_t *>(reinterpret_cast<const uint8_t *>(a.ids) + slot * a.ids_nb0 +
+                                                          (int64_t)t * a.ids_nb1);
+        return min(max(ex, 0), E - 1);     // host validates ids; never index out of bounds
+    };
+    for (int p = threadIdx.x; p < P; p += 1024) atomicAdd(&cnt[expert_of(p)], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int o = 0, tl = 0;
+        for (int e = 0; e < E; ++e) {
+            offsets[e] = o;
+            tile_off[e] = tl;
+            cur[e] = o;
+            o += cnt[e];
+            tl += (cnt[e] + MOE_BN - 1) / MOE_BN;
+        }
+        offsets[E] = o;
+        tile_off[E] = tl;
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < P; p += 1024) pos_pair[atomicAdd(&cur[expert_of(p)], 1)] = p;
+}
+
+bool mmq_id_supported(int type, const MmArgs &a) {
+    const int P = a.n_used * a.n_tok;
+    MmArgs b = a;
+    b.M = P;
+    return a.n_expert <= MOE_MAX_EXPERTS && mmq_supported(type, b);
+}
+
+hipError_t mmq_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch) {
+    const int Kpad = (a.K + MQ_BK - 1) / MQ_BK * MQ_BK;
+    const int P = a.n_used * a.n_tok, E = a.n_expert;
+    const size_t x16_bytes = ((size_t)P * Kpad * sizeof(_Float16) + 255) & ~(size_t)255;
+    const size_t inv_bytes = ((size_t)P * sizeof(float) + 255) & ~(size_t)255;
+    const size_t map_bytes = sizeof(int) * (2 * (size_t)(E + 1) + P);
+    uint8_t *buf = static_cast<uint8_t *>(scratch.get(x16_bytes + inv_bytes + map_bytes, st));
+    if (!buf) return hipErrorOutOfMemory;
+    _Float16 *x16 = reinterpret_cast<_Float16 *>(buf);
+    float *xinv = reinterpret_cast<float *>(buf + x16_bytes);
+    int *offsets = reinterpret_cast<int *>(buf + x16_bytes + inv_bytes);
+    int *tile_off = offsets + (E + 1);
+    int *pos_pair = tile_off + (E + 1);
+    hipLaunchKernelGGL(moe_prep, dim3(1), dim3(1024), 0, st, a, offsets, tile_off, pos_pair);
+    hipLaunchKernelGGL(mmq_convert_x, dim3(P, 1), dim3(256), 0, st, a, x16, xinv, Kpad, (const int *)pos_pair);
+    const MoeMap moe{offsets, tile_off, pos_pair, E, a.n_used};
+    const dim3 grid((a.N + 127) / 128, (P + MOE_BN - 1) / MOE_BN + E, 1);
+    const uint32_t w_extent = (uint32_t)((int64_t)(a.N - 1) * a.nb01 + row_bytes(type, a.K));
+    switch (type) {
+#define MQ_ID(TT) case TT: hipLaunchKernelGGL((mmq_kernel<TT, 128, MOE_BN, false, true>), grid, dim3(MQ_THREADS), 0, st, a, x16, xinv, Kpad, w_extent, moe); break;
+        MQ_ID(T_Q4_0) MQ_ID(T_Q8_0) MQ_ID(T_Q4_K) MQ_ID(T_Q5_K) MQ_ID(T_Q6_K)
+#undef MQ_ID
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

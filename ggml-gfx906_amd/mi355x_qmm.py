@@ -103,9 +103,12 @@ def tensor(t: int, ptr: int, ne, nb) -> MmTensor:
 
 
 def _stream_ptr(stream) -> int | None:
+    """hipStream_t for a call: None = torch's current stream; a torch Stream; or a raw handle"""
     if stream is None:
         import torch
         return torch.cuda.current_stream().cuda_stream
+    if hasattr(stream, "cuda_stream"):
+        return stream.cuda_stream
     return int(stream)
 
 

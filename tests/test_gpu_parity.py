@@ -196,3 +196,37 @@ def test_mmq_activation_range(mm, scale):
     wf = qref.dequantize(t, w, N * K).reshape(N, K).astype(np.float64)
     exact = (x.reshape(M_, K).astype(np.float64) @ wf.T).reshape(-1)
     assert qref.nmse(got.astype(np.float64), exact) <= 1e-5
+
+
+# ------------------------------------------------------------------------------------------
+# MUL_MAT_ID, grouped MFMA path (>= 64 (slot, token) pairs): experts sorted on the device
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("t", qref.HOT_TYPES, ids=lambda t: qref.NAMES[t])
+@pytest.mark.parametrize("bcast", [False, True], ids=["b_per_slot", "b_shared"])
+def test_mul_mat_id_grouped(mm, t, bcast):
+    K = 512 if qref.BLCK[t] == 256 else 96 * 3
+    N, E, U, T = 300, 8, 2, 200
+    w = qref.quantize(t, qref.fill_uniform(N * K * E, 51), n_per_row=K)
+    b_ne1 = 1 if bcast else U
+    x = qref.fill_uniform(K * b_ne1 * T, 52)
+    rng = np.random.default_rng(53)
+    ids = np.stack([rng.permutation(E)[:U] for _ in range(T)]).astype(np.int32)   # [T][U]
+    ids[: T // 2, 0] = 3                                                           # a hot expert
+    ids[: T // 2, 1] = np.where(ids[: T // 2, 1] == 3, 5, ids[: T // 2, 1])
+    a = G.Operand(t, w, [K, N, E, 1], qref.contiguous_nb(t, [K, N, E, 1]))
+    b = G.Operand(qref.F32, x, [K, b_ne1, T, 1], qref.contiguous_nb(qref.F32, [K, b_ne1, T, 1]))
+    iop = G.Operand(qref.I32, ids, [U, T, 1, 1], [4, 4 * U, 4 * U * T, 4 * U * T])
+    out_ne = [N, U, T, 1]
+    da, db, di = dev_bytes(w), dev_bytes(x), dev_bytes(ids)
+    nel = int(np.prod(out_ne))
+    dout = guarded_out(nel)
+    A = mm.tensor(t, da.data_ptr(), a.ne, a.nb)
+    B = mm.tensor(qref.F32, db.data_ptr(), b.ne, b.nb)
+    I = mm.tensor(qref.I32, di.data_ptr(), iop.ne, iop.nb)
+    D = mm.tensor(qref.F32, dout.data_ptr() + 4 * SENT, out_ne, qref.contiguous_nb(qref.F32, out_ne))
+    mm.mul_mat_id(A, B, I, D)
+    torch.cuda.synchronize()
+    got = check_guard(dout, nel)
+    want = G.oracle_mul_mat_id(a, b, iop, out_ne)
+    assert np.all(np.isfinite(got))
+    assert qref.nmse(got, want) <= 5e-4
