@@ -321,18 +321,21 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_dst
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds_dst, 16, voff, 0, 0, 0);
 }
 
-template <int T, int BM, int BN, bool STAMP = false, bool IDS = false>
-__global__ __launch_bounds__(MQ_THREADS) void mmq_kernel(const MmArgs a, const _Float16 *__restrict__ x16,
-                                                         const float *__restrict__ xinv, int Kpad, uint32_t w_extent,
-                                                         const MoeMap moe) {
-    constexpr int WGM = BM / 32;                 // waves along weight rows
-    constexpr int WGN = 8 / WGM;                 // waves along tokens
+// NW waves per workgroup; each wave owns TM x TN MFMA tiles of 32 x 32 (weight rows x tokens).
+// TM = TN = 2 (64 x 64 per wave) reads one LDS fragment per MFMA instead of two.
+template <int T, int BM, int BN, bool STAMP = false, bool IDS = false, int NW = 8, int TM = 1>
+__global__ __launch_bounds__(NW * 64) void mmq_kernel(const MmArgs a, const _Float16 *__restrict__ x16,
+                                                      const float *__restrict__ xinv, int Kpad, uint32_t w_extent,
+                                                      const MoeMap moe) {
+    constexpr int THREADS = NW * 64;
+    constexpr int WGM = BM / (32 * TM);          // waves along weight rows
+    constexpr int WGN = NW / WGM;                // waves along tokens
     constexpr int TN = BN / WGN / 32;            // MFMA tiles per wave along tokens
-    constexpr int U = BM / 64;                   // 8-weight units per thread per step
-    constexpr int V = BN / 64;                   // 1-KiB activation pieces per wave per step
+    constexpr int U = BM * 8 / THREADS;          // 8-weight units per thread per step
+    constexpr int V = BN / 8 / NW;               // 1-KiB activation pieces per wave per step
     constexpr int WB = BM * 128, XB = BN * 128;  // bytes of one W / X slot
     constexpr int VM_PHASE = U * LoadsPerUnit<T>::n + V;   // VMEM ops one wave issues per phase
-    static_assert(WGM * WGN == 8 && TN >= 1 && U >= 1 && V >= 1, "tile shape");
+    static_assert(WGM * WGN == NW && TN >= 1 && U >= 1 && V >= 1 && VM_PHASE < 64, "tile shape");
     __shared__ __align__(16) uint8_t lds[2 * WB + 3 * XB];   // one array: see the .s traps in the guide
     uint8_t *const wslot = lds;
     uint8_t *const xslot = lds + 2 * WB;
@@ -394,7 +397,7 @@ __global__ __launch_bounds__(MQ_THREADS) void mmq_kernel(const MmArgs a, const _
     int w_r[U], w_c[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const int g = tid + MQ_THREADS * u;
+        const int g = tid + THREADS * u;
         w_r[u] = g >> 3;
         w_c[u] = (g & 7) * 8;
         w_row[u] = (uint32_t)(wrow0 + w_r[u]) * (uint32_t)a.nb01;
@@ -404,7 +407,7 @@ __global__ __launch_bounds__(MQ_THREADS) void mmq_kernel(const MmArgs a, const _
     uint32_t x_off[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-        const int r = 8 * (wave + 8 * v) + (lane >> 3);
+        const int r = 8 * (wave + NW * v) + (lane >> 3);
         const int c = (lane & 7) ^ ((r >> 1) & 7);
         x_off[v] = ((uint32_t)(tok0 + r) * (uint32_t)Kpad + (uint32_t)c * 8u) * 2u;
     }
@@ -420,7 +423,7 @@ __global__ __launch_bounds__(MQ_THREADS) void mmq_kernel(const MmArgs a, const _
         const uint32_t k2 = (uint32_t)step * MQ_BK * 2u;
 #pragma unroll
         for (int v = 0; v < V; ++v)
-            dma16(xr, xslot + slot * XB + (wave + 8 * v) * 1024, x_off[v] + k2);
+            dma16(xr, xslot + slot * XB + (wave + NW * v) * 1024, x_off[v] + k2);
     };
     auto store_w = [&](Deq8<T> (&w)[U], int slot) {
 #pragma unroll
@@ -431,11 +434,13 @@ __global__ __launch_bounds__(MQ_THREADS) void mmq_kernel(const MmArgs a, const _
             *reinterpret_cast<u32x4 *>(W + swz(w_r[u], w_c[u] / 8)) = w[u].emit();
     };
 
-    float16v acc[TN];
+    float16v acc[TM][TN];
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     const int fr = lane & 31, fh = lane >> 5;
     auto compute = [&](int wsl, int xsl) {
@@ -444,13 +449,18 @@ __global__ __launch_bounds__(MQ_THREADS) void mmq_kernel(const MmArgs a, const _
 #pragma unroll
         for (int ks = 0; ks < MQ_BK / 16; ++ks) {
             const int c = 2 * ks + fh;
-            const half8 bw = *reinterpret_cast<const half8 *>(W + swz(wm * 32 + fr, c));
-            half8 ax[TN];
+            half8 bw[TM], ax[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                bw[i] = *reinterpret_cast<const half8 *>(W + swz(wm * (TM * 32) + 32 * i + fr, c));
 #pragma unroll
             for (int j = 0; j < TN; ++j)
                 ax[j] = *reinterpret_cast<const half8 *>(X + swz(wn * (TN * 32) + 32 * j + fr, c));
 #pragma unroll
-            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax[j], bw, acc[j], 0, 0, 0);
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax[j], bw[i], acc[i][j], 0, 0, 0);
         }
     };
     auto barrier = [&]() {
@@ -526,7 +536,9 @@ __global__ __launch_bounds__(MQ_THREADS) void mmq_kernel(const MmArgs a, const _
             const int tok = tok0 + wn * (TN * 32) + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * fh;
             inv[j][r] = xinv_s[min(tok, tok_end - 1)];
         }
-    const int orow = wrow0 + wm * 32 + fr;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+    const int orow = wrow0 + wm * (TM * 32) + 32 * i + fr;
     if (orow < a.N) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -541,10 +553,11 @@ __global__ __launch_bounds__(MQ_THREADS) void mmq_kernel(const MmArgs a, const _
                     } else {
                         drow = dmat + (int64_t)tok * a.nb1;
                     }
-                    reinterpret_cast<float *>(drow)[orow] = acc[j][r] * inv[j][r];
+                    reinterpret_cast<float *>(drow)[orow] = acc[i][j][r] * inv[j][r];
                 }
             }
         }
+    }
     }
 }
 
@@ -562,15 +575,15 @@ bool mmq_supported(int type, const MmArgs &a) {
     return a.nb01 >= row_bytes(type, a.K) && w_span < (1LL << 32) && (int64_t)(a.M + 128) * kpad * 2 < (1LL << 32);
 }
 
-template <int T, int BM, int BN>
+template <int T, int BM, int BN, int NW = 8, int TM = 1>
 static void launch_tile(const MmArgs &a, const _Float16 *x16, const float *xinv, int Kpad, int slices, hipStream_t st) {
     const dim3 grid((a.N + BM - 1) / BM, (a.M + BN - 1) / BN, slices);
     const uint32_t w_extent = (uint32_t)((int64_t)(a.N - 1) * a.nb01 + row_bytes(T, a.K));
     const MoeMap none{};
     if (a.stamps && (size_t)grid.x * grid.y * grid.z * 64 <= 8 * 65536)
-        hipLaunchKernelGGL((mmq_kernel<T, BM, BN, true>), grid, dim3(MQ_THREADS), 0, st, a, x16, xinv, Kpad, w_extent, none);
+        hipLaunchKernelGGL((mmq_kernel<T, BM, BN, true, false, NW, TM>), grid, dim3(NW * 64), 0, st, a, x16, xinv, Kpad, w_extent, none);
     else
-        hipLaunchKernelGGL((mmq_kernel<T, BM, BN>), grid, dim3(MQ_THREADS), 0, st, a, x16, xinv, Kpad, w_extent, none);
+        hipLaunchKernelGGL((mmq_kernel<T, BM, BN, false, false, NW, TM>), grid, dim3(NW * 64), 0, st, a, x16, xinv, Kpad, w_extent, none);
 }
 
 template <int T>
@@ -579,18 +592,22 @@ static void launch_type(int tile, const MmArgs &a, const _Float16 *x16, const fl
     switch (tile) {
         case 0: launch_tile<T, 64, 128>(a, x16, xinv, Kpad, slices, st); break;
         case 1: launch_tile<T, 128, 64>(a, x16, xinv, Kpad, slices, st); break;
+        case 3: launch_tile<T, 128, 128, 4, 2>(a, x16, xinv, Kpad, slices, st); break;
+        case 4: launch_tile<T, 64, 128, 4, 1>(a, x16, xinv, Kpad, slices, st); break;
         default: launch_tile<T, 128, 128>(a, x16, xinv, Kpad, slices, st); break;
     }
 }
 
-// tile shape; GGML_MI355X_MMQ_TILE
-// (64x128 | 128x64 | 128x128) overrides it for measurements
+// tile shape; GGML_MI355X_MMQ_TILE (64x128 | 128x64 | 128x128 | 128x128w4 | 64x128w4, the w4
+// forms with 4 waves of 64 x 64 or 32 x 128 tiles) overrides it for measurements
 static int pick_tile(const MmArgs &a, int slices) {
     static const char *env = getenv("GGML_MI355X_MMQ_TILE");
     if (env) {
         if (!strcmp(env, "64x128")) return 0;
         if (!strcmp(env, "128x64")) return 1;
         if (!strcmp(env, "128x128")) return 2;
+        if (!strcmp(env, "128x128w4")) return 3;
+        if (!strcmp(env, "64x128w4")) return 4;
     }
     auto wgs = [&](int bm, int bn) { return (int64_t)((a.N + bm - 1) / bm) * ((a.M + bn - 1) / bn) * slices; };
     // measured on MI355X (scripts/mmq_sweep.sh): 128x128 once it fills the chip, otherwise the
