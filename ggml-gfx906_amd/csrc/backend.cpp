@@ -121,6 +121,10 @@ bool is_view_op(int op) {
            op == GGMLABI_OP_TRANSPOSE;
 }
 
+// ggml node -> the graph_ops.hip description (ops around the matmuls);
+// false for an op that is not one of them
+bool graph_op_of(const struct ggml_tensor *node, GraphOp &g);
+
 bool is_empty(const struct ggml_tensor *t) {
     for (int i = 0; i < 4; ++i)
         if (t->ne[i] == 0) return true;
@@ -136,6 +140,39 @@ TensorView tv(const struct ggml_tensor *t) {
         v.nb[i] = t->nb[i];
     }
     return v;
+}
+
+bool graph_op_of(const struct ggml_tensor *node, GraphOp &g) {
+    g = GraphOp{};
+    switch (node->op) {
+        case GGMLABI_OP_ADD: g.op = GOP_ADD; break;
+        case GGMLABI_OP_SUB: g.op = GOP_SUB; break;
+        case GGMLABI_OP_MUL: g.op = GOP_MUL; break;
+        case GGMLABI_OP_DIV: g.op = GOP_DIV; break;
+        case GGMLABI_OP_NORM: g.op = GOP_NORM; break;
+        case GGMLABI_OP_SCALE: g.op = GOP_SCALE; break;
+        case GGMLABI_OP_DIAG_MASK_INF: g.op = GOP_DIAG_MASK_INF; break;
+        case GGMLABI_OP_DIAG_MASK_ZERO: g.op = GOP_DIAG_MASK_ZERO; break;
+        case GGMLABI_OP_SOFT_MAX: g.op = GOP_SOFT_MAX; break;
+        case GGMLABI_OP_CPY:
+        case GGMLABI_OP_CONT:
+        case GGMLABI_OP_DUP: g.op = GOP_CPY; break;
+        case GGMLABI_OP_MUL_MAT: g.op = GOP_MUL_MAT; break;
+        case GGMLABI_OP_UNARY:
+            if (node->op_params[0] != GGMLABI_UNARY_OP_GELU) return false;
+            g.op = GOP_GELU;
+            break;
+        default: return false;
+    }
+    for (int i = 0; i < 4; ++i) g.params[i] = node->op_params[i];
+    g.dst = tv(node);
+    // CPY's second source is its destination (node is a view of it); it is not an input
+    const int nsrc = node->op == GGMLABI_OP_CPY ? 1 : 3;
+    for (int i = 0; i < nsrc; ++i) {
+        g.has_src[i] = node->src[i] != nullptr;
+        if (g.has_src[i]) g.src[i] = tv(node->src[i]);
+    }
+    return true;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -305,14 +342,17 @@ enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
         struct ggml_tensor *node = gb.graph_node(g, i);
         if (is_empty(node) || is_view_op(node->op)) continue;
         int rc;
-        if (node->op == GGMLABI_OP_MUL_MAT) {
+        GraphOp gop;
+        if (node->op == GGMLABI_OP_MUL_MAT && is_hot_quant(node->src[0]->type)) {
             rc = mul_mat(tv(node->src[0]), tv(node->src[1]), tv(node), c->stream, c->scratch);
         } else if (node->op == GGMLABI_OP_MUL_MAT_ID) {
             rc = mul_mat_id(tv(node->src[0]), tv(node->src[1]), tv(node->src[2]), tv(node), c->stream, c->scratch);
         } else if (node->op == GGMLABI_OP_GET_ROWS) {
             rc = get_rows(tv(node->src[0]), tv(node->src[1]), tv(node), c->stream);
-        } else if (node->op == GGMLABI_OP_CPY) {
+        } else if (node->op == GGMLABI_OP_CPY && is_hot_quant(node->type)) {
             rc = quantize(tv(node->src[0]), tv(node), c->stream);   // node is the view of src[1]
+        } else if (graph_op_of(node, gop)) {
+            rc = run_graph_op(gop, c->stream);
         } else {
             fprintf(stderr, "[ggml-mi355x] unsupported op %d in graph (node %s)\n", node->op, node->name);
             return GGML_STATUS_FAILED;
@@ -410,6 +450,7 @@ bool dv_supports_op(ggml_backend_dev_t, const struct ggml_tensor *op) {
         case GGMLABI_OP_TRANSPOSE:
             return true;
         case GGMLABI_OP_MUL_MAT:
+            if (!is_hot_quant(op->src[0]->type)) break;   // f32 / f16 weights: graph_ops (below)
             return op->type == GGMLABI_TYPE_F32 && supports_mm_operands(op->src[0], op->src[1]) &&
                    op->src[1]->ne[2] % op->src[0]->ne[2] == 0 && op->src[1]->ne[3] % op->src[0]->ne[3] == 0;
         case GGMLABI_OP_MUL_MAT_ID:
@@ -420,10 +461,14 @@ bool dv_supports_op(ggml_backend_dev_t, const struct ggml_tensor *op) {
             return check_get_rows(tv(op->src[0]), tv(op->src[1]), tv(op)) == GGML_MI355X_OK;
         // f32 -> Q4_0 / Q8_0 copies (the reference GPU's cpy_f32_q subset of these types)
         case GGMLABI_OP_CPY:
-            return check_quantize(tv(op->src[0]), tv(op)) == GGML_MI355X_OK;
+            if (is_hot_quant(op->type)) return check_quantize(tv(op->src[0]), tv(op)) == GGML_MI355X_OK;
+            break;
         default:
-            return false;
+            break;
     }
+    // the f32 ops of the GPT-2 graph around the matmuls (graph_ops.hip)
+    GraphOp g;
+    return graph_op_of(op, g) && check_graph_op(g) == GGML_MI355X_OK;
 }
 
 bool dv_supports_buft(ggml_backend_dev_t d, ggml_backend_buffer_type_t bt) {

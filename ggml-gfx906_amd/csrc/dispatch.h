@@ -41,4 +41,19 @@ int get_rows(const TensorView &a, const TensorView &rows, const TensorView &d, h
 int check_quantize(const TensorView &src, const TensorView &d);
 int quantize(const TensorView &src, const TensorView &d, hipStream_t st);
 
+// the f32 graph ops around the matmuls (graph_ops.hip)
+enum GraphOpKind {
+    GOP_ADD, GOP_SUB, GOP_MUL, GOP_DIV, GOP_NORM, GOP_SCALE, GOP_DIAG_MASK_INF, GOP_DIAG_MASK_ZERO,
+    GOP_SOFT_MAX, GOP_GELU, GOP_CPY, GOP_MUL_MAT,
+};
+struct GraphOp {
+    int op;                 // GraphOpKind
+    int32_t params[4];      // the node's op_params[0..3] (eps, scale/bias, n_past, ...)
+    TensorView dst;
+    TensorView src[3];
+    bool has_src[3];
+};
+int check_graph_op(const GraphOp &g);
+int run_graph_op(const GraphOp &g, hipStream_t st);
+
 }  // namespace mi355x

@@ -27,15 +27,30 @@ enum ggml_status { GGML_STATUS_ALLOC_FAILED = -2, GGML_STATUS_FAILED = -1, GGML_
 // only the op codes this backend inspects (values from include/ggml.h's enum ggml_op)
 enum {
     GGMLABI_OP_NONE = 0,
+    GGMLABI_OP_DUP = 1,
+    GGMLABI_OP_ADD = 2,
+    GGMLABI_OP_SUB = 6,
+    GGMLABI_OP_MUL = 7,
+    GGMLABI_OP_DIV = 8,
+    GGMLABI_OP_NORM = 23,
     GGMLABI_OP_MUL_MAT = 28,
-    GGMLABI_OP_CPY = 33,
     GGMLABI_OP_MUL_MAT_ID = 29,
+    GGMLABI_OP_SCALE = 31,
+    GGMLABI_OP_CPY = 33,
+    GGMLABI_OP_CONT = 34,
     GGMLABI_OP_RESHAPE = 35,
     GGMLABI_OP_VIEW = 36,
     GGMLABI_OP_PERMUTE = 37,
     GGMLABI_OP_TRANSPOSE = 38,
     GGMLABI_OP_GET_ROWS = 39,
+    GGMLABI_OP_DIAG_MASK_INF = 43,
+    GGMLABI_OP_DIAG_MASK_ZERO = 44,
+    GGMLABI_OP_SOFT_MAX = 45,
+    GGMLABI_OP_UNARY = 78,
 };
+
+// enum ggml_unary_op (include/ggml.h), the value in op_params[0] of a GGML_OP_UNARY node
+enum { GGMLABI_UNARY_OP_GELU = 8 };
 
 enum { GGMLABI_TYPE_F32 = 0, GGMLABI_TYPE_F16 = 1, GGMLABI_TYPE_I32 = 26 };
 

@@ -30,6 +30,19 @@
 int main() {
     std::printf("api_version %d\n", (int)API_VERSION);
     E(GGMLABI_OP_NONE, GGML_OP_NONE)
+    E(GGMLABI_OP_DUP, GGML_OP_DUP)
+    E(GGMLABI_OP_ADD, GGML_OP_ADD)
+    E(GGMLABI_OP_SUB, GGML_OP_SUB)
+    E(GGMLABI_OP_MUL, GGML_OP_MUL)
+    E(GGMLABI_OP_DIV, GGML_OP_DIV)
+    E(GGMLABI_OP_NORM, GGML_OP_NORM)
+    E(GGMLABI_OP_SCALE, GGML_OP_SCALE)
+    E(GGMLABI_OP_CONT, GGML_OP_CONT)
+    E(GGMLABI_OP_DIAG_MASK_INF, GGML_OP_DIAG_MASK_INF)
+    E(GGMLABI_OP_DIAG_MASK_ZERO, GGML_OP_DIAG_MASK_ZERO)
+    E(GGMLABI_OP_SOFT_MAX, GGML_OP_SOFT_MAX)
+    E(GGMLABI_OP_UNARY, GGML_OP_UNARY)
+    E(GGMLABI_UNARY_OP_GELU, GGML_UNARY_OP_GELU)
     E(GGMLABI_OP_MUL_MAT, GGML_OP_MUL_MAT)
     E(GGMLABI_OP_MUL_MAT_ID, GGML_OP_MUL_MAT_ID)
     E(GGMLABI_OP_CPY, GGML_OP_CPY)

@@ -3,7 +3,7 @@
 # Each step runs under its own time limit; a crash-class exit (abort, segfault, timeout,
 # kill) ends the session so nothing else touches a possibly faulted GPU. Assertion failures
 # (exit 1) do not stop the later measurement steps.
-#   scripts/gpu_session.sh <step> [<step> ...]   steps: info tests smoke tbo bench prof
+#   scripts/gpu_session.sh <step> [<step> ...]   steps: info tests smoke tbo tbo-<OP> bench prof
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
@@ -30,6 +30,7 @@ for step in "$@"; do
         tboid) run tboid 900 env GGML_BACKEND_PATH=$PWD/ggml-gfx906_amd/libggml-hip-mi355x.so ./oracle/_ref/test-backend-ops test -o MUL_MAT_ID -b MI355X0 ;;
         tbogr) run tbogr 900 env GGML_BACKEND_PATH=$PWD/ggml-gfx906_amd/libggml-hip-mi355x.so ./oracle/_ref/test-backend-ops test -o GET_ROWS -b MI355X0 ;;
         tbocpy) run tbocpy 900 env GGML_BACKEND_PATH=$PWD/ggml-gfx906_amd/libggml-hip-mi355x.so ./oracle/_ref/test-backend-ops test -o CPY -b MI355X0 ;;
+        tbo-*) op=${step#tbo-}; run "tbo_$op" 900 env GGML_BACKEND_PATH=$PWD/ggml-gfx906_amd/libggml-hip-mi355x.so ./oracle/_ref/test-backend-ops test -o "$op" -b MI355X0 ;;
         bench) run bench 600 python bench.py ;;
         prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --no-extra --cpu-seconds 1 ;;
         pmc)   run pmc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/pmc -o pmc -- python bench.py --no-extra --cpu-seconds 1 --steps 5 --warmup 1 ;;
