@@ -250,11 +250,6 @@ __global__ __launch_bounds__(256) void soft_max_kernel(const DevT d, const DevT 
 // the fp16 table lookup, i.e. fp16(gelu_tanh(fp16(x))) with the table built in f32
 // (ggml-cpu.c:3542).
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ float gelu_ref(float x) {
-    constexpr float GELU_COEF_A = 0.044715f;
-    constexpr float SQRT_2_OVER_PI = 0.79788456080286535587989211986876f;
-    return 0.5f * x * (1.0f + tanhf(SQRT_2_OVER_PI * x * (1.0f + GELU_COEF_A * x * x)));
-}
 
 __global__ __launch_bounds__(256) void gelu_kernel(const DevT d, const DevT a, int64_t rows) {
     for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
@@ -264,11 +259,7 @@ __global__ __launch_bounds__(256) void gelu_kernel(const DevT d, const DevT a, i
         char *pd = d.p + i1 * d.nb[1] + i2 * d.nb[2] + i3 * d.nb[3];
         for (int64_t i0 = threadIdx.x; i0 < d.ne[0]; i0 += 256) {
             const float x = *reinterpret_cast<const float *>(pa + i0 * a.nb[0]);
-            float y;
-            if (x <= -10.0f) y = 0.0f;
-            else if (x >= 10.0f) y = x;
-            else y = h2f_dev(f2h_dev(gelu_ref(h2f_dev(f2h_dev(x)))));
-            *reinterpret_cast<float *>(pd + i0 * d.nb[0]) = y;
+            *reinterpret_cast<float *>(pd + i0 * d.nb[0]) = gelu_ggml(x);
         }
     }
 }

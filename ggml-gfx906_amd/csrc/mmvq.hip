@@ -1,565 +1,8 @@
-// mmvq.hip — quantized mat-vec (decode, ne11 <= 8) for gfx950.
-//
-// Replaces the reference's mul_mat_vec_q / quantize_q8_1 pair (src/ggml-cuda/mmvq.cu:139-226,
-// quantize.cu:4-48) with a CDNA4-first design:
-//
-//  * one 512-thread workgroup = 8 waves; each wave owns RPW consecutive weight rows;
-//  * a lane owns a fixed 64-weight "slot" of K for every row it touches (Q4_0/Q8_0: two
-//    32-blocks; Q4_K/Q5_K: one 64-chunk of a super-block; Q6_K: a quarter of a 128-half), so
-//    a wave's weight stream is a handful of wide (dwordx4) loads per row, issued for all RPW
-//    rows up front, straight to VGPRs (no LDS round trip for the once-read weights);
-//  * src1 is quantized to int8 per 32-block (d = amax/127, round-to-nearest-even) once per
-//    workgroup into LDS, in a slot-interleaved layout so lane s reads its 64 activations with
-//    4 conflict-free ds_read_b128. Quantization is ~2 VALU per value: one FMA against the
-//    1.5*2^23 magic constant rounds and biases, v_perm_b32 packs bytes, v_dot4_u32_u8 sums;
-//  * beside the bytes sit d, d*sum(q) per 32-block and d*sum(q) per 16-run, so the zero-point
-//    terms of Q4_0 (q-8), Q6_K (q-32) and the Q4_K/Q5_K mins cost one FMA per block instead of
-//    a per-byte fix-up;
-//  * integer block dots on v_dot4_i32_i8, fp32 scale accumulation per block — the reference's
-//    per-block arithmetic (src/ggml-cpu/quants.c:115-758);
-//  * cross-lane reduction by a butterfly transpose on DPP / permlane swaps: RPW*NC partial
-//    sums per lane collapse to one value per lane without touching LDS.
-//
-// Templated on <type, NC columns, RPW rows per wave, IDS = MUL_MAT_ID routing, RAG, XA>.
-#include <algorithm>
-#include <cstdlib>
-
-#include "qcommon.h"
-#include "qmm_args.h"
+// mmvq.hip — launchers of the quantized mat-vec kernel (mmvq_impl.h) for plain MUL_MAT and
+// MUL_MAT_ID. The fused decode-layer instantiations live in mmvq_fused.hip.
+#include "mmvq_impl.h"
 
 namespace mi355x {
-
-constexpr int MMVQ_WAVES = 8;
-constexpr int MMVQ_THREADS = MMVQ_WAVES * WAVE;
-
-// ------------------------------------------------------------------------------------------
-// slot geometry: K-chunk (16 activations) q  <->  (slot s, part j)
-// ------------------------------------------------------------------------------------------
-template <int T> struct SlotMap {
-    // slot s covers activations [64 s, 64 s + 64): parts are consecutive 16-chunks
-    __device__ static inline void place(int q, int &s, int &j) { s = q >> 2; j = q & 3; }
-};
-template <> struct SlotMap<T_Q6_K> {
-    // slot s = 4 sb + 2 h + p covers 256 sb + 128 h + 16 p + 32 j + [0,16), j = 0..3
-    __device__ static inline void place(int q, int &s, int &j) {
-        const int sb = q >> 4, r = q & 15, h = r >> 3, r2 = r & 7;
-        j = r2 >> 1;
-        s = 4 * sb + 2 * h + (r2 & 1);
-    }
-};
-
-// ------------------------------------------------------------------------------------------
-// activation quantization into LDS (per column m, Kpad = K rounded up to 64):
-//   xq  : int8 [Kpad]      slot-interleaved: chunk (s, j) at (j * nslots + s) * 16
-//   xd  : f32  [Kpad/32]   block scale d = amax / 127
-//   xs  : f32  [Kpad/32]   d * sum(q) over the 32-block
-//   x16 : f32  [Kpad/16]   d * sum(q) over each 16-run
-// Work split: 4 lanes per 32-block (8 values each, DPP inside the quad); a round covers
-// MMVQ_THREADS/4 blocks; loads of a round are issued before its arithmetic.
-// ------------------------------------------------------------------------------------------
-struct XSmem {
-    int8_t *xq;
-    float *xd, *xs, *x16;
-};
-
-__device__ __forceinline__ XSmem xsmem(uint8_t *smem, int Kpad, int nc) {
-    XSmem s;
-    s.xq = reinterpret_cast<int8_t *>(smem);
-    s.xd = reinterpret_cast<float *>(smem + (size_t)nc * Kpad);
-    s.xs = s.xd + nc * (Kpad / 32);
-    s.x16 = s.xs + nc * (Kpad / 32);
-    return s;
-}
-
-constexpr int XR_STRIDE = MMVQ_THREADS / 4;
-
-// Branch-free: the address is clamped into the row and out-of-range values are zeroed by a
-// select, so every lane issues the same loads. (A load under a branch makes the compiler's
-// in-order vmcnt bookkeeping ambiguous and it then waits for ALL outstanding loads — which
-// would include the weight stream.)
-template <bool XA>
-__device__ __forceinline__ void xblock_load(const MmArgs &a, const uint8_t *xcol, int kb, float4 &v0, float4 &v1) {
-    const int k0 = kb * 32 + (threadIdx.x & 3) * 8;
-    const float *src = reinterpret_cast<const float *>(xcol) + min(k0, a.K - 8);
-    if constexpr (XA) {
-        v0 = reinterpret_cast<const float4 *>(src)[0];
-        v1 = reinterpret_cast<const float4 *>(src)[1];
-    } else {
-        v0 = make_float4(src[0], src[1], src[2], src[3]);
-        v1 = make_float4(src[4], src[5], src[6], src[7]);
-    }
-    const bool in = k0 < a.K;
-    v0.x = in ? v0.x : 0.f; v0.y = in ? v0.y : 0.f; v0.z = in ? v0.z : 0.f; v0.w = in ? v0.w : 0.f;
-    v1.x = in ? v1.x : 0.f; v1.y = in ? v1.y : 0.f; v1.z = in ? v1.z : 0.f; v1.w = in ? v1.w : 0.f;
-}
-
-template <int T>
-__device__ __forceinline__ void xblock_store(int Kpad, int kb, const float4 &v0, const float4 &v1, int8_t *xq,
-                                             float *xd, float *xs, float *x16) {
-    const int sub = threadIdx.x & 3;
-    float amax = fmaxf(fmaxf(fmaxf(fabsf(v0.x), fabsf(v0.y)), fmaxf(fabsf(v0.z), fabsf(v0.w))),
-                       fmaxf(fmaxf(fabsf(v1.x), fabsf(v1.y)), fmaxf(fabsf(v1.z), fabsf(v1.w))));
-    amax = fmaxf(amax, dpp_f<DPP_XOR1>(amax));
-    amax = fmaxf(amax, dpp_f<DPP_XOR2>(amax));
-    const float d = amax * (1.0f / 127.f);
-    const float id = amax > 0.f ? 127.f * __builtin_amdgcn_rcpf(amax) : 0.f;
-    // t = x*id + (1.5*2^23 + 128): the FMA rounds to nearest-even into the mantissa, so the
-    // low byte of t's bits is 128 + q with q in [-127, 127]
-    constexpr float MAGIC = 12582912.0f + 128.0f;
-    const uint32_t b0 = __builtin_bit_cast(uint32_t, __builtin_fmaf(v0.x, id, MAGIC));
-    const uint32_t b1 = __builtin_bit_cast(uint32_t, __builtin_fmaf(v0.y, id, MAGIC));
-    const uint32_t b2 = __builtin_bit_cast(uint32_t, __builtin_fmaf(v0.z, id, MAGIC));
-    const uint32_t b3 = __builtin_bit_cast(uint32_t, __builtin_fmaf(v0.w, id, MAGIC));
-    const uint32_t b4 = __builtin_bit_cast(uint32_t, __builtin_fmaf(v1.x, id, MAGIC));
-    const uint32_t b5 = __builtin_bit_cast(uint32_t, __builtin_fmaf(v1.y, id, MAGIC));
-    const uint32_t b6 = __builtin_bit_cast(uint32_t, __builtin_fmaf(v1.z, id, MAGIC));
-    const uint32_t b7 = __builtin_bit_cast(uint32_t, __builtin_fmaf(v1.w, id, MAGIC));
-    const uint32_t w0 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(b3, b2, 0x0c0c0400u), __builtin_amdgcn_perm(b1, b0, 0x0c0c0400u), 0x05040100u);
-    const uint32_t w1 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(b7, b6, 0x0c0c0400u), __builtin_amdgcn_perm(b5, b4, 0x0c0c0400u), 0x05040100u);
-    // biased bytes (128 + q): sum(q) = udot4(bytes, 1) - 4*128 per dword
-    const int qs = (int)__builtin_amdgcn_udot4(w0, 0x01010101u, __builtin_amdgcn_udot4(w1, 0x01010101u, 0u, false), false) - 1024;
-    int s, j;
-    SlotMap<T>::place(kb * 2 + (sub >> 1), s, j);
-    const int nslots = Kpad / 64;
-    *reinterpret_cast<uint2 *>(xq + (size_t)(j * nslots + s) * 16 + (sub & 1) * 8) = make_uint2(w0 ^ 0x80808080u, w1 ^ 0x80808080u);
-    float fs = (float)qs;
-    fs += dpp_f<DPP_XOR1>(fs);              // 16-run sum (lane pairs 0-1 / 2-3)
-    if ((sub & 1) == 0) x16[kb * 2 + (sub >> 1)] = d * fs;
-    fs += dpp_f<DPP_XOR2>(fs);              // 32-block sum
-    if (sub == 0) {
-        xd[kb] = d;
-        xs[kb] = d * fs;
-    }
-}
-
-// ------------------------------------------------------------------------------------------
-// per-type weight fragment: load (raw bytes of one slot of one row) and dot with a column.
-//   X  : 16 dwords = the slot's 64 int8 activations (parts j = 0..3)
-//   dx : block scales of the slot's 32-blocks (2, or 4 for Q6_K)
-//   sx : d*sum(q): per 32-block (Q4_0, Q4_K, Q5_K) or per 16-run (Q6_K)
-// ------------------------------------------------------------------------------------------
-template <int T> struct Frag;
-
-// Q4_0: slot = blocks 2s, 2s+1 (36 contiguous bytes); sum (q-8)*x = sum q*x - 8 sum x
-template <> struct Frag<T_Q4_0> {
-    uint32_t D[9];
-    template <bool RAG>
-    __device__ inline void load(const uint8_t *row, int s, int nblk) {
-        const uint8_t *p = row + (size_t)s * 36;
-        ld16(p, D);
-        if (!RAG || 2 * s + 1 < nblk) {
-            ld16(p + 16, D + 4);
-            D[8] = ld4(p + 32);
-        } else {                     // ragged tail: K % 64 == 32, second block absent
-            D[4] = ld2(p + 16);
-            D[5] = D[6] = D[7] = D[8] = 0;
-        }
-    }
-    __device__ inline void zero() { for (int i = 0; i < 9; ++i) D[i] = 0; }
-    __device__ inline float dot(const uint32_t X[16], const float *dx, const float *sx) const {
-        const float d0 = h2f((uint16_t)(D[0] & 0xffff));
-        const float d1 = h2f((uint16_t)(D[4] >> 16));
-        int s0 = 0, s1 = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t q0 = align2(D[i + 1], D[i]);      // qs of block 0 at byte 2
-            s0 = dot4(q0 & 0x0f0f0f0fu, X[i], s0);
-            s0 = dot4((q0 >> 4) & 0x0f0f0f0fu, X[4 + i], s0);
-            const uint32_t q1 = D[5 + i];                   // qs of block 1 at byte 20
-            s1 = dot4(q1 & 0x0f0f0f0fu, X[8 + i], s1);
-            s1 = dot4((q1 >> 4) & 0x0f0f0f0fu, X[12 + i], s1);
-        }
-        return d0 * __builtin_fmaf(dx[0], (float)s0, -8.f * sx[0]) + d1 * __builtin_fmaf(dx[1], (float)s1, -8.f * sx[1]);
-    }
-};
-
-// Q8_0: slot = blocks 2s, 2s+1 (68 contiguous bytes)
-template <> struct Frag<T_Q8_0> {
-    uint32_t D[17];
-    template <bool RAG>
-    __device__ inline void load(const uint8_t *row, int s, int nblk) {
-        const uint8_t *p = row + (size_t)s * 68;
-        ld16(p, D);
-        ld16(p + 16, D + 4);
-        if (!RAG || 2 * s + 1 < nblk) {
-            ld16(p + 32, D + 8);
-            ld16(p + 48, D + 12);
-            D[16] = ld4(p + 64);
-        } else {
-            D[8] = ld2(p + 32);
-            for (int i = 9; i < 17; ++i) D[i] = 0;
-        }
-    }
-    __device__ inline void zero() { for (int i = 0; i < 17; ++i) D[i] = 0; }
-    __device__ inline float dot(const uint32_t X[16], const float *dx, const float *) const {
-        const float d0 = h2f((uint16_t)(D[0] & 0xffff));
-        const float d1 = h2f((uint16_t)(D[8] >> 16));
-        int s0 = 0, s1 = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            s0 = dot4(align2(D[i + 1], D[i]), X[i], s0);
-            s1 = dot4(D[9 + i], X[8 + i], s1);
-        }
-        return (d0 * dx[0]) * (float)s0 + (d1 * dx[1]) * (float)s1;
-    }
-};
-
-// Q4_K: slot = (super-block s/4, 64-chunk c = s%4): header 16 B + qs[32c .. 32c+32)
-template <> struct Frag<T_Q4_K> {
-    uint32_t H[4], Q[8];
-    int c;
-    template <bool RAG>
-    __device__ inline void load(const uint8_t *row, int s, int) {
-        const uint8_t *p = row + (size_t)(s >> 2) * 144;
-        c = s & 3;
-        ld16(p, H);
-        ld16(p + 16 + 32 * c, Q);
-        ld16(p + 32 + 32 * c, Q + 4);
-    }
-    __device__ inline void zero() { for (int i = 0; i < 4; ++i) H[i] = 0; for (int i = 0; i < 8; ++i) Q[i] = 0; c = 0; }
-    __device__ inline float dot(const uint32_t X[16], const float *dx, const float *sx) const {
-        const float d = h2f((uint16_t)(H[0] & 0xffff)), dmin = h2f((uint16_t)(H[0] >> 16));
-        const uint32_t S[3] = {H[1], H[2], H[3]};
-        uint32_t sc0, sc1, m0, m1;
-        k4_scale_min_pair(S, c, sc0, sc1, m0, m1);
-        int s0 = 0, s1 = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            s0 = dot4(Q[i] & 0x0f0f0f0fu, X[i], s0);
-            s1 = dot4((Q[i] >> 4) & 0x0f0f0f0fu, X[8 + i], s1);
-        }
-        return d * ((float)sc0 * dx[0] * (float)s0 + (float)sc1 * dx[1] * (float)s1) -
-               dmin * ((float)m0 * sx[0] + (float)m1 * sx[1]);
-    }
-};
-
-// Q5_K: as Q4_K plus the 32-byte qh (bit 2c / 2c+1 of qh[l] is the 5th bit)
-template <> struct Frag<T_Q5_K> {
-    uint32_t H[4], QH[8], Q[8];
-    int c;
-    template <bool RAG>
-    __device__ inline void load(const uint8_t *row, int s, int) {
-        const uint8_t *p = row + (size_t)(s >> 2) * 176;
-        c = s & 3;
-        ld16(p, H);
-        ld16(p + 16, QH);
-        ld16(p + 32, QH + 4);
-        ld16(p + 48 + 32 * c, Q);
-        ld16(p + 64 + 32 * c, Q + 4);
-    }
-    __device__ inline void zero() {
-        for (int i = 0; i < 4; ++i) H[i] = 0;
-        for (int i = 0; i < 8; ++i) QH[i] = Q[i] = 0;
-        c = 0;
-    }
-    __device__ inline float dot(const uint32_t X[16], const float *dx, const float *sx) const {
-        const float d = h2f((uint16_t)(H[0] & 0xffff)), dmin = h2f((uint16_t)(H[0] >> 16));
-        const uint32_t S[3] = {H[1], H[2], H[3]};
-        uint32_t sc0, sc1, m0, m1;
-        k4_scale_min_pair(S, c, sc0, sc1, m0, m1);
-        int s0 = 0, s1 = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const uint32_t lo = (Q[i] & 0x0f0f0f0fu) | (((QH[i] >> (2 * c)) & 0x01010101u) << 4);
-            const uint32_t hi = ((Q[i] >> 4) & 0x0f0f0f0fu) | (((QH[i] >> (2 * c + 1)) & 0x01010101u) << 4);
-            s0 = dot4(lo, X[i], s0);
-            s1 = dot4(hi, X[8 + i], s1);
-        }
-        return d * ((float)sc0 * dx[0] * (float)s0 + (float)sc1 * dx[1] * (float)s1) -
-               dmin * ((float)m0 * sx[0] + (float)m1 * sx[1]);
-    }
-};
-
-// Q6_K: slot = (super-block sb = s/4, half h = (s/2)%2, part p = s%2); lane handles
-// positions 128h + 16p + 32k + [0,16) for k = 0..3, i.e. ql[64h+16p..], ql[64h+32+16p..],
-// qh[32h+16p..] and scales 8h + p + 2k; sum (q-32)*x = sum q*x - 32 sum x per 16-run.
-template <> struct Frag<T_Q6_K> {
-    uint32_t L0[4], L1[4], QH[4], SC[2];
-    uint16_t dh;
-    int p;
-    // a super-block starts 2-byte aligned when sb is odd; 2-byte-misaligned 16-B loads stream
-    // ~16 % slower on MI355X (scripts/hbm_probe.hip), 4-byte aligned ones at full rate, so
-    // every piece is loaded from its 4-byte-aligned floor and funnel-shifted into place.
-    __device__ static inline void ld16_a4(const uint8_t *p, uint32_t *o) {
-        const uintptr_t ip = reinterpret_cast<uintptr_t>(p);
-        const uint8_t *pa = reinterpret_cast<const uint8_t *>(ip & ~(uintptr_t)3);
-        const uint32_t sh = (uint32_t)(ip & 3);
-        const uint4 w = *reinterpret_cast<const uint4 *>(pa);    // 4-B aligned dwordx4
-        const uint32_t w4 = *reinterpret_cast<const uint32_t *>(pa + 16);
-        o[0] = __builtin_amdgcn_alignbyte(w.y, w.x, sh);
-        o[1] = __builtin_amdgcn_alignbyte(w.z, w.y, sh);
-        o[2] = __builtin_amdgcn_alignbyte(w.w, w.z, sh);
-        o[3] = __builtin_amdgcn_alignbyte(w4, w.w, sh);
-    }
-    template <bool RAG>
-    __device__ inline void load(const uint8_t *row, int s, int) {
-        const uint8_t *b = row + (size_t)(s >> 2) * 210;
-        const int h = (s >> 1) & 1;
-        p = s & 1;
-        ld16_a4(b + 64 * h + 16 * p, L0);
-        ld16_a4(b + 64 * h + 32 + 16 * p, L1);
-        ld16_a4(b + 128 + 32 * h + 16 * p, QH);
-        {
-            const uintptr_t ip = reinterpret_cast<uintptr_t>(b + 192 + 8 * h);
-            const uint8_t *pa = reinterpret_cast<const uint8_t *>(ip & ~(uintptr_t)3);
-            const uint32_t sh = (uint32_t)(ip & 3);
-            const uint2 w = *reinterpret_cast<const uint2 *>(pa);
-            // third dword only matters when misaligned (then it ends at byte 209 of the block);
-            // aligned blocks re-read the second one, so the load is unconditional (no branch
-            // around a load, which would force a vmcnt(0) drain) and never passes the block end
-            const uint32_t w2 = *reinterpret_cast<const uint32_t *>(pa + (sh ? 8 : 4));
-            SC[0] = __builtin_amdgcn_alignbyte(w.y, w.x, sh);
-            SC[1] = __builtin_amdgcn_alignbyte(w2, w.y, sh);
-        }
-        dh = ld2(b + 208);
-    }
-    __device__ inline void zero() {
-        for (int i = 0; i < 4; ++i) L0[i] = L1[i] = QH[i] = 0;
-        SC[0] = SC[1] = 0;
-        dh = 0;
-        p = 0;
-    }
-    // dx: d of the four 32-blocks 4h + k; sx: d*sum(q) of the four 16-runs
-    __device__ inline float dot(const uint32_t X[16], const float *dx, const float *sx) const {
-        int s[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const uint32_t w0 = (L0[t] & 0x0f0f0f0fu) | ((QH[t] & 0x03030303u) << 4);
-            const uint32_t w1 = (L1[t] & 0x0f0f0f0fu) | ((QH[t] & 0x0c0c0c0cu) << 2);
-            const uint32_t w2 = ((L0[t] >> 4) & 0x0f0f0f0fu) | (QH[t] & 0x30303030u);
-            const uint32_t w3 = ((L1[t] >> 4) & 0x0f0f0f0fu) | ((QH[t] & 0xc0c0c0c0u) >> 2);
-            s[0] = dot4(w0, X[t], s[0]);
-            s[1] = dot4(w1, X[4 + t], s[1]);
-            s[2] = dot4(w2, X[8 + t], s[2]);
-            s[3] = dot4(w3, X[12 + t], s[3]);
-        }
-        // scales sc[8h + p + 2k]: byte (p + 2k) of the 8 loaded scale bytes
-        float acc = 0.f;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int byte = p + 2 * k;
-            const int8_t sc = (int8_t)((SC[byte >> 2] >> (8 * (byte & 3))) & 0xff);
-            acc += (float)sc * __builtin_fmaf(dx[k], (float)s[k], -32.f * sx[k]);
-        }
-        return h2f(dh) * acc;
-    }
-};
-
-template <int T> struct XdCount { static constexpr int n = 2; };
-template <> struct XdCount<T_Q6_K> { static constexpr int n = 4; };
-
-// ------------------------------------------------------------------------------------------
-// butterfly-transpose wave reduction: V (power of two, <= 64) partial sums per lane.
-// On return lane L holds the full sum of value index (L >> (6 - log2 V)).
-// ------------------------------------------------------------------------------------------
-template <int x> struct Log2 { static constexpr int v = 1 + Log2<x / 2>::v; };
-template <> struct Log2<1> { static constexpr int v = 0; };
-constexpr int pow2ceil(int x) { return x <= 1 ? 1 : 2 * pow2ceil((x + 1) / 2); }
-
-template <int V, int STEP>
-__device__ __forceinline__ void butterfly_step(float (&v)[V], int lane) {
-    constexpr int HALF = V >> (STEP + 1);
-    constexpr int DIST = 32 >> STEP;
-    const bool upper = (lane & DIST) != 0;
-#pragma unroll
-    for (int i = 0; i < HALF; ++i) {
-        const float send = upper ? v[i] : v[i + HALF];
-        const float keep = upper ? v[i + HALF] : v[i];
-        v[i] = keep + xchg<DIST>(send);
-    }
-}
-
-template <int V>
-__device__ inline float wave_reduce_transpose(float (&v)[V]) {
-    constexpr int LV = Log2<V>::v;
-    const int lane = threadIdx.x & 63;
-    if constexpr (LV > 0) butterfly_step<V, 0>(v, lane);
-    if constexpr (LV > 1) butterfly_step<V, 1>(v, lane);
-    if constexpr (LV > 2) butterfly_step<V, 2>(v, lane);
-    if constexpr (LV > 3) butterfly_step<V, 3>(v, lane);
-    if constexpr (LV > 4) butterfly_step<V, 4>(v, lane);
-    if constexpr (LV > 5) butterfly_step<V, 5>(v, lane);
-    float r = v[0];
-    if constexpr (LV <= 0) r += xchg<32>(r);
-    if constexpr (LV <= 1) r += xchg<16>(r);
-    if constexpr (LV <= 2) r += xchg<8>(r);
-    if constexpr (LV <= 3) r += xchg<4>(r);
-    if constexpr (LV <= 4) r += xchg<2>(r);
-    if constexpr (LV <= 5) r += xchg<1>(r);
-    return r;
-}
-
-// ------------------------------------------------------------------------------------------
-// the kernel
-//   RAG : K % 64 == 32 (only possible for the 32-block types): last slot holds one block
-//   XA  : src1 rows and strides are 16-byte aligned (float4 activation loads)
-//
-// Work: blockIdx.y selects the matrix / column group (batch entry, or (expert, token) for
-// MUL_MAT_ID); the workgroup quantizes that column group into LDS ONCE, then walks row groups
-// g = blockIdx.x, blockIdx.x + gridDim.x, ... (8 waves x RPW rows each). Each unit of work
-// = (row group, 64-slot iteration of K); the weights of unit u+1 are in flight while unit u
-// is computed (two register buffers), so a workgroup keeps HBM busy across its whole life and
-// the activation quantization is amortized over every row it covers.
-// ------------------------------------------------------------------------------------------
-template <int T, int NC, int RPW, bool IDS, bool RAG, bool XA, bool BIGK>
-__global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
-    extern __shared__ __align__(16) uint8_t smem[];
-    constexpr int NX = XdCount<T>::n;
-    constexpr int V = pow2ceil(RPW * NC);
-    constexpr int ROWS_PER_GROUP = MMVQ_WAVES * RPW;
-
-    const int Kpad = (a.K + 63) & ~63;
-    const int nslots = Kpad / 64;
-    const int nblk = a.K / QT<T>::blck;           // quant blocks per row
-    const int nxblk = Kpad / 32;
-    const XSmem sm = xsmem(smem, Kpad, NC);
-
-    // ---- which matrix / columns this workgroup serves
-    const uint8_t *wmat;
-    const uint8_t *xcol0;
-    uint8_t *dcol0;
-    if constexpr (IDS) {
-        // one (expert slot e, token t) pair per blockIdx.y, NC == 1
-        const int e = blockIdx.y % a.n_used, t = blockIdx.y / a.n_used;
-        int ex = *reinterpret_cast<const int32_t *>(reinterpret_cast<const uint8_t *>(a.ids) + e * a.ids_nb0 + t * a.ids_nb1);
-        ex = min(max(ex, 0), a.n_expert - 1);     // host validates ids; never index out of bounds
-        wmat = a.w + (int64_t)ex * a.nb02;
-        xcol0 = a.x + (int64_t)(e % a.ne11_b) * a.nb11 + (int64_t)t * a.nb12;
-        dcol0 = a.dst + (int64_t)e * a.nb1 + (int64_t)t * a.nb2;
-    } else {
-        const int i12 = blockIdx.y % a.ne12, i13 = blockIdx.y / a.ne12;
-        wmat = a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03;
-        xcol0 = a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13 + (int64_t)blockIdx.z * NC * a.nb11;
-        dcol0 = a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3 + (int64_t)blockIdx.z * NC * a.nb1;
-    }
-
-    const int wave = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
-    const int n_groups = (a.N + ROWS_PER_GROUP - 1) / ROWS_PER_GROUP;
-    const int n_it = (nslots + WAVE - 1) / WAVE;
-    const int my_groups = (n_groups - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-    const int n_units = my_groups * n_it;
-    const bool stamp = a.stamps != nullptr && threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
-    if (stamp) { a.stamps[blockIdx.x * 8 + 0] = __builtin_amdgcn_s_memrealtime(); a.stamps[blockIdx.x * 8 + 4] = __builtin_amdgcn_s_memtime(); }
-
-    // unit u -> first row of this wave and K slot of this lane (slot clamped: straight-line
-    // loads; dead lanes / rows read valid memory and are masked out of the sums)
-    auto unit_row0 = [&](int u) { return ((int)blockIdx.x + (u / n_it) * (int)gridDim.x) * ROWS_PER_GROUP + wave * RPW; };
-    auto unit_slot = [&](int u) { return lane + (u % n_it) * WAVE; };
-    auto load_unit = [&](Frag<T> (&f)[RPW], int u) {
-        const int r0 = unit_row0(u);
-        const int s = min(unit_slot(u), nslots - 1);
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) f[r].template load<RAG>(wmat + (int64_t)min(r0 + r, a.N - 1) * a.nb01, s, nblk);
-    };
-
-    // ---- activation loads of the first round first (L2/MALL hits), then the weight stream of
-    // unit 0, so the quantization waits only for the activations (vmcnt is in-order) while the
-    // weights stay in flight.
-    // up to two rounds (K <= 8192) are preloaded; BIGK kernels loop over the rest
-    const int kb0 = threadIdx.x >> 2;
-    constexpr int PRE = BIGK ? 1 : 2;
-    float4 xa[NC][PRE], xb[NC][PRE];
-#pragma unroll
-    for (int m = 0; m < NC; ++m)
-#pragma unroll
-        for (int r = 0; r < PRE; ++r) xblock_load<XA>(a, xcol0 + (int64_t)m * a.nb11, kb0 + r * XR_STRIDE, xa[m][r], xb[m][r]);
-
-    Frag<T> fa[RPW], fb[RPW];
-    load_unit(fa, 0);
-    __builtin_amdgcn_sched_barrier(0);
-
-#pragma unroll
-    for (int r = 0; r < PRE; ++r) {
-        const int kb = kb0 + r * XR_STRIDE;
-        if (kb < nxblk) {
-#pragma unroll
-            for (int m = 0; m < NC; ++m)
-                xblock_store<T>(Kpad, kb, xa[m][r], xb[m][r], sm.xq + (size_t)m * Kpad, sm.xd + m * nxblk,
-                                sm.xs + m * nxblk, sm.x16 + m * 2 * nxblk);
-        }
-    }
-    if constexpr (BIGK) {
-        for (int kb = kb0 + XR_STRIDE; kb < nxblk; kb += XR_STRIDE) {
-#pragma unroll
-            for (int m = 0; m < NC; ++m) {
-                xblock_load<XA>(a, xcol0 + (int64_t)m * a.nb11, kb, xa[m][0], xb[m][0]);
-                xblock_store<T>(Kpad, kb, xa[m][0], xb[m][0], sm.xq + (size_t)m * Kpad, sm.xd + m * nxblk,
-                                sm.xs + m * nxblk, sm.x16 + m * 2 * nxblk);
-            }
-        }
-    }
-    __syncthreads();
-    if (stamp) a.stamps[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
-
-    float acc[V];
-#pragma unroll
-    for (int i = 0; i < V; ++i) acc[i] = 0.f;
-
-    auto compute_unit = [&](const Frag<T> (&f)[RPW], int u) {
-        const int s_raw = unit_slot(u);
-        const int s = min(s_raw, nslots - 1);
-        const float live = s_raw < nslots ? 1.f : 0.f;
-        int xb0, x16b;
-        if constexpr (T == T_Q6_K) {
-            xb0 = 8 * (s >> 2) + 4 * ((s >> 1) & 1);
-            x16b = 16 * (s >> 2) + 8 * ((s >> 1) & 1) + (s & 1);
-        } else {
-            xb0 = 2 * s;
-            x16b = 0;
-        }
-#pragma unroll
-        for (int m = 0; m < NC; ++m) {
-            uint32_t X[16];
-            const int8_t *xm = sm.xq + (size_t)m * Kpad;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint4 t4 = *reinterpret_cast<const uint4 *>(xm + (size_t)(j * nslots + s) * 16);
-                X[4 * j + 0] = t4.x; X[4 * j + 1] = t4.y; X[4 * j + 2] = t4.z; X[4 * j + 3] = t4.w;
-            }
-            float dx[NX], sx[NX];
-#pragma unroll
-            for (int i = 0; i < NX; ++i) dx[i] = sm.xd[m * nxblk + xb0 + i];
-            if constexpr (T == T_Q6_K) {
-#pragma unroll
-                for (int i = 0; i < NX; ++i) sx[i] = sm.x16[m * 2 * nxblk + x16b + 2 * i];
-            } else {
-#pragma unroll
-                for (int i = 0; i < NX; ++i) sx[i] = sm.xs[m * nxblk + xb0 + i];
-            }
-#pragma unroll
-            for (int r = 0; r < RPW; ++r) acc[r * NC + m] += live * f[r].dot(X, dx, sx);
-        }
-        // last K iteration of this row group: reduce across the wave and store
-        if (u % n_it == n_it - 1) {
-            const float sum = wave_reduce_transpose<V>(acc);
-            constexpr int SHIFT = 6 - Log2<V>::v;
-            const int idx = lane >> SHIFT;
-            const int r0 = unit_row0(u);
-            if ((lane & ((1 << SHIFT) - 1)) == 0 && idx < RPW * NC) {
-                const int r = idx / NC, m = idx % NC;
-                if (r0 + r < a.N) reinterpret_cast<float *>(dcol0 + (int64_t)m * a.nb1)[r0 + r] = sum;
-            }
-#pragma unroll
-            for (int i = 0; i < V; ++i) acc[i] = 0.f;
-        }
-    };
-
-    // prefetches are unconditional (clamped to the last unit: a repeat of addresses already
-    // in flight, served on-chip) so the load stream never sits under a branch
-    // sched_barrier pins each prefetch ahead of the compute that follows it (left alone, the
-    // scheduler sinks the loads below the compute to save registers and the overlap is lost)
-    for (int u = 0; u < n_units; u += 2) {
-        load_unit(fb, min(u + 1, n_units - 1));
-        __builtin_amdgcn_sched_barrier(0);
-        compute_unit(fa, u);
-        if (u + 1 >= n_units) break;
-        load_unit(fa, min(u + 2, n_units - 1));
-        __builtin_amdgcn_sched_barrier(0);
-        compute_unit(fb, u + 1);
-    }
-    if (stamp) { a.stamps[blockIdx.x * 8 + 2] = a.stamps[blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime(); a.stamps[blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memtime(); }
-}
 
 // ------------------------------------------------------------------------------------------
 // host-side launch helpers (called from dispatch.cpp)

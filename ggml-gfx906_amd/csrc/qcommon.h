@@ -127,4 +127,22 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
+// fp32 -> fp16 RNE keeping the sign of zero (GGML_FP32_TO_FP16, reference src/ggml-impl.h:358-405)
+__device__ __forceinline__ uint16_t f2h_rne(float f) {
+    const uint16_t h = __builtin_bit_cast(uint16_t, (_Float16)f);
+    return (uint16_t)(h | ((__builtin_bit_cast(uint32_t, f) >> 16) & 0x8000u));
+}
+
+// GELU as ggml-cpu evaluates it (src/ggml-cpu/vec.h:601-646 with GGML_GELU_FP16): x <= -10 -> 0,
+// x >= 10 -> x, else the fp16 table entry, i.e. fp16(gelu_tanh(fp16(x))) with the table built
+// in f32 (src/ggml-cpu/ggml-cpu.c:3542).
+__device__ __forceinline__ float gelu_ggml(float x) {
+    constexpr float GELU_COEF_A = 0.044715f;
+    constexpr float SQRT_2_OVER_PI = 0.79788456080286535587989211986876f;
+    if (x <= -10.0f) return 0.0f;
+    if (x >= 10.0f) return x;
+    const float xh = h2f(f2h_rne(x));
+    return h2f(f2h_rne(0.5f * xh * (1.0f + tanhf(SQRT_2_OVER_PI * xh * (1.0f + GELU_COEF_A * xh * xh)))));
+}
+
 }  // namespace mi355x

@@ -9,6 +9,8 @@
 
 namespace mi355x {
 
+enum { EPI_GELU = 1, EPI_RESID = 2 };
+
 struct MmArgs {
     const uint8_t *w;      // src0, quantized rows (nb00 == block bytes)
     int64_t nb01, nb02, nb03;
@@ -29,6 +31,15 @@ struct MmArgs {
     int ne11_b;            // b->ne[1]
     int n_expert;          // as->ne[2]
     int x_aligned16;       // src1 rows / strides are 16-byte aligned
+    // fused decode-layer variant (gpt2.cpp; plain MUL_MAT leaves all of these zero):
+    //   prologue, ln_g != nullptr: each src1 column is layer-normalized before quantization,
+    //     x <- (x - mean) / sqrt(var + ln_eps) * ln_g + ln_b  (ggml_norm + mul + add)
+    //   epilogue: v <- v + bias[row]; epi & EPI_GELU: v <- gelu(v); epi & EPI_RESID: dst += v
+    const float *ln_g, *ln_b;
+    float ln_eps;
+    const float *bias;
+    int epi;
+    int fused;
     // diagnostics (GGML_MI355X_STAMPS): per-workgroup s_memrealtime stamps, or nullptr
     unsigned long long *stamps;
     int diag;              // diagnostics: bit0 = skip activation loads, bit1 = skip weight loads

@@ -1,0 +1,297 @@
+// oracle/gpt2_ref.cpp — TEST INFRASTRUCTURE ONLY (never part of the product path).
+//
+// Runs GPT-2 through the REFERENCE ggml (oracle/_ref/libggml-ref.so, compiled from
+// /root/reference/src by oracle/ref.mk) to produce the logits our engine is checked against,
+// and to time the reference's CPU path for bench.py's cpu_baseline.
+//
+// The graph is the one of examples/gpt-2/main-sched.cpp:553-858 (gpt2_graph), written here
+// against the public ggml API (not copied): wte/wpe get_rows + add, per layer norm -> mul ->
+// add, MUL_MAT attn + bias, K/V stored into the cache, KQ = K.Q, scale, diag_mask_inf,
+// soft_max, KQV = V^T.softmax, projection + bias + residual, norm, MLP (fc, gelu, proj),
+// residual; final norm and lm_head. The legacy-format loader follows main-sched.cpp:155-546.
+// Evaluation is token by token (N = 1 graphs, n_past = position), i.e. the decode path.
+//
+// Two modes:
+//   default          : ggml-cpu backend only (the oracle)
+//   --plugin LIB     : load a ggml backend plugin (ours: libggml-hip-mi355x.so) with
+//                      ggml_backend_load, place layer il on GPU device il*D/n_layer (D =
+//                      --devices, default all), and let the reference's ggml_backend_sched
+//                      split the graph across [GPU devices..., CPU] — the reference's own
+//                      scheduler driving our backend, i.e. the drop-in check for examples/gpt-2.
+//
+// usage: gpt2_ref MODEL --tokens 1,2,3 [--out logits.f32] [--threads N] [--plugin LIB]
+//                 [--devices D] [--time-tokens T]
+#include "ggml-alloc.h"
+#include "ggml-backend.h"
+#include "ggml-cpu.h"
+#include "ggml.h"
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <string>
+#include <vector>
+
+struct Layer {
+    ggml_tensor *ln_1_g, *ln_1_b, *ln_2_g, *ln_2_b;
+    ggml_tensor *c_attn_attn_w, *c_attn_attn_b, *c_attn_proj_w, *c_attn_proj_b;
+    ggml_tensor *c_mlp_fc_w, *c_mlp_fc_b, *c_mlp_proj_w, *c_mlp_proj_b;
+    ggml_tensor *memory_k, *memory_v;   // per layer: [n_ctx * n_embd] f32
+};
+
+struct Model {
+    int32_t n_vocab, n_ctx, n_embd, n_head, n_layer, ftype;
+    float eps = 1e-5f;
+    ggml_tensor *ln_f_g, *ln_f_b, *wte, *wpe, *lm_head;
+    std::vector<Layer> layers;
+    std::vector<ggml_context *> ctxs;   // one weight context per placement
+    std::map<std::string, ggml_tensor *> tensors;
+};
+
+static void die(const char *m) {
+    fprintf(stderr, "gpt2_ref: %s\n", m);
+    exit(1);
+}
+
+int main(int argc, char **argv) {
+    if (argc < 2) die("usage: gpt2_ref MODEL --tokens a,b,c [--out F] [--threads N] [--plugin LIB] [--devices D] [--time-tokens T]");
+    std::string fname = argv[1], out, plugin;
+    std::vector<int32_t> toks;
+    int threads = 8, want_dev = -1, time_tokens = 0;
+    for (int i = 2; i < argc; ++i) {
+        std::string a = argv[i];
+        auto next = [&]() { if (i + 1 >= argc) die("missing value"); return std::string(argv[++i]); };
+        if (a == "--tokens") {
+            std::string s = next();
+            size_t p = 0;
+            while (p < s.size()) {
+                size_t q = s.find(',', p);
+                if (q == std::string::npos) q = s.size();
+                toks.push_back(atoi(s.substr(p, q - p).c_str()));
+                p = q + 1;
+            }
+        } else if (a == "--out") out = next();
+        else if (a == "--threads") threads = atoi(next().c_str());
+        else if (a == "--plugin") plugin = next();
+        else if (a == "--devices") want_dev = atoi(next().c_str());
+        else if (a == "--time-tokens") time_tokens = atoi(next().c_str());
+        else die(("unknown arg " + a).c_str());
+    }
+
+    // ---- backends: [GPU devices of the plugin...] + CPU (main-sched.cpp:109-152 uses 1 GPU)
+    std::vector<ggml_backend_t> gpus;
+    if (!plugin.empty()) {
+        ggml_backend_reg_t reg = ggml_backend_load(plugin.c_str());
+        if (!reg) die("ggml_backend_load failed");
+        const int n = (int)ggml_backend_reg_dev_count(reg);
+        const int use = want_dev < 0 ? n : std::min(n, want_dev);
+        for (int d = 0; d < use; ++d) gpus.push_back(ggml_backend_dev_init(ggml_backend_reg_dev_get(reg, d), nullptr));
+        if (gpus.empty()) die("plugin has no devices");
+    }
+    ggml_backend_t cpu = ggml_backend_cpu_init();
+    ggml_backend_cpu_set_n_threads(cpu, threads);
+
+    // ---- header + vocab (main-sched.cpp:161-223)
+    Model m;
+    std::ifstream fin(fname, std::ios::binary);
+    if (!fin) die("cannot open model");
+    uint32_t magic;
+    fin.read((char *)&magic, 4);
+    if (magic != GGML_FILE_MAGIC) die("bad magic");
+    fin.read((char *)&m.n_vocab, 4);
+    fin.read((char *)&m.n_ctx, 4);
+    fin.read((char *)&m.n_embd, 4);
+    fin.read((char *)&m.n_head, 4);
+    fin.read((char *)&m.n_layer, 4);
+    fin.read((char *)&m.ftype, 4);
+    m.ftype %= GGML_QNT_VERSION_FACTOR;
+    int32_t nv;
+    fin.read((char *)&nv, 4);
+    if (nv != m.n_vocab) die("bad vocab size");
+    for (int i = 0; i < nv; ++i) {
+        uint32_t len;
+        fin.read((char *)&len, 4);
+        fin.seekg(len, std::ios::cur);
+    }
+    const ggml_type wtype = ggml_ftype_to_ggml_type((ggml_ftype)m.ftype);
+    if (wtype == GGML_TYPE_COUNT) die("bad ftype");
+
+    // ---- weights: one context per placement (GPU d or CPU), layer il -> GPU il*D/n_layer
+    const int D = (int)gpus.size();
+    const int n_place = D > 0 ? D : 1;
+    for (int p = 0; p < n_place; ++p) {
+        ggml_init_params ip = {ggml_tensor_overhead() * (16 + 14 * (size_t)m.n_layer), nullptr, true};
+        m.ctxs.push_back(ggml_init(ip));
+    }
+    auto place_of_layer = [&](int il) { return D > 0 ? il * D / m.n_layer : 0; };
+    const int64_t E = m.n_embd;
+    ggml_context *c0 = m.ctxs[0], *cl = m.ctxs[n_place - 1];
+    m.wte = ggml_new_tensor_2d(c0, wtype, E, m.n_vocab);
+    m.wpe = ggml_new_tensor_2d(c0, GGML_TYPE_F32, E, m.n_ctx);
+    m.ln_f_g = ggml_new_tensor_1d(cl, GGML_TYPE_F32, E);
+    m.ln_f_b = ggml_new_tensor_1d(cl, GGML_TYPE_F32, E);
+    m.lm_head = ggml_new_tensor_2d(cl, wtype, E, m.n_vocab);
+    m.tensors["model/wte"] = m.wte;
+    m.tensors["model/wpe"] = m.wpe;
+    m.tensors["model/ln_f/g"] = m.ln_f_g;
+    m.tensors["model/ln_f/b"] = m.ln_f_b;
+    m.tensors["model/lm_head"] = m.lm_head;
+    m.layers.resize(m.n_layer);
+    for (int il = 0; il < m.n_layer; ++il) {
+        ggml_context *c = m.ctxs[place_of_layer(il)];
+        Layer &L = m.layers[il];
+        const std::string pfx = "model/h" + std::to_string(il) + "/";
+        auto t1 = [&](const char *n, int64_t ne0) { ggml_tensor *t = ggml_new_tensor_1d(c, GGML_TYPE_F32, ne0); m.tensors[pfx + n] = t; return t; };
+        auto t2 = [&](const char *n, int64_t ne0, int64_t ne1) { ggml_tensor *t = ggml_new_tensor_2d(c, wtype, ne0, ne1); m.tensors[pfx + n] = t; return t; };
+        L.ln_1_g = t1("ln_1/g", E);
+        L.ln_1_b = t1("ln_1/b", E);
+        L.ln_2_g = t1("ln_2/g", E);
+        L.ln_2_b = t1("ln_2/b", E);
+        L.c_attn_attn_w = t2("attn/c_attn/w", E, 3 * E);
+        L.c_attn_attn_b = t1("attn/c_attn/b", 3 * E);
+        L.c_attn_proj_w = t2("attn/c_proj/w", E, E);
+        L.c_attn_proj_b = t1("attn/c_proj/b", E);
+        L.c_mlp_fc_w = t2("mlp/c_fc/w", E, 4 * E);
+        L.c_mlp_fc_b = t1("mlp/c_fc/b", 4 * E);
+        L.c_mlp_proj_w = t2("mlp/c_proj/w", 4 * E, E);
+        L.c_mlp_proj_b = t1("mlp/c_proj/b", E);
+        L.memory_k = ggml_new_tensor_1d(c, GGML_TYPE_F32, E * m.n_ctx);
+        L.memory_v = ggml_new_tensor_1d(c, GGML_TYPE_F32, E * m.n_ctx);
+    }
+    std::vector<ggml_backend_buffer_t> bufs;
+    for (int p = 0; p < n_place; ++p) {
+        ggml_backend_buffer_type_t bt = D > 0 ? ggml_backend_get_default_buffer_type(gpus[p]) : ggml_backend_cpu_buffer_type();
+        ggml_backend_buffer_t b = ggml_backend_alloc_ctx_tensors_from_buft(m.ctxs[p], bt);
+        if (!b) die("weight buffer allocation failed");
+        ggml_backend_buffer_clear(b, 0);
+        bufs.push_back(b);
+    }
+
+    // ---- tensor records (main-sched.cpp:429-517), tied lm_head (:503-510)
+    bool has_lm_head = false;
+    std::vector<char> rb;
+    for (;;) {
+        int32_t n_dims, len, ttype;
+        fin.read((char *)&n_dims, 4);
+        fin.read((char *)&len, 4);
+        fin.read((char *)&ttype, 4);
+        if (fin.eof()) break;
+        int32_t ne[2] = {1, 1};
+        for (int i = 0; i < n_dims; ++i) fin.read((char *)&ne[i], 4);
+        std::string name(len, 0);
+        fin.read(&name[0], len);
+        auto it = m.tensors.find(name);
+        if (it == m.tensors.end()) die(("unknown tensor " + name).c_str());
+        ggml_tensor *t = it->second;
+        if (t->ne[0] != ne[0] || t->ne[1] != ne[1] || t->type != ttype) die(("wrong shape/type " + name).c_str());
+        rb.resize(ggml_nbytes(t));
+        fin.read(rb.data(), rb.size());
+        ggml_backend_tensor_set(t, rb.data(), 0, rb.size());
+        if (name == "model/wte" && !has_lm_head) ggml_backend_tensor_set(m.lm_head, rb.data(), 0, rb.size());
+        if (name == "model/lm_head") has_lm_head = true;
+    }
+
+    // ---- inputs (CPU buffer; main-sched.cpp:519-530)
+    ggml_init_params ipi = {ggml_tensor_overhead() * 4, nullptr, true};
+    ggml_context *cin = ggml_init(ipi);
+    ggml_tensor *embd = ggml_new_tensor_1d(cin, GGML_TYPE_I32, 1);
+    ggml_tensor *position = ggml_new_tensor_1d(cin, GGML_TYPE_I32, 1);
+    ggml_backend_buffer_t bin = ggml_backend_alloc_ctx_tensors_from_buft(cin, ggml_backend_cpu_buffer_type());
+
+    std::vector<ggml_backend_t> backends = gpus;
+    backends.push_back(cpu);
+    const int MAX_NODES = 4096;
+    ggml_backend_sched_t sched = ggml_backend_sched_new(backends.data(), nullptr, (int)backends.size(), MAX_NODES, false, true);
+    std::vector<uint8_t> gbuf(ggml_tensor_overhead() * MAX_NODES + ggml_graph_overhead_custom(MAX_NODES, false));
+
+    // gpt2_graph with N = 1 (main-sched.cpp:553-858)
+    auto build = [&](int n_past) {
+        ggml_init_params gp = {gbuf.size(), gbuf.data(), true};
+        ggml_context *ctx = ggml_init(gp);
+        ggml_cgraph *gf = ggml_new_graph_custom(ctx, MAX_NODES, false);
+        const int N = 1;
+        const float KQ_scale = 1.0f / sqrtf(float(m.n_embd) / m.n_head);
+        ggml_tensor *inpL = ggml_add(ctx, ggml_get_rows(ctx, m.wte, embd), ggml_get_rows(ctx, m.wpe, position));
+        for (int il = 0; il < m.n_layer; ++il) {
+            const Layer &L = m.layers[il];
+            ggml_tensor *cur = ggml_norm(ctx, inpL, m.eps);
+            cur = ggml_add(ctx, ggml_mul(ctx, cur, L.ln_1_g), L.ln_1_b);
+            cur = ggml_add(ctx, ggml_mul_mat(ctx, L.c_attn_attn_w, cur), L.c_attn_attn_b);
+            ggml_tensor *Qcur = ggml_view_2d(ctx, cur, E, N, cur->nb[1], 0 * sizeof(float) * E);
+            ggml_tensor *Kcur = ggml_view_2d(ctx, cur, E, N, cur->nb[1], 1 * sizeof(float) * E);
+            ggml_tensor *Vcur = ggml_view_2d(ctx, cur, E, N, cur->nb[1], 2 * sizeof(float) * E);
+            ggml_tensor *k = ggml_view_1d(ctx, L.memory_k, N * E, ggml_element_size(L.memory_k) * E * n_past);
+            ggml_tensor *v = ggml_view_1d(ctx, L.memory_v, N * E, ggml_element_size(L.memory_v) * E * n_past);
+            ggml_build_forward_expand(gf, ggml_cpy(ctx, Kcur, k));
+            ggml_build_forward_expand(gf, ggml_cpy(ctx, Vcur, v));
+            ggml_tensor *Q = ggml_permute(ctx, ggml_cont_3d(ctx, Qcur, E / m.n_head, m.n_head, N), 0, 2, 1, 3);
+            ggml_tensor *K = ggml_permute(ctx, ggml_reshape_3d(ctx, ggml_view_1d(ctx, L.memory_k, (n_past + N) * E, 0), E / m.n_head, m.n_head, n_past + N), 0, 2, 1, 3);
+            ggml_tensor *KQ = ggml_mul_mat(ctx, K, Q);
+            ggml_tensor *KQ_scaled = ggml_scale(ctx, KQ, KQ_scale);
+            ggml_tensor *KQ_masked = ggml_diag_mask_inf(ctx, KQ_scaled, n_past);
+            ggml_tensor *KQ_soft_max = ggml_soft_max(ctx, KQ_masked);
+            ggml_tensor *V_trans = ggml_cont_3d(ctx, ggml_permute(ctx, ggml_reshape_3d(ctx, ggml_view_1d(ctx, L.memory_v, (n_past + N) * E, 0), E / m.n_head, m.n_head, n_past + N), 1, 2, 0, 3),
+                                                n_past + N, E / m.n_head, m.n_head);
+            ggml_tensor *KQV = ggml_mul_mat(ctx, V_trans, KQ_soft_max);
+            cur = ggml_cont_2d(ctx, ggml_permute(ctx, KQV, 0, 2, 1, 3), E, N);
+            cur = ggml_add(ctx, ggml_mul_mat(ctx, L.c_attn_proj_w, cur), L.c_attn_proj_b);
+            cur = ggml_add(ctx, cur, inpL);
+            ggml_tensor *inpFF = cur;
+            cur = ggml_norm(ctx, inpFF, m.eps);
+            cur = ggml_add(ctx, ggml_mul(ctx, cur, L.ln_2_g), L.ln_2_b);
+            cur = ggml_add(ctx, ggml_mul_mat(ctx, L.c_mlp_fc_w, cur), L.c_mlp_fc_b);
+            cur = ggml_gelu(ctx, cur);
+            cur = ggml_add(ctx, ggml_mul_mat(ctx, L.c_mlp_proj_w, cur), L.c_mlp_proj_b);
+            inpL = ggml_add(ctx, cur, inpFF);
+        }
+        inpL = ggml_norm(ctx, inpL, m.eps);
+        inpL = ggml_add(ctx, ggml_mul(ctx, inpL, m.ln_f_g), m.ln_f_b);
+        inpL = ggml_mul_mat(ctx, m.lm_head, inpL);
+        ggml_build_forward_expand(gf, inpL);
+        ggml_free(ctx);
+        return gf;
+    };
+
+    std::vector<float> logits((size_t)m.n_vocab * toks.size());
+    auto eval = [&](int n_past, int32_t tok, float *dst) {
+        ggml_cgraph *gf = build(n_past);
+        ggml_backend_sched_reset(sched);
+        if (!ggml_backend_sched_alloc_graph(sched, gf)) die("sched alloc failed");
+        ggml_backend_tensor_set(embd, &tok, 0, 4);
+        ggml_backend_tensor_set(position, &n_past, 0, 4);
+        if (ggml_backend_sched_graph_compute(sched, gf) != GGML_STATUS_SUCCESS) die("compute failed");
+        ggml_tensor *res = ggml_graph_node(gf, -1);
+        if (dst) ggml_backend_tensor_get(res, dst, 0, sizeof(float) * m.n_vocab);
+    };
+    for (size_t i = 0; i < toks.size(); ++i) eval((int)i, toks[i], logits.data() + i * m.n_vocab);
+    fprintf(stderr, "gpt2_ref: %zu tokens evaluated, %d backends, %d splits\n", toks.size(), (int)backends.size(),
+            ggml_backend_sched_get_n_splits(sched));
+    if (!out.empty()) {
+        FILE *f = fopen(out.c_str(), "wb");
+        if (!f) die("cannot write output");
+        fwrite(logits.data(), sizeof(float), logits.size(), f);
+        fclose(f);
+    }
+    if (time_tokens > 0) {   // decode timing: positions continue after the given tokens
+        std::vector<float> tmp(m.n_vocab);
+        const int start = (int)toks.size();
+        const int n = std::min(time_tokens, m.n_ctx - start);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < n; ++i) eval(start + i, (int32_t)(i % m.n_vocab), tmp.data());
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        printf("{\"tokens\": %d, \"seconds\": %.6f, \"ms_per_token\": %.4f, \"tokens_per_s\": %.3f, \"threads\": %d}\n", n, s,
+               1e3 * s / n, n / s, threads);
+    }
+    ggml_backend_sched_free(sched);
+    for (auto b : bufs) ggml_backend_buffer_free(b);
+    for (auto c : m.ctxs) ggml_free(c);
+    ggml_backend_buffer_free(bin);
+    ggml_free(cin);
+    for (auto g : gpus) ggml_backend_free(g);
+    ggml_backend_free(cpu);
+    return 0;
+}

@@ -15,6 +15,8 @@
 #   _ref/test-quantize-fns    upstream quantization pins (tests/test-quantize-fns.cpp)
 #   _ref/gen_golden           our fixture generator (oracle/gen_golden.cpp) linked to the above
 #   _ref/ref_cpu_bench        our CPU-baseline timer (oracle/ref_cpu_bench.cpp) linked to the above
+#   _ref/gpt2_ref             GPT-2 logits / decode timing through the reference ggml graph
+#                             (oracle/gpt2_ref.cpp), CPU or the reference scheduler + our plugin
 #
 # ISA: x86-64-v3 (AVX2/FMA/F16C) so the binaries also run on the GPU box's EPYC host;
 # -march=native here could emit AVX-512/AMX the box may lack.
@@ -43,7 +45,7 @@ CPU_CXX  := ggml-cpu/ggml-cpu.cpp ggml-cpu/repack.cpp ggml-cpu/hbm.cpp ggml-cpu/
 
 OBJS := $(patsubst %.c,$(OBJ)/%.c.o,$(BASE_C) $(CPU_C)) $(patsubst %.cpp,$(OBJ)/%.cpp.o,$(BASE_CXX) $(CPU_CXX))
 
-all: $(OUT)/libggml-ref.so $(OUT)/test-backend-ops $(OUT)/test-quantize-fns $(OUT)/gen_golden $(OUT)/ref_cpu_bench
+all: $(OUT)/libggml-ref.so $(OUT)/test-backend-ops $(OUT)/test-quantize-fns $(OUT)/gen_golden $(OUT)/ref_cpu_bench $(OUT)/gpt2_ref
 
 $(OBJ)/ggml-cpu/%.c.o: $(REF)/src/ggml-cpu/%.c
 	@mkdir -p $(dir $@)
@@ -76,6 +78,9 @@ $(OUT)/gen_golden: oracle/gen_golden.cpp $(OUT)/libggml-ref.so
 	g++ $(CXXFLAGS) $< -o $@ $(LINK)
 
 $(OUT)/ref_cpu_bench: oracle/ref_cpu_bench.cpp $(OUT)/libggml-ref.so
+	g++ $(CXXFLAGS) $< -o $@ $(LINK)
+
+$(OUT)/gpt2_ref: oracle/gpt2_ref.cpp $(OUT)/libggml-ref.so
 	g++ $(CXXFLAGS) $< -o $@ $(LINK)
 
 clean:

@@ -23,8 +23,8 @@ for step in "$@"; do
     case $step in
         info)  run info 60 bash -c 'lscpu | head -20; nproc; rocm-smi --showproductname; python -c "import torch;print(torch.cuda.get_device_name(0))"' ;;
         build) run build 600 python -c "import __graft_entry__ as g; g.build()" ;;
-        tests) run tests 900 python -m pytest tests -m gpu -x -q ;;
-        testsall) run testsall 900 python -m pytest tests -m gpu -q ;;
+        tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+        testsall) run testsall 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         tbo)   run tbo 900 env GGML_BACKEND_PATH=$PWD/ggml-gfx906_amd/libggml-hip-mi355x.so ./oracle/_ref/test-backend-ops test -o MUL_MAT -b MI355X0 ;;
         tboid) run tboid 900 env GGML_BACKEND_PATH=$PWD/ggml-gfx906_amd/libggml-hip-mi355x.so ./oracle/_ref/test-backend-ops test -o MUL_MAT_ID -b MI355X0 ;;
