@@ -26,6 +26,12 @@ Extra fields on the single JSON line:
   configs       the other BASELINE.json kernel configs (Q4_K north star, Q4_K/Q5_K/Q6_K
                 4096x11008, Q8_0 M=512): GB/s, TFLOP/s, roofline fractions; *_single rows
                 are one matrix per launch
+  gpt2          the metric's second half, BASELINE.json configs[4]: GPT-2 117M Q4_0 greedy
+                decode tokens/s (random-init weights generated and quantized on the device),
+                layers pipeline-split over the N ranks (gpt2.py: one stage per GPU, RCCL
+                send/recv of the 3 KB/sequence hidden state per tick, N micro-batches in
+                flight); at N=1 also the single-stream latency. The reference's ggml-cpu runs
+                the same model shape on the host (cpu_baseline.gpt2, oracle/_ref/gpt2_ref).
 """
 from __future__ import annotations
 
@@ -184,6 +190,104 @@ def cpu_baseline(seconds: float) -> dict:
             "us_per_mul_mat": round(per * 1e6, 2)}
 
 
+def gpt2_leg(torch, world: int, rank: int, n_seq: int, ticks: int, warm: int) -> dict:
+    """GPT-2 117M Q4_0 decode through the pipeline ring (gpt2.Pipeline): stage `rank` of
+    `world`, n_micro = world micro-batches of n_seq sequences. Returns this rank's timing."""
+    import gpt2 as G
+    import torch.distributed as dist
+    hp = G.make_hparams(M.Q4_0)
+    parts = G.partition_layers(hp["n_layer"], world)
+    stage = G.Stage(hp, *parts[rank])
+    stage.fill_synthetic(1234)
+    n_micro = world
+    ctxs = [G.Context(stage, n_seq) for _ in range(n_micro)]
+    st = torch.cuda.current_stream().cuda_stream
+    dev = torch.device("cuda", torch.cuda.current_device())
+    zeros = torch.zeros(n_seq, dtype=torch.int32, device=dev)
+    for c in ctxs:
+        c.set_pos(zeros.data_ptr(), st)
+    E = hp["n_embd"]
+    send = [torch.zeros(n_seq * E, dtype=torch.float32, device=dev) for _ in range(n_micro)]
+    prompt = [torch.full((n_seq * E,), 0, dtype=torch.int32, device=dev) for _ in range(n_micro)]
+    for mb in range(n_micro):
+        prompt[mb][:n_seq] = torch.arange(n_seq, dtype=torch.int32, device=dev) + 40 + mb
+
+    def stage_fn(mb, inbuf, valid):
+        c = ctxs[mb]
+        if valid:
+            if stage.first:
+                c.set_tokens(inbuf.data_ptr(), st)
+            else:
+                c._copy(c.hidden_ptr, inbuf.data_ptr(), c.hidden_bytes, st)
+            c.decode(st, graph=True)
+        src = c.tokens_ptr if stage.last else c.hidden_ptr
+        c._copy(send[mb].data_ptr(), src, 4 * n_seq if stage.last else c.hidden_bytes, st)
+        return send[mb]
+
+    pipe = G.Pipeline(rank, world, n_micro, n_seq * E, dev)
+    first = lambda mb: prompt[mb].view(torch.float32)  # noqa: E731
+
+    def sync():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # warm-up fills the ring (world - 1 ticks) and captures every context's hipGraph; the
+    # timed ticks then each complete one micro-batch step at the last stage
+    pipe.run(warm + world - 1, stage_fn, first)
+    sync()
+    t0 = time.perf_counter()
+    pipe.run(ticks, stage_fn, first)
+    sync()
+    el = time.perf_counter() - t0
+    out = {"elapsed": el, "ticks": ticks, "stages": parts, "stage_weight_bytes": stage.nbytes()}
+    # single-stream latency at N=1: back-to-back graph replays with the device-side argmax loop
+    if world == 1:
+        c = G.Context(stage, 1)
+        c.set_pos(zeros.data_ptr(), st)
+        c.set_tokens(prompt[0].data_ptr(), st)
+        for _ in range(4):
+            c.decode(st, graph=True)
+        sync()
+        n = 256
+        t1 = time.perf_counter()
+        for _ in range(n):
+            c.decode(st, graph=True)
+        sync()
+        out["latency_ms_per_token"] = (time.perf_counter() - t1) / n * 1e3
+        c.free()
+    for c in ctxs:
+        c.free()
+    stage.free()
+    return out
+
+
+def cpu_gpt2_baseline(threads: int, tokens: int = 128) -> dict | None:
+    """the reference's ggml-cpu GPT-2 graph (oracle/_ref/gpt2_ref) on a synthetic 117M Q4_0
+    checkpoint written by tests/gpt2_synth.py: decode ms/token over `tokens` positions"""
+    exe = os.path.join(ROOT, "oracle", "_ref", "gpt2_ref")
+    if not os.path.exists(exe):
+        return None
+    sys.path[:0] = [os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+    import tempfile
+
+    import gpt2_synth
+    import qref
+    path = os.path.join(tempfile.gettempdir(), f"bench_gpt2_117m_{os.getpid()}.bin")
+    gpt2_synth.write_model(path, gpt2_synth.GPT2_117M, qref.Q4_0, 1234)
+    try:
+        r = subprocess.run([exe, path, "--tokens", "40", "--threads", str(threads), "--time-tokens", str(tokens)],
+                           capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            return None
+        j = json.loads(r.stdout.strip().splitlines()[-1])
+    finally:
+        os.remove(path)
+    return {"value": round(j["tokens_per_s"], 2), "unit": "tokens/s", "cores": threads, "kind": "reference",
+            "sample": f"GPT-2 117M Q4_0 (synthetic), 1 sequence, {tokens} decode positions after a 1-token prompt",
+            "ms_per_token": round(j["ms_per_token"], 4)}
+
+
 def launch_env():
     """(world, rank, local_rank) as torch.distributed.run exports them; 1 process by default"""
     return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
@@ -213,6 +317,8 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-extra", action="store_true", help="skip the secondary configs")
+    ap.add_argument("--no-gpt2", action="store_true", help="skip the GPT-2 decode leg")
+    ap.add_argument("--gpt2-ticks", type=int, default=256, help="timed pipeline ticks of the GPT-2 leg")
     args = ap.parse_args()
 
     import torch
@@ -287,6 +393,29 @@ def main() -> None:
 
     cpu = cpu_baseline(args.cpu_seconds) if (rank == 0 and world == 1) else None
 
+    # ---------------- GPT-2 117M Q4_0 decode, layers pipeline-split over the ranks ------------
+    gpt2 = None
+    if not args.no_gpt2:
+        torch.cuda.empty_cache()
+        runs = {}
+        for n_seq in (1, 8):
+            r = gpt2_leg(torch, world, rank, n_seq, args.gpt2_ticks, 8)
+            t_g = max_over_ranks(r["elapsed"], torch.device("cuda", local)) if world > 1 else r["elapsed"]
+            runs[n_seq] = (r, t_g)
+        r1, t1 = runs[1]
+        gpt2 = {"metric": "GPT-2 117M Q4_0 greedy decode tokens/s", "unit": "tokens/s",
+                "value": round(args.gpt2_ticks * 1 / t1, 1),
+                "ms_per_tick": round(t1 / args.gpt2_ticks * 1e3, 4),
+                "batched_n_seq8_tokens_per_s": round(args.gpt2_ticks * 8 / runs[8][1], 1),
+                "parallelism": f"pp{world} (layer ranges {r1['stages']}), {world} micro-batch(es) in flight",
+                "stage0_weight_bytes": r1["stage_weight_bytes"],
+                "data": "synthetic random-init GPT-2 117M weights, quantized to Q4_0 on the device"}
+        if "latency_ms_per_token" in r1:
+            gpt2["single_stream_ms_per_token"] = round(r1["latency_ms_per_token"], 4)
+            gpt2["single_stream_tokens_per_s"] = round(1e3 / r1["latency_ms_per_token"], 1)
+        if cpu is not None:
+            cpu["gpt2"] = cpu_gpt2_baseline(cpu["cores"])
+
     if rank == 0:
         line = {
             "metric": "quantized GEMM GB/s (Q4_0 mul_mat_vec 4096x4096, M=1, HBM-cold)",
@@ -313,6 +442,7 @@ def main() -> None:
                          "frac_of_measured_copy_bw": round(achieved / HBM_MEASURED_GBS, 4)},
             "cpu_baseline": cpu,
             "configs": extra,
+            "gpt2": gpt2,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

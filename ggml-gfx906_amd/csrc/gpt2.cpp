@@ -30,6 +30,7 @@
 
 namespace mi355x {
 hipError_t mmvq_fused_launch(int type, const MmArgs &a, int nc, int rpw, hipStream_t st);
+hipError_t mmvq_fused_prepare(int type);
 hipError_t gpt2_embed_launch(int wtype, const void *wte, int64_t wte_nb1, const float *wpe, const int32_t *tokens,
                              const int32_t *pos, float *x, int n_seq, int n_embd, int n_vocab, int n_ctx, hipStream_t st);
 hipError_t gpt2_attn_launch(const float *qkv, float *kc, float *vc, const int32_t *pos, float *out, int n_seq, int n_head,
@@ -101,7 +102,12 @@ struct ggml_mi355x_gpt2_ctx {
 
 namespace {
 
-int hip_status(hipError_t e) { return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP; }
+int hip_status_at(hipError_t e, const char *where) {
+    if (e == hipSuccess) return GGML_MI355X_OK;
+    fprintf(stderr, "gpt2: %s: %s\n", where, hipGetErrorString(e));
+    return GGML_MI355X_EHIP;
+}
+#define hip_status(e) hip_status_at((e), #e)
 
 // widest column group with a kernel that divides n_seq
 int pick_nc(int n) {
@@ -374,6 +380,7 @@ int ggml_mi355x_gpt2_ctx_init(ggml_mi355x_gpt2_model *m, int32_t n_seq, ggml_mi3
     const size_t b_logits = m->last ? al(4 * S * hp.n_vocab) : 0;
     const size_t b_cache = al(4 * n_layers * S * hp.n_ctx * E);
     const size_t total = 2 * b_tok + 2 * b_x + b_qkv + b_h + b_logits + 2 * b_cache;
+    if (mmvq_fused_prepare(m->wtype) != hipSuccess) return GGML_MI355X_EHIP;   // before any capture
     auto *c = new ggml_mi355x_gpt2_ctx();
     c->m = m;
     c->n_seq = n_seq;
@@ -418,17 +425,17 @@ int ggml_mi355x_gpt2_decode(ggml_mi355x_gpt2_ctx *c, void *stream, int32_t use_g
     if (it == c->graphs.end()) {
         if (st == nullptr) return GGML_MI355X_EINVAL;   // the legacy default stream cannot be captured
         hipGraph_t g = nullptr;
-        if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) return GGML_MI355X_EHIP;
+        if (int rc = hip_status(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed))) return rc;
         const int rc = run_step(c, st);
         const hipError_t e = hipStreamEndCapture(st, &g);
         if (rc != 0 || e != hipSuccess) {
             if (g) (void)hipGraphDestroy(g);
-            return rc != 0 ? rc : GGML_MI355X_EHIP;
+            return rc != 0 ? rc : hip_status(e);
         }
         hipGraphExec_t ex = nullptr;
         const hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
         (void)hipGraphDestroy(g);
-        if (ei != hipSuccess) return GGML_MI355X_EHIP;
+        if (ei != hipSuccess) return hip_status(ei);
         it = c->graphs.emplace(st, ex).first;
     }
     return hip_status(hipGraphLaunch(it->second, st));

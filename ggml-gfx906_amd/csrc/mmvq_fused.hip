@@ -15,14 +15,20 @@ size_t mmvq_lds_bytes(int K, int nc);
 
 namespace {
 
+// prepare_only: just raise the instantiation's dynamic-LDS limit. That is not a stream
+// operation and fails inside a hipGraph capture, so mmvq_fused_prepare() runs it for every
+// instantiation before the engine captures a decode step.
 template <int T, int NC, int RPW>
-hipError_t fused_one(const MmArgs &a, int grid_z, hipStream_t st) {
+hipError_t fused_one(const MmArgs &a, int grid_z, hipStream_t st, bool prepare_only = false) {
     auto kern = mmvq_kernel<T, NC, RPW, false, false, true, false, true>;
     static bool attr_set = false;   // per-instantiation
     if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        // 160 KB of LDS per CU minus the prologue's static reduction array
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);
+        if (e != hipSuccess) return e;
         attr_set = true;
     }
+    if (prepare_only) return hipSuccess;
     const int rows_per_group = MMVQ_WAVES * RPW;
     const int n_groups = (a.N + rows_per_group - 1) / rows_per_group;
     const int want = std::max(1, 2048 / grid_z);
@@ -48,7 +54,37 @@ hipError_t fused_type(const MmArgs &a, int nc, int rpw, int grid_z, hipStream_t 
     return rpw <= 1 ? fused_nc<T, 1>(a, nc, grid_z, st) : fused_nc<T, 2>(a, nc, grid_z, st);
 }
 
+template <int T, int RPW>
+hipError_t prepare_nc() {
+    MmArgs a{};
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = fused_one<T, 1, RPW>(a, 1, nullptr, true);
+    if (e == hipSuccess) e = fused_one<T, 2, RPW>(a, 1, nullptr, true);
+    if (e == hipSuccess) e = fused_one<T, 3, RPW>(a, 1, nullptr, true);
+    if (e == hipSuccess) e = fused_one<T, 4, RPW>(a, 1, nullptr, true);
+    if (e == hipSuccess) e = fused_one<T, 8, RPW>(a, 1, nullptr, true);
+    return e;
+}
+
+template <int T>
+hipError_t prepare_type() {
+    const hipError_t e = prepare_nc<T, 1>();
+    return e != hipSuccess ? e : prepare_nc<T, 2>();
+}
+
 }  // namespace
+
+// raise the LDS limit of every fused instantiation of `type` (outside any graph capture)
+hipError_t mmvq_fused_prepare(int type) {
+    switch (type) {
+        case T_Q4_0: return prepare_type<T_Q4_0>();
+        case T_Q8_0: return prepare_type<T_Q8_0>();
+        case T_Q4_K: return prepare_type<T_Q4_K>();
+        case T_Q5_K: return prepare_type<T_Q5_K>();
+        case T_Q6_K: return prepare_type<T_Q6_K>();
+        default: return hipErrorInvalidValue;
+    }
+}
 
 // a.M columns in groups of nc (a.M % nc == 0); a.ne12 == a.ne13 == 1
 hipError_t mmvq_fused_launch(int type, const MmArgs &a, int nc, int rpw, hipStream_t st) {

@@ -84,26 +84,32 @@ def make_hparams(wtype: int = Q.Q4_0, **kw) -> dict:
 
 
 def partition_layers(n_layer: int, n_stages: int, head_cost: float = 1.0, embed_cost: float = 0.25) -> list:
-    """Contiguous layer ranges [(l0, l1), ...] balancing per-stage cost, where a layer costs 1,
-    the last stage's ln_f + lm_head `head_cost` and the first stage's embedding `embed_cost`
-    (decode is launch-bound: a layer is five launches, the head one wide mat-vec). Every stage
-    gets at least one layer. Greedy over the prefix sums: stage s ends where the cumulative
-    cost crosses its share."""
+    """Contiguous layer ranges [(l0, l1), ...], one per stage, minimizing the slowest stage
+    (the pipeline's tick), where a layer costs 1, the last stage's ln_f + lm_head `head_cost`
+    and the first stage's embedding `embed_cost` (decode is launch-bound: a layer is five
+    launches, the head one wide mat-vec). Every stage gets at least one layer; exact DP over
+    split points (n_layer is tens)."""
     if n_stages < 1 or n_stages > n_layer:
         raise ValueError(f"cannot split {n_layer} layers over {n_stages} stages")
-    total = n_layer + head_cost + embed_cost
-    bounds, l = [], 0
-    for s in range(n_stages):
-        if s == n_stages - 1:
-            bounds.append((l, n_layer))
-            break
-        target = total * (s + 1) / n_stages - (embed_cost)
-        end = l + 1
-        while end < n_layer - (n_stages - 1 - s) and end + 0.5 <= target:
-            end += 1
-        bounds.append((l, end))
-        l = end
-    return bounds
+    INF = float("inf")
+
+    def cost(s, a, b):
+        return (b - a) + (embed_cost if s == 0 else 0.0) + (head_cost if s == n_stages - 1 else 0.0)
+
+    # best[s][b] = (max stage cost, split) for stages 0..s covering layers [0, b)
+    best = [[(INF, None)] * (n_layer + 1) for _ in range(n_stages)]
+    for b in range(1, n_layer + 1):
+        best[0][b] = (cost(0, 0, b), [(0, b)])
+    for s in range(1, n_stages):
+        for b in range(s + 1, n_layer + 1):
+            for a in range(s, b):
+                prev, split = best[s - 1][a]
+                if split is None:
+                    continue
+                c = max(prev, cost(s, a, b))
+                if c < best[s][b][0] - 1e-9:
+                    best[s][b] = (c, split + [(a, b)])
+    return best[n_stages - 1][n_layer][1]
 
 
 class Stage:
@@ -249,32 +255,37 @@ class Pipeline:
         self.next, self.prev = (rank + 1) % world, (rank - 1) % world
         self.recv = [torch.zeros(msg_elems, dtype=torch.float32, device=device) for _ in range(2)]
         self.group = group
+        self.cur = 0
+        self.k = 0
 
-    def run(self, n_ticks: int, stage_fn, first_input_fn):
-        """Runs n_ticks ticks. At tick k this rank holds micro-batch m = (k - rank) mod n_micro,
-        valid once k >= rank. Stage 0's input at its first visit of a micro-batch comes from
+    def tick(self, k: int, stage_fn, first_input_fn) -> bool:
+        """Tick k: this rank holds micro-batch m = (k - rank) mod n_micro, valid once k >= rank.
+        Stage 0's input on its first visit of a micro-batch (k < n_micro) comes from
         first_input_fn(mb) (the prompt), afterwards from the ring (the last stage's tokens).
-        Returns the number of (tick, micro-batch) steps this rank computed."""
+        Ends with the tick's one batched exchange. Returns whether a real step was computed."""
         import torch.distributed as dist
+        mb = (k - self.rank) % self.n_micro
+        valid = k >= self.rank
+        if self.rank == 0 and k < self.n_micro:
+            inbuf = first_input_fn(mb)
+        else:
+            inbuf = self.recv[self.cur]
+        out = stage_fn(mb, inbuf, valid)
+        if self.world > 1:
+            nxt = 1 - self.cur
+            ops = [dist.P2POp(dist.isend, out, self.next, self.group),
+                   dist.P2POp(dist.irecv, self.recv[nxt], self.prev, self.group)]
+            for r in dist.batch_isend_irecv(ops):
+                r.wait()
+            self.cur = nxt
+        else:
+            self.recv[self.cur].copy_(out)
+        return valid
+
+    def run(self, n_ticks: int, stage_fn, first_input_fn) -> int:
+        """n_ticks more ticks; returns how many real steps this rank computed"""
         done = 0
-        cur = 0
-        for k in range(n_ticks):
-            mb = (k - self.rank) % self.n_micro
-            valid = k >= self.rank
-            if self.rank == 0:
-                inbuf = first_input_fn(mb) if k < self.n_micro else self.recv[cur]
-            else:
-                inbuf = self.recv[cur]
-            out = stage_fn(mb, inbuf, valid)
-            if valid:
-                done += 1
-            if self.world > 1:
-                nxt = 1 - cur
-                ops = [dist.P2POp(dist.isend, out, self.next, self.group),
-                       dist.P2POp(dist.irecv, self.recv[nxt], self.prev, self.group)]
-                for r in dist.batch_isend_irecv(ops):
-                    r.wait()
-                cur = nxt
-            else:
-                self.recv[cur].copy_(out)
+        for _ in range(n_ticks):
+            done += self.tick(self.k, stage_fn, first_input_fn)
+            self.k += 1
         return done

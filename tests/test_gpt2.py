@@ -6,9 +6,16 @@ checkpoints of every hot weight type are committed (tests/golden/gpt2_*.logits.f
 oracle/gen_gpt2_golden.py); the checkpoints are regenerated bit-identically from their seed
 (sha256 checked). At the full 117M shape the oracle binary runs live next to the engine.
 
-Tolerance: NMSE <= 5e-4 per position against the reference's logits — the reference's own
-MUL_MAT bar (tests/test-backend-ops.cpp:3106-3108); the engine's int8 activations and fused
-f32 arithmetic differ from ggml-cpu's Q8 activations only by rounding.
+Tolerances, per position (NMSE, the reference's own measure, tests/test-backend-ops.cpp:
+3106-3108, whose per-op bar is 5e-4):
+  * engine vs the EXACT forward (oracle/gpt2_np.py: float64 on the bit-exact dequantized
+    weights, unquantized activations): <= 5e-4 — the engine is as close to the exact product
+    as one reference op is allowed to be;
+  * engine vs the reference's ggml-cpu logits: <= 1e-3. Both sides quantize activations
+    (ggml-cpu: Q8_0 blocks for Q4_0/Q8_0 weights, coarser per-256 Q8_K for the K-quants,
+    src/ggml-cpu/ggml-cpu.c:1264-1299; ours: int8 per 32), so each sits up to ~5e-4 from
+    exact (measured: ggml-cpu 2e-4 for Q4_0/Q8_0, 4.3e-4 for the K-quants, pinned by
+    test_reference_cpu_is_near_exact) and their difference is bounded by the sum.
 """
 import json
 import os
@@ -27,7 +34,8 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 REF_BIN = os.path.join(ROOT, "oracle", "_ref", "gpt2_ref")
 MANIFEST = json.load(open(os.path.join(GOLDEN, "gpt2_manifest.json")))
 SMALL = MANIFEST["hparams"]
-NMSE_MAX = 5e-4
+NMSE_MAX = 5e-4          # vs the exact forward
+NMSE_VS_REF = 1e-3       # vs the reference ggml-cpu (two quantized-activation paths)
 
 
 def nmse(a, b):
@@ -86,6 +94,27 @@ def test_read_hparams_host_only():
     open(bad, "wb").write(b"\0" * 64)
     with pytest.raises(Exception):
         G.read_hparams(bad)
+
+
+_exact = {}
+
+
+def exact_logits(name: str, n: int) -> np.ndarray:
+    import gpt2_np
+    if (name, n) not in _exact:
+        _exact[(name, n)] = gpt2_np.logits(small_model(name), MANIFEST["cases"][name]["tokens"][:n])
+    return _exact[(name, n)]
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST["cases"]))
+def test_reference_cpu_is_near_exact(name):
+    """pins the float64 forward to the reference: ggml-cpu's logits sit within its own
+    per-op bar of the exact product on every position"""
+    want = exact_logits(name, 12)
+    got = golden_logits(name)[:12]
+    errs = [nmse(got[i], want[i]) for i in range(12)]
+    assert max(errs) <= NMSE_MAX, errs
+    assert (got.argmax(1) == want.argmax(1)).mean() >= 0.9
 
 
 @pytest.mark.skipif(not os.path.exists(REF_BIN), reason="oracle/_ref not built")
@@ -229,12 +258,15 @@ def _run_logits(path, tokens, n_seq=1, graph=True, split=None):
 def test_engine_matches_reference_logits(name):
     c = MANIFEST["cases"][name]
     got = _run_logits(small_model(name), c["tokens"])[:, 0]
+    assert np.isfinite(got).all()
     want = golden_logits(name)
     errs = [nmse(got[i], want[i]) for i in range(len(want))]
+    assert max(errs) <= NMSE_VS_REF, errs
+    assert (got.argmax(1) == want.argmax(1)).mean() >= 0.9
+    n = min(len(want), 24)
+    ex = exact_logits(name, n)
+    errs = [nmse(got[i], ex[i]) for i in range(n)]
     assert max(errs) <= NMSE_MAX, errs
-    assert np.isfinite(got).all()
-    agree = (got.argmax(1) == want.argmax(1)).mean()
-    assert agree >= 0.9, agree
 
 
 @pytest.mark.gpu
@@ -300,7 +332,7 @@ def test_engine_117m_matches_reference_live():
     got = _run_logits(path, toks)[:, 0]
     errs = [nmse(got[i], want[i]) for i in range(len(toks))]
     os.remove(path)
-    assert max(errs) <= NMSE_MAX, max(errs)
+    assert max(errs) <= NMSE_VS_REF, max(errs)
 
 
 @pytest.mark.gpu
@@ -316,4 +348,4 @@ def test_reference_scheduler_drives_plugin():
     got = np.fromfile(out, np.float32).reshape(24, -1)
     want = golden_logits("q4_0")[:24]
     errs = [nmse(got[i], want[i]) for i in range(24)]
-    assert max(errs) <= NMSE_MAX, errs
+    assert max(errs) <= NMSE_VS_REF, errs
