@@ -33,8 +33,9 @@ hipError_t mmvq_fused_launch(int type, const MmArgs &a, int nc, int rpw, hipStre
 hipError_t mmvq_fused_prepare(int type);
 hipError_t gpt2_embed_launch(int wtype, const void *wte, int64_t wte_nb1, const float *wpe, const int32_t *tokens,
                              const int32_t *pos, float *x, int n_seq, int n_embd, int n_vocab, int n_ctx, hipStream_t st);
-hipError_t gpt2_attn_launch(const float *qkv, float *kc, float *vc, const int32_t *pos, float *out, int n_seq, int n_head,
-                            int n_embd, int n_ctx, float scale, hipStream_t st);
+int gpt2_attn_nsplit(int n_ctx);
+hipError_t gpt2_attn_launch(const float *qkv, float *kc, float *vc, const int32_t *pos, float *out, float *part, uint32_t *counter,
+                            int n_seq, int n_head, int n_embd, int n_ctx, float scale, hipStream_t st);
 hipError_t gpt2_argmax_launch(const float *logits, int n_seq, int n_vocab, int32_t *tokens, hipStream_t st);
 hipError_t gpt2_advance_launch(int32_t *pos, int n_seq, hipStream_t st);
 }  // namespace mi355x
@@ -97,6 +98,8 @@ struct ggml_mi355x_gpt2_ctx {
     int32_t *tokens = nullptr, *pos = nullptr;
     float *x = nullptr, *qkv = nullptr, *attn = nullptr, *h = nullptr, *logits = nullptr;
     float *kc = nullptr, *vc = nullptr;        // [layer][seq][n_ctx][n_embd]
+    float *part = nullptr;                     // attention split partials [seq][head][split][2 + 64]
+    uint32_t *counter = nullptr;               // attention split arrival counters [seq][head]
     std::map<hipStream_t, hipGraphExec_t> graphs;
 };
 
@@ -161,7 +164,8 @@ int run_step(ggml_mi355x_gpt2_ctx *c, hipStream_t st) {
         float *kc = c->kc + (size_t)(l - m->l0) * cache_layer;
         float *vc = c->vc + (size_t)(l - m->l0) * cache_layer;
         if ((rc = fused_matvec(c, L.attn_w, c->x, c->qkv, &L.ln1_g, &L.ln1_b, &L.attn_b, 0, st))) return rc;
-        if ((rc = hip_status(gpt2_attn_launch(c->qkv, kc, vc, c->pos, c->attn, c->n_seq, hp.n_head, E, hp.n_ctx, kq_scale, st)))) return rc;
+        if ((rc = hip_status(gpt2_attn_launch(c->qkv, kc, vc, c->pos, c->attn, c->part, c->counter, c->n_seq, hp.n_head, E, hp.n_ctx,
+                                              kq_scale, st)))) return rc;
         if ((rc = fused_matvec(c, L.proj_w, c->attn, c->x, nullptr, nullptr, &L.proj_b, EPI_RESID, st))) return rc;
         if ((rc = fused_matvec(c, L.fc_w, c->x, c->h, &L.ln2_g, &L.ln2_b, &L.fc_b, EPI_GELU, st))) return rc;
         if ((rc = fused_matvec(c, L.mproj_w, c->h, c->x, nullptr, nullptr, &L.mproj_b, EPI_RESID, st))) return rc;
@@ -379,7 +383,9 @@ int ggml_mi355x_gpt2_ctx_init(ggml_mi355x_gpt2_model *m, int32_t n_seq, ggml_mi3
     const size_t b_tok = al(4 * S), b_x = al(4 * S * E), b_qkv = al(12 * S * E), b_h = al(16 * S * E);
     const size_t b_logits = m->last ? al(4 * S * hp.n_vocab) : 0;
     const size_t b_cache = al(4 * n_layers * S * hp.n_ctx * E);
-    const size_t total = 2 * b_tok + 2 * b_x + b_qkv + b_h + b_logits + 2 * b_cache;
+    const size_t b_part = al(4 * S * hp.n_head * gpt2_attn_nsplit(hp.n_ctx) * 66);
+    const size_t b_cnt = al(4 * S * hp.n_head);
+    const size_t total = 2 * b_tok + 2 * b_x + b_qkv + b_h + b_logits + 2 * b_cache + b_part + b_cnt;
     if (mmvq_fused_prepare(m->wtype) != hipSuccess) return GGML_MI355X_EHIP;   // before any capture
     auto *c = new ggml_mi355x_gpt2_ctx();
     c->m = m;
@@ -399,6 +405,8 @@ int ggml_mi355x_gpt2_ctx_init(ggml_mi355x_gpt2_model *m, int32_t n_seq, ggml_mi3
     c->logits = m->last ? reinterpret_cast<float *>(take(b_logits)) : nullptr;
     c->kc = reinterpret_cast<float *>(take(b_cache));
     c->vc = reinterpret_cast<float *>(take(b_cache));
+    c->part = reinterpret_cast<float *>(take(b_part));
+    c->counter = reinterpret_cast<uint32_t *>(take(b_cnt));
     if (hipMemset(c->arena, 0, total) != hipSuccess) {
         (void)hipFree(c->arena);
         delete c;

@@ -16,6 +16,8 @@
 // Positions live in device memory, so one captured hipGraph replays every decode step.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "deq.h"
 
 namespace mi355x {
@@ -44,71 +46,128 @@ __global__ __launch_bounds__(256) void embed_kernel(const uint8_t *__restrict__ 
     }
 }
 
-// grid (n_head, n_seq), 256 threads = 4 waves; dynamic LDS: n_ctx floats of scores
+// Split-key decode attention ("flash decoding"): grid (n_head, n_seq, nsplit), 256 threads.
+// Workgroup (h, s, c) takes keys [c*chunk, min(p+1, (c+1)*chunk)), chunk = ceil((p+1)/nsplit)
+// with p = pos[s] read on the device, so one captured launch serves every position and all
+// nsplit*n_head*n_seq workgroups stream the cache in parallel. Each writes (max, sum, o[64])
+// of its keys; the last to finish (device-scope counter, release/acquire fences across the 8
+// XCDs' L2s) merges them with the usual rescaling and resets the counter for the next launch.
+// Dynamic LDS: chunk_max floats of scores.
 __global__ __launch_bounds__(256) void attn_decode_kernel(const float *__restrict__ qkv, float *__restrict__ kc, float *__restrict__ vc,
-                                                          const int32_t *__restrict__ pos, float *__restrict__ out, int n_embd,
-                                                          int n_ctx, float scale) {
+                                                          const int32_t *__restrict__ pos, float *__restrict__ out, float *__restrict__ part,
+                                                          uint32_t *__restrict__ counter, int n_embd, int n_ctx, float scale) {
     extern __shared__ float sc[];
     __shared__ float red[4][HEAD_DIM];
     __shared__ float rmax[4], rsum[4];
-    const int h = blockIdx.x, s = blockIdx.y;
+    __shared__ bool is_last;
+    const int h = blockIdx.x, s = blockIdx.y, c = blockIdx.z, nsplit = gridDim.z;
+    const int n_head = gridDim.x;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int p = min(max(pos[s], 0), n_ctx - 1);
+    const int nk = p + 1;
+    const int chunk = (nk + nsplit - 1) / nsplit;
+    const int j0 = c * chunk, j1 = min(nk, j0 + chunk);
     const float *q = qkv + (int64_t)s * 3 * n_embd + h * HEAD_DIM;
     const float *kcur = q + n_embd;
     const float *vcur = q + 2 * n_embd;
     float *K = kc + (int64_t)s * n_ctx * n_embd + h * HEAD_DIM;
     float *V = vc + (int64_t)s * n_ctx * n_embd + h * HEAD_DIM;
+    float *pm = part + ((int64_t)(s * n_head + h) * nsplit + c) * (HEAD_DIM + 2);
 
-    // store the new token's K and V (the reference's ggml_cpy into memory_k / memory_v)
-    if (tid < HEAD_DIM) {
+    // the new token's K and V go to the cache once (the reference's ggml_cpy into memory_k/v);
+    // this launch reads them from qkv, later launches from the cache
+    if (c == 0 && tid < HEAD_DIM) {
         K[(int64_t)p * n_embd + tid] = kcur[tid];
         V[(int64_t)p * n_embd + tid] = vcur[tid];
     }
 
-    // scores: 4 lanes per key, 16 dims each (float4 x 4); 16 keys per wave per pass
-    const int g = lane >> 2, sub = lane & 3;
-    float4 qv[4];
+    float mx = -INFINITY, l = 0.f;
+    if (j0 < j1) {
+        // scores: 4 lanes per key (16 dims each), 64 keys per pass
+        const int g = tid >> 2, sub = tid & 3;
+        float4 qv[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) qv[i] = reinterpret_cast<const float4 *>(q + sub * 16)[i];
-    float lmax = -INFINITY;
-    for (int j = wave * 16 + g; j <= p; j += 64) {
-        const float *kr = (j == p ? kcur : K + (int64_t)j * n_embd) + sub * 16;
-        float d = 0.f;
+        for (int i = 0; i < 4; ++i) qv[i] = reinterpret_cast<const float4 *>(q + sub * 16)[i];
+        float lmax = -INFINITY;
+        for (int j = j0 + g; j < j1; j += 64) {
+            const float *kr = (j == p ? kcur : K + (int64_t)j * n_embd) + sub * 16;
+            float4 kv[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float4 kv = reinterpret_cast<const float4 *>(kr)[i];
-            d += qv[i].x * kv.x + qv[i].y * kv.y + qv[i].z * kv.z + qv[i].w * kv.w;
+            for (int i = 0; i < 4; ++i) kv[i] = reinterpret_cast<const float4 *>(kr)[i];
+            float d = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) d += qv[i].x * kv[i].x + qv[i].y * kv[i].y + qv[i].z * kv[i].z + qv[i].w * kv[i].w;
+            d += dpp_f<DPP_XOR1>(d);
+            d += dpp_f<DPP_XOR2>(d);
+            d *= scale;
+            if (sub == 0) sc[j - j0] = d;
+            lmax = fmaxf(lmax, d);
         }
-        d += dpp_f<DPP_XOR1>(d);
-        d += dpp_f<DPP_XOR2>(d);
-        d *= scale;
-        if (sub == 0) sc[j] = d;
-        lmax = fmaxf(lmax, d);
-    }
-    // softmax over [0, p] (src/ggml-cpu/ops.cpp soft_max: max, exp(x - max), 1/sum)
-    lmax = fmaxf(lmax, xchg<1>(lmax)); lmax = fmaxf(lmax, xchg<2>(lmax)); lmax = fmaxf(lmax, xchg<4>(lmax));
-    lmax = fmaxf(lmax, xchg<8>(lmax)); lmax = fmaxf(lmax, xchg<16>(lmax)); lmax = fmaxf(lmax, xchg<32>(lmax));
-    if (lane == 0) rmax[wave] = lmax;
-    __syncthreads();
-    const float mx = fmaxf(fmaxf(rmax[0], rmax[1]), fmaxf(rmax[2], rmax[3]));
-    float lsum = 0.f;
-    for (int j = tid; j <= p; j += 256) {
-        const float e = expf(sc[j] - mx);
-        sc[j] = e;
-        lsum += e;
-    }
-    lsum = wave_sum(lsum);
-    if (lane == 0) rsum[wave] = lsum;
-    __syncthreads();
-    const float inv = 1.0f / ((rsum[0] + rsum[1]) + (rsum[2] + rsum[3]));
+        lmax = fmaxf(lmax, xchg<1>(lmax)); lmax = fmaxf(lmax, xchg<2>(lmax)); lmax = fmaxf(lmax, xchg<4>(lmax));
+        lmax = fmaxf(lmax, xchg<8>(lmax)); lmax = fmaxf(lmax, xchg<16>(lmax)); lmax = fmaxf(lmax, xchg<32>(lmax));
+        if (lane == 0) rmax[wave] = lmax;
+        __syncthreads();
+        mx = fmaxf(fmaxf(rmax[0], rmax[1]), fmaxf(rmax[2], rmax[3]));
+        float lsum = 0.f;
+        for (int j = j0 + tid; j < j1; j += 256) {
+            const float e = expf(sc[j - j0] - mx);
+            sc[j - j0] = e;
+            lsum += e;
+        }
+        lsum = wave_sum(lsum);
+        if (lane == 0) rsum[wave] = lsum;
+        __syncthreads();
+        l = (rsum[0] + rsum[1]) + (rsum[2] + rsum[3]);
 
-    // KQV: wave w sums keys j = w, w+4, ...; lane = head dimension (coalesced 256-B rows)
-    float acc = 0.f;
-    for (int j = wave; j <= p; j += 4) acc += sc[j] * (j == p ? vcur[lane] : V[(int64_t)j * n_embd + lane]);
-    red[wave][lane] = acc;
+        // o = sum_j e_j V_j: lane = (key slot ks = lane >> 4, dims 4*(lane & 15) .. +3), a wave
+        // covers 4 keys per pass (coalesced 256-B rows), the workgroup 16; 2 passes in flight
+        const int ks = lane >> 4, dq = (lane & 15) * 4;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = j0 + wave * 4 + ks; j < j1; j += 16) {
+            const float e = sc[j - j0];
+            const float4 v = *reinterpret_cast<const float4 *>((j == p ? vcur : V + (int64_t)j * n_embd) + dq);
+            acc.x += e * v.x; acc.y += e * v.y; acc.z += e * v.z; acc.w += e * v.w;
+        }
+        acc.x += xchg<16>(acc.x); acc.y += xchg<16>(acc.y); acc.z += xchg<16>(acc.z); acc.w += xchg<16>(acc.w);
+        acc.x += xchg<32>(acc.x); acc.y += xchg<32>(acc.y); acc.z += xchg<32>(acc.z); acc.w += xchg<32>(acc.w);
+        if (lane < 16) *reinterpret_cast<float4 *>(&red[wave][dq]) = acc;
+        __syncthreads();
+        if (tid < HEAD_DIM) pm[2 + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+    } else if (tid < HEAD_DIM) {
+        pm[2 + tid] = 0.f;
+    }
+    if (tid == 0) {
+        pm[0] = mx;
+        pm[1] = l;
+    }
+
+    // last-arriving workgroup of (h, s) merges the nsplit partials
+    __threadfence();
     __syncthreads();
-    if (wave == 0) out[(int64_t)s * n_embd + h * HEAD_DIM + lane] = ((red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane])) * inv;
+    if (tid == 0) {
+        const uint32_t prev = atomicAdd(&counter[s * n_head + h], 1u);
+        is_last = prev == (uint32_t)nsplit - 1;
+    }
+    __syncthreads();
+    if (!is_last) return;
+    __threadfence();
+    if (tid < HEAD_DIM) {
+        const float *pb = part + (int64_t)(s * n_head + h) * nsplit * (HEAD_DIM + 2);
+        float M = -INFINITY;
+        for (int i = 0; i < nsplit; ++i) M = fmaxf(M, __builtin_nontemporal_load(pb + i * (HEAD_DIM + 2)));
+        float L = 0.f, O = 0.f;
+        for (int i = 0; i < nsplit; ++i) {
+            const float *pi = pb + i * (HEAD_DIM + 2);
+            const float li = __builtin_nontemporal_load(pi + 1);
+            if (li > 0.f) {
+                const float w = expf(__builtin_nontemporal_load(pi) - M);
+                L += w * li;
+                O += w * __builtin_nontemporal_load(pi + 2 + tid);
+            }
+        }
+        out[(int64_t)s * n_embd + h * HEAD_DIM + tid] = O / L;
+    }
+    if (tid == 0) counter[s * n_head + h] = 0u;
 }
 
 __global__ __launch_bounds__(1024) void argmax_kernel(const float *__restrict__ logits, int n_vocab, int32_t *__restrict__ tokens) {
@@ -159,11 +218,16 @@ hipError_t gpt2_embed_launch(int wtype, const void *wte, int64_t wte_nb1, const 
     return hipGetLastError();
 }
 
-hipError_t gpt2_attn_launch(const float *qkv, float *kc, float *vc, const int32_t *pos, float *out, int n_seq, int n_head,
-                            int n_embd, int n_ctx, float scale, hipStream_t st) {
+// keys per split: at most 64 (the score pass width); n_ctx = 1024 -> 16 splits
+int gpt2_attn_nsplit(int n_ctx) { return std::min(64, std::max(1, (n_ctx + 63) / 64)); }
+
+hipError_t gpt2_attn_launch(const float *qkv, float *kc, float *vc, const int32_t *pos, float *out, float *part, uint32_t *counter,
+                            int n_seq, int n_head, int n_embd, int n_ctx, float scale, hipStream_t st) {
     if (n_embd != n_head * HEAD_DIM) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(attn_decode_kernel, dim3(n_head, n_seq), dim3(256), (size_t)n_ctx * sizeof(float), st, qkv, kc, vc, pos, out,
-                       n_embd, n_ctx, scale);
+    const int nsplit = gpt2_attn_nsplit(n_ctx);
+    const int chunk_max = (n_ctx + nsplit - 1) / nsplit;
+    hipLaunchKernelGGL(attn_decode_kernel, dim3(n_head, n_seq, nsplit), dim3(256), (size_t)chunk_max * sizeof(float), st, qkv, kc, vc,
+                       pos, out, part, counter, n_embd, n_ctx, scale);
     return hipGetLastError();
 }
 
