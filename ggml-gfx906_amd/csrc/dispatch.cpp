@@ -71,6 +71,8 @@ bool is_hot_quant(int t) { return type_blck(t) != 0; }
 // matrix needs all 512 workgroups of RPW=1 to cover 256 CUs twice; batched / taller problems
 // (rows x batch) switch to 2 and 4 rows per wave.
 static int pick_rpw(int64_t rows_total) {
+    static const int force = getenv("GGML_MI355X_RPW") ? atoi(getenv("GGML_MI355X_RPW")) : 0;
+    if (force > 0) return force;
     return rows_total >= 16384 ? 2 : 1;
 }
 

@@ -33,10 +33,10 @@ hipError_t mmvq_fused_launch(int type, const MmArgs &a, int nc, int rpw, hipStre
 hipError_t mmvq_fused_prepare(int type);
 hipError_t gpt2_embed_launch(int wtype, const void *wte, int64_t wte_nb1, const float *wpe, const int32_t *tokens,
                              const int32_t *pos, float *x, int n_seq, int n_embd, int n_vocab, int n_ctx, hipStream_t st);
-int gpt2_attn_nsplit(int n_ctx);
-hipError_t gpt2_attn_launch(const float *qkv, float *kc, float *vc, const int32_t *pos, float *out, float *part, uint32_t *counter,
-                            int n_seq, int n_head, int n_embd, int n_ctx, float scale, hipStream_t st);
-hipError_t gpt2_argmax_launch(const float *logits, int n_seq, int n_vocab, int32_t *tokens, hipStream_t st);
+hipError_t gpt2_attn_launch(const float *qkv, float *kc, float *vc, const int32_t *pos, float *out, int n_seq, int n_head,
+                            int n_embd, int n_ctx, float scale, hipStream_t st);
+hipError_t gpt2_argmax_launch(const float *pv, const int32_t *pi, int n_seq, int32_t *tokens, int32_t *pos, hipStream_t st);
+hipError_t gpt2_argmax_reset(float *pv, int32_t *pi, int n_seq, hipStream_t st);
 hipError_t gpt2_advance_launch(int32_t *pos, int n_seq, hipStream_t st);
 }  // namespace mi355x
 
@@ -98,8 +98,8 @@ struct ggml_mi355x_gpt2_ctx {
     int32_t *tokens = nullptr, *pos = nullptr;
     float *x = nullptr, *qkv = nullptr, *attn = nullptr, *h = nullptr, *logits = nullptr;
     float *kc = nullptr, *vc = nullptr;        // [layer][seq][n_ctx][n_embd]
-    float *part = nullptr;                     // attention split partials [seq][head][split][2 + 64]
-    uint32_t *counter = nullptr;               // attention split arrival counters [seq][head]
+    float *amax_v = nullptr;                   // lm_head per-workgroup argmax partials [seq][ARGMAX_SLOTS]
+    int32_t *amax_i = nullptr;
     std::map<hipStream_t, hipGraphExec_t> graphs;
 };
 
@@ -122,6 +122,7 @@ int pick_nc(int n) {
 // y[n_seq][N] (+)= W[N][K] . x[n_seq][K] with the fused prologue / epilogue
 int fused_matvec(const ggml_mi355x_gpt2_ctx *c, const Tensor &w, const float *x, float *y, const Tensor *ln_g, const Tensor *ln_b,
                  const Tensor *bias, int epi, hipStream_t st) {
+    // EPI_ARGMAX writes one partial per workgroup: ARGMAX_SLOTS bounds the grid (mmvq_fused.hip)
     MmArgs a{};
     const int K = (int)w.ne0, N = (int)w.ne1, M = c->n_seq;
     a.w = w.data;
@@ -143,6 +144,8 @@ int fused_matvec(const ggml_mi355x_gpt2_ctx *c, const Tensor &w, const float *x,
     a.ln_eps = 1e-5f;   // gpt2_hparams::eps, main-sched.cpp:51
     a.bias = bias ? reinterpret_cast<const float *>(bias->data) : nullptr;
     a.epi = epi;
+    a.amax_v = c->amax_v;
+    a.amax_i = c->amax_i;
     a.fused = 1;
     return hip_status(mmvq_fused_launch(w.type, a, pick_nc(M), N >= 16384 ? 2 : 1, st));
 }
@@ -164,15 +167,16 @@ int run_step(ggml_mi355x_gpt2_ctx *c, hipStream_t st) {
         float *kc = c->kc + (size_t)(l - m->l0) * cache_layer;
         float *vc = c->vc + (size_t)(l - m->l0) * cache_layer;
         if ((rc = fused_matvec(c, L.attn_w, c->x, c->qkv, &L.ln1_g, &L.ln1_b, &L.attn_b, 0, st))) return rc;
-        if ((rc = hip_status(gpt2_attn_launch(c->qkv, kc, vc, c->pos, c->attn, c->part, c->counter, c->n_seq, hp.n_head, E, hp.n_ctx,
-                                              kq_scale, st)))) return rc;
+        if ((rc = hip_status(gpt2_attn_launch(c->qkv, kc, vc, c->pos, c->attn, c->n_seq, hp.n_head, E, hp.n_ctx, kq_scale, st)))) return rc;
         if ((rc = fused_matvec(c, L.proj_w, c->attn, c->x, nullptr, nullptr, &L.proj_b, EPI_RESID, st))) return rc;
         if ((rc = fused_matvec(c, L.fc_w, c->x, c->h, &L.ln2_g, &L.ln2_b, &L.fc_b, EPI_GELU, st))) return rc;
         if ((rc = fused_matvec(c, L.mproj_w, c->h, c->x, nullptr, nullptr, &L.mproj_b, EPI_RESID, st))) return rc;
     }
     if (m->last) {
-        if ((rc = fused_matvec(c, m->lm_head, c->x, c->logits, &m->ln_f_g, &m->ln_f_b, nullptr, 0, st))) return rc;
-        if ((rc = hip_status(gpt2_argmax_launch(c->logits, c->n_seq, hp.n_vocab, c->tokens, st)))) return rc;
+        // lm_head with the per-workgroup argmax epilogue, then one small launch that picks the
+        // token and advances the positions
+        if ((rc = fused_matvec(c, m->lm_head, c->x, c->logits, &m->ln_f_g, &m->ln_f_b, nullptr, EPI_ARGMAX, st))) return rc;
+        return hip_status(gpt2_argmax_launch(c->amax_v, c->amax_i, c->n_seq, c->tokens, c->pos, st));
     }
     return hip_status(gpt2_advance_launch(c->pos, c->n_seq, st));
 }
@@ -383,9 +387,8 @@ int ggml_mi355x_gpt2_ctx_init(ggml_mi355x_gpt2_model *m, int32_t n_seq, ggml_mi3
     const size_t b_tok = al(4 * S), b_x = al(4 * S * E), b_qkv = al(12 * S * E), b_h = al(16 * S * E);
     const size_t b_logits = m->last ? al(4 * S * hp.n_vocab) : 0;
     const size_t b_cache = al(4 * n_layers * S * hp.n_ctx * E);
-    const size_t b_part = al(4 * S * hp.n_head * gpt2_attn_nsplit(hp.n_ctx) * 66);
-    const size_t b_cnt = al(4 * S * hp.n_head);
-    const size_t total = 2 * b_tok + 2 * b_x + b_qkv + b_h + b_logits + 2 * b_cache + b_part + b_cnt;
+    const size_t b_amax = m->last ? al(4 * S * ARGMAX_SLOTS) : 0;
+    const size_t total = 2 * b_tok + 2 * b_x + b_qkv + b_h + b_logits + 2 * b_cache + 2 * b_amax;
     if (mmvq_fused_prepare(m->wtype) != hipSuccess) return GGML_MI355X_EHIP;   // before any capture
     auto *c = new ggml_mi355x_gpt2_ctx();
     c->m = m;
@@ -405,9 +408,12 @@ int ggml_mi355x_gpt2_ctx_init(ggml_mi355x_gpt2_model *m, int32_t n_seq, ggml_mi3
     c->logits = m->last ? reinterpret_cast<float *>(take(b_logits)) : nullptr;
     c->kc = reinterpret_cast<float *>(take(b_cache));
     c->vc = reinterpret_cast<float *>(take(b_cache));
-    c->part = reinterpret_cast<float *>(take(b_part));
-    c->counter = reinterpret_cast<uint32_t *>(take(b_cnt));
-    if (hipMemset(c->arena, 0, total) != hipSuccess) {
+    if (m->last) {
+        c->amax_v = reinterpret_cast<float *>(take(b_amax));
+        c->amax_i = reinterpret_cast<int32_t *>(take(b_amax));
+    }
+    if (hipMemset(c->arena, 0, total) != hipSuccess ||
+        (m->last && (gpt2_argmax_reset(c->amax_v, c->amax_i, n_seq, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess))) {
         (void)hipFree(c->arena);
         delete c;
         return GGML_MI355X_EHIP;

@@ -19,6 +19,7 @@
 #include <algorithm>
 
 #include "deq.h"
+#include "mmvq_impl.h"   // group_reduce_transpose
 
 namespace mi355x {
 
@@ -46,140 +47,125 @@ __global__ __launch_bounds__(256) void embed_kernel(const uint8_t *__restrict__ 
     }
 }
 
-// Split-key decode attention ("flash decoding"): grid (n_head, n_seq, nsplit), 256 threads.
-// Workgroup (h, s, c) takes keys [c*chunk, min(p+1, (c+1)*chunk)), chunk = ceil((p+1)/nsplit)
-// with p = pos[s] read on the device, so one captured launch serves every position and all
-// nsplit*n_head*n_seq workgroups stream the cache in parallel. Each writes (max, sum, o[64])
-// of its keys; the last to finish (device-scope counter, release/acquire fences across the 8
-// XCDs' L2s) merges them with the usual rescaling and resets the counter for the next launch.
-// Dynamic LDS: chunk_max floats of scores.
-__global__ __launch_bounds__(256) void attn_decode_kernel(const float *__restrict__ qkv, float *__restrict__ kc, float *__restrict__ vc,
-                                                          const int32_t *__restrict__ pos, float *__restrict__ out, float *__restrict__ part,
-                                                          uint32_t *__restrict__ counter, int n_embd, int n_ctx, float scale) {
-    extern __shared__ float sc[];
-    __shared__ float red[4][HEAD_DIM];
-    __shared__ float rmax[4], rsum[4];
-    __shared__ bool is_last;
-    const int h = blockIdx.x, s = blockIdx.y, c = blockIdx.z, nsplit = gridDim.z;
-    const int n_head = gridDim.x;
+// Decode attention, one workgroup of 8 waves per (head, sequence), no cross-workgroup traffic.
+// The p + 1 visible keys (p = pos[s], read on the device, so one captured launch serves every
+// position) are cut into 8 contiguous chunks, one per wave; inside a wave each lane owns keys
+// j = j0 + lane + 64 t and keeps a flash-decoding state of its own (running max m, sum l and
+// the 64-wide o = sum_j exp(s_j - m) V_j in registers). The lane states merge with one
+// butterfly transpose over the wave (64 partial o vectors -> lane d holds o[d]); the 8 wave
+// states merge in LDS. Every K/V row is read once, as 16 dwordx4 per lane, K and V of a pass
+// in flight together. Numerically this is the reference's softmax(K.q * scale) . V
+// (main-sched.cpp:685-735) evaluated in the rescaling order of online softmax.
+__global__ __launch_bounds__(512) void attn_decode_kernel(const float *__restrict__ qkv, float *__restrict__ kc, float *__restrict__ vc,
+                                                          const int32_t *__restrict__ pos, float *__restrict__ out, int n_embd, int n_ctx,
+                                                          float scale) {
+    __shared__ float4 qs[HEAD_DIM / 4];
+    __shared__ float wo[8][HEAD_DIM];
+    __shared__ float wm[8], wl[8];
+    const int h = blockIdx.x, s = blockIdx.y;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int p = min(max(pos[s], 0), n_ctx - 1);
     const int nk = p + 1;
-    const int chunk = (nk + nsplit - 1) / nsplit;
-    const int j0 = c * chunk, j1 = min(nk, j0 + chunk);
     const float *q = qkv + (int64_t)s * 3 * n_embd + h * HEAD_DIM;
     const float *kcur = q + n_embd;
     const float *vcur = q + 2 * n_embd;
     float *K = kc + (int64_t)s * n_ctx * n_embd + h * HEAD_DIM;
     float *V = vc + (int64_t)s * n_ctx * n_embd + h * HEAD_DIM;
-    float *pm = part + ((int64_t)(s * n_head + h) * nsplit + c) * (HEAD_DIM + 2);
 
-    // the new token's K and V go to the cache once (the reference's ggml_cpy into memory_k/v);
-    // this launch reads them from qkv, later launches from the cache
-    if (c == 0 && tid < HEAD_DIM) {
-        K[(int64_t)p * n_embd + tid] = kcur[tid];
-        V[(int64_t)p * n_embd + tid] = vcur[tid];
-    }
-
-    float mx = -INFINITY, l = 0.f;
-    if (j0 < j1) {
-        // scores: 4 lanes per key (16 dims each), 64 keys per pass
-        const int g = tid >> 2, sub = tid & 3;
-        float4 qv[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) qv[i] = reinterpret_cast<const float4 *>(q + sub * 16)[i];
-        float lmax = -INFINITY;
-        for (int j = j0 + g; j < j1; j += 64) {
-            const float *kr = (j == p ? kcur : K + (int64_t)j * n_embd) + sub * 16;
-            float4 kv[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) kv[i] = reinterpret_cast<const float4 *>(kr)[i];
-            float d = 0.f;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) d += qv[i].x * kv[i].x + qv[i].y * kv[i].y + qv[i].z * kv[i].z + qv[i].w * kv[i].w;
-            d += dpp_f<DPP_XOR1>(d);
-            d += dpp_f<DPP_XOR2>(d);
-            d *= scale;
-            if (sub == 0) sc[j - j0] = d;
-            lmax = fmaxf(lmax, d);
-        }
-        lmax = fmaxf(lmax, xchg<1>(lmax)); lmax = fmaxf(lmax, xchg<2>(lmax)); lmax = fmaxf(lmax, xchg<4>(lmax));
-        lmax = fmaxf(lmax, xchg<8>(lmax)); lmax = fmaxf(lmax, xchg<16>(lmax)); lmax = fmaxf(lmax, xchg<32>(lmax));
-        if (lane == 0) rmax[wave] = lmax;
-        __syncthreads();
-        mx = fmaxf(fmaxf(rmax[0], rmax[1]), fmaxf(rmax[2], rmax[3]));
-        float lsum = 0.f;
-        for (int j = j0 + tid; j < j1; j += 256) {
-            const float e = expf(sc[j - j0] - mx);
-            sc[j - j0] = e;
-            lsum += e;
-        }
-        lsum = wave_sum(lsum);
-        if (lane == 0) rsum[wave] = lsum;
-        __syncthreads();
-        l = (rsum[0] + rsum[1]) + (rsum[2] + rsum[3]);
-
-        // o = sum_j e_j V_j: lane = (key slot ks = lane >> 4, dims 4*(lane & 15) .. +3), a wave
-        // covers 4 keys per pass (coalesced 256-B rows), the workgroup 16; 2 passes in flight
-        const int ks = lane >> 4, dq = (lane & 15) * 4;
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int j = j0 + wave * 4 + ks; j < j1; j += 16) {
-            const float e = sc[j - j0];
-            const float4 v = *reinterpret_cast<const float4 *>((j == p ? vcur : V + (int64_t)j * n_embd) + dq);
-            acc.x += e * v.x; acc.y += e * v.y; acc.z += e * v.z; acc.w += e * v.w;
-        }
-        acc.x += xchg<16>(acc.x); acc.y += xchg<16>(acc.y); acc.z += xchg<16>(acc.z); acc.w += xchg<16>(acc.w);
-        acc.x += xchg<32>(acc.x); acc.y += xchg<32>(acc.y); acc.z += xchg<32>(acc.z); acc.w += xchg<32>(acc.w);
-        if (lane < 16) *reinterpret_cast<float4 *>(&red[wave][dq]) = acc;
-        __syncthreads();
-        if (tid < HEAD_DIM) pm[2 + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
-    } else if (tid < HEAD_DIM) {
-        pm[2 + tid] = 0.f;
-    }
-    if (tid == 0) {
-        pm[0] = mx;
-        pm[1] = l;
-    }
-
-    // last-arriving workgroup of (h, s) merges the nsplit partials
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) {
-        const uint32_t prev = atomicAdd(&counter[s * n_head + h], 1u);
-        is_last = prev == (uint32_t)nsplit - 1;
+    // q (pre-scaled) to LDS; the new token's K and V to the cache (the reference's ggml_cpy
+    // into memory_k / memory_v). This launch reads them from qkv, later launches from the cache.
+    if (tid < HEAD_DIM / 4) {
+        float4 v = reinterpret_cast<const float4 *>(q)[tid];
+        v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale;
+        qs[tid] = v;
+    } else if (tid >= 64 && tid < 64 + HEAD_DIM / 4) {
+        const int i = tid - 64;
+        reinterpret_cast<float4 *>(K + (int64_t)p * n_embd)[i] = reinterpret_cast<const float4 *>(kcur)[i];
+        reinterpret_cast<float4 *>(V + (int64_t)p * n_embd)[i] = reinterpret_cast<const float4 *>(vcur)[i];
     }
     __syncthreads();
-    if (!is_last) return;
-    __threadfence();
-    if (tid < HEAD_DIM) {
-        const float *pb = part + (int64_t)(s * n_head + h) * nsplit * (HEAD_DIM + 2);
-        float M = -INFINITY;
-        for (int i = 0; i < nsplit; ++i) M = fmaxf(M, __builtin_nontemporal_load(pb + i * (HEAD_DIM + 2)));
+
+    const int chunk = (nk + 7) >> 3;
+    const int j0 = wave * chunk, j1 = min(nk, j0 + chunk);
+    float m = -INFINITY, l = 0.f;
+    float o[HEAD_DIM];
+#pragma unroll
+    for (int d = 0; d < HEAD_DIM; ++d) o[d] = 0.f;
+    for (int jb = j0; jb < j1; jb += 64) {
+        const int j = jb + lane;
+        const bool live = j < j1;
+        const int jc = live ? j : j0;                     // dead lanes re-read a live row
+        const float *kr = jc == p ? kcur : K + (int64_t)jc * n_embd;
+        const float *vr = jc == p ? vcur : V + (int64_t)jc * n_embd;
+        float4 kv[HEAD_DIM / 4], vv[HEAD_DIM / 4];
+#pragma unroll
+        for (int i = 0; i < HEAD_DIM / 4; ++i) kv[i] = reinterpret_cast<const float4 *>(kr)[i];
+#pragma unroll
+        for (int i = 0; i < HEAD_DIM / 4; ++i) vv[i] = reinterpret_cast<const float4 *>(vr)[i];
+        float sc = 0.f;
+#pragma unroll
+        for (int i = 0; i < HEAD_DIM / 4; ++i) {
+            const float4 qv = qs[i];
+            sc += qv.x * kv[i].x + qv.y * kv[i].y + qv.z * kv[i].z + qv.w * kv[i].w;
+        }
+        if (live) {
+            const float mn = fmaxf(m, sc);
+            const float c = expf(m - mn);                 // 0 on the first key (m = -inf)
+            const float e = expf(sc - mn);
+            l = l * c + e;
+#pragma unroll
+            for (int i = 0; i < HEAD_DIM / 4; ++i) {
+                o[4 * i + 0] = o[4 * i + 0] * c + e * vv[i].x;
+                o[4 * i + 1] = o[4 * i + 1] * c + e * vv[i].y;
+                o[4 * i + 2] = o[4 * i + 2] * c + e * vv[i].z;
+                o[4 * i + 3] = o[4 * i + 3] * c + e * vv[i].w;
+            }
+            m = mn;
+        }
+    }
+    // wave merge: rescale every lane to the wave max, then one transpose reduction
+    float M = m;
+    M = fmaxf(M, xchg<1>(M)); M = fmaxf(M, xchg<2>(M)); M = fmaxf(M, xchg<4>(M));
+    M = fmaxf(M, xchg<8>(M)); M = fmaxf(M, xchg<16>(M)); M = fmaxf(M, xchg<32>(M));
+    const float f = l > 0.f ? expf(m - M) : 0.f;
+    l = wave_sum(l * f);
+#pragma unroll
+    for (int d = 0; d < HEAD_DIM; ++d) o[d] *= f;
+    const float od = group_reduce_transpose<HEAD_DIM, 64>(o);   // lane d: sum over the wave's keys
+    wo[wave][lane] = od;
+    if (lane == 0) { wm[wave] = M; wl[wave] = l; }
+    __syncthreads();
+    if (wave == 0) {
+        float MX = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) if (wl[w] > 0.f) MX = fmaxf(MX, wm[w]);
         float L = 0.f, O = 0.f;
-        for (int i = 0; i < nsplit; ++i) {
-            const float *pi = pb + i * (HEAD_DIM + 2);
-            const float li = __builtin_nontemporal_load(pi + 1);
-            if (li > 0.f) {
-                const float w = expf(__builtin_nontemporal_load(pi) - M);
-                L += w * li;
-                O += w * __builtin_nontemporal_load(pi + 2 + tid);
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            if (wl[w] > 0.f) {
+                const float g = expf(wm[w] - MX);
+                L += g * wl[w];
+                O += g * wo[w][lane];
             }
         }
-        out[(int64_t)s * n_embd + h * HEAD_DIM + tid] = O / L;
+        out[(int64_t)s * n_embd + h * HEAD_DIM + lane] = O / L;
     }
-    if (tid == 0) counter[s * n_head + h] = 0u;
 }
 
-__global__ __launch_bounds__(1024) void argmax_kernel(const float *__restrict__ logits, int n_vocab, int32_t *__restrict__ tokens) {
-    __shared__ float bv[16];
-    __shared__ int bi[16];
+// greedy next token from the lm_head's per-workgroup partials (EPI_ARGMAX, mmvq_impl.h):
+// ARGMAX_SLOTS (value, row) pairs per sequence, unused slots hold (-inf, INT_MAX). Lowest row
+// on ties. Also advances the sequence's position (the step's last launch).
+__global__ __launch_bounds__(256) void argmax_final_kernel(const float *__restrict__ pv, const int32_t *__restrict__ pi,
+                                                           int32_t *__restrict__ tokens, int32_t *__restrict__ pos) {
+    __shared__ float bv[4];
+    __shared__ int bi[4];
     const int s = blockIdx.x;
-    const float *l = logits + (int64_t)s * n_vocab;
     float v = -INFINITY;
     int idx = 0x7fffffff;
-    for (int i = threadIdx.x; i < n_vocab; i += blockDim.x) {
-        const float x = l[i];
-        if (x > v) { v = x; idx = i; }   // strided scan: a later i only wins when strictly greater
+    for (int k = threadIdx.x; k < ARGMAX_SLOTS; k += 256) {
+        const float x = pv[(int64_t)s * ARGMAX_SLOTS + k];
+        const int i = pi[(int64_t)s * ARGMAX_SLOTS + k];
+        if (x > v || (x == v && i < idx)) { v = x; idx = i; }
     }
     for (int d = 1; d < 64; d <<= 1) {
         const float ov = __shfl_xor(v, d);
@@ -190,10 +176,17 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const float *__restrict__ 
     if ((threadIdx.x & 63) == 0) { bv[wave] = v; bi[wave] = idx; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+        for (int w = 1; w < 4; ++w)
             if (bv[w] > v || (bv[w] == v && bi[w] < idx)) { v = bv[w]; idx = bi[w]; }
         tokens[s] = idx == 0x7fffffff ? 0 : idx;
+        pos[s] += 1;
     }
+}
+
+// reset the partial slots to (-inf, INT_MAX) (once per context)
+__global__ void argmax_reset_kernel(float *pv, int32_t *pi, int64_t n) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) { pv[k] = -INFINITY; pi[k] = 0x7fffffff; }
 }
 
 __global__ void advance_kernel(int32_t *pos, int n_seq) {
@@ -218,21 +211,21 @@ hipError_t gpt2_embed_launch(int wtype, const void *wte, int64_t wte_nb1, const 
     return hipGetLastError();
 }
 
-// keys per split: at most 64 (the score pass width); n_ctx = 1024 -> 16 splits
-int gpt2_attn_nsplit(int n_ctx) { return std::min(64, std::max(1, (n_ctx + 63) / 64)); }
-
-hipError_t gpt2_attn_launch(const float *qkv, float *kc, float *vc, const int32_t *pos, float *out, float *part, uint32_t *counter,
-                            int n_seq, int n_head, int n_embd, int n_ctx, float scale, hipStream_t st) {
+hipError_t gpt2_attn_launch(const float *qkv, float *kc, float *vc, const int32_t *pos, float *out, int n_seq, int n_head,
+                            int n_embd, int n_ctx, float scale, hipStream_t st) {
     if (n_embd != n_head * HEAD_DIM) return hipErrorInvalidValue;
-    const int nsplit = gpt2_attn_nsplit(n_ctx);
-    const int chunk_max = (n_ctx + nsplit - 1) / nsplit;
-    hipLaunchKernelGGL(attn_decode_kernel, dim3(n_head, n_seq, nsplit), dim3(256), (size_t)chunk_max * sizeof(float), st, qkv, kc, vc,
-                       pos, out, part, counter, n_embd, n_ctx, scale);
+    hipLaunchKernelGGL(attn_decode_kernel, dim3(n_head, n_seq), dim3(512), 0, st, qkv, kc, vc, pos, out, n_embd, n_ctx, scale);
     return hipGetLastError();
 }
 
-hipError_t gpt2_argmax_launch(const float *logits, int n_seq, int n_vocab, int32_t *tokens, hipStream_t st) {
-    hipLaunchKernelGGL(argmax_kernel, dim3(n_seq), dim3(1024), 0, st, logits, n_vocab, tokens);
+hipError_t gpt2_argmax_launch(const float *pv, const int32_t *pi, int n_seq, int32_t *tokens, int32_t *pos, hipStream_t st) {
+    hipLaunchKernelGGL(argmax_final_kernel, dim3(n_seq), dim3(256), 0, st, pv, pi, tokens, pos);
+    return hipGetLastError();
+}
+
+hipError_t gpt2_argmax_reset(float *pv, int32_t *pi, int n_seq, hipStream_t st) {
+    const int64_t n = (int64_t)n_seq * ARGMAX_SLOTS;
+    hipLaunchKernelGGL(argmax_reset_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, pv, pi, n);
     return hipGetLastError();
 }
 

@@ -12,20 +12,30 @@ size_t mmvq_lds_bytes(int K, int nc) {
     return (size_t)nc * Kpad + sizeof(float) * (size_t)nc * (Kpad / 32) * 4;   // xq + xd + xs + x16
 }
 
-int mmvq_rows_per_wg(int rpw) { return MMVQ_WAVES * rpw; }
+// lanes per weight row: the width (16 or 64) that leaves the fewest idle slot lanes for this K;
+// ties go to 64 (fewer K iterations per row)
+int mmvq_pick_lpr(int K) {
+    const int nslots = (K + 63) / 64;
+    const int u16 = 16 * ((nslots + 15) / 16), u64 = 64 * ((nslots + 63) / 64);
+    return u16 < u64 ? 16 : 64;
+}
+
+int mmvq_rows_per_group(int lpr, int rpw) { return MMVQ_WAVES * (WAVE / lpr) * rpw; }
 
 constexpr int64_t MMVQ_TARGET_WGS = 2048;   // two rounds of 4 resident 8-wave workgroups per CU (scripts/mmvq_sweep.sh)
 
-template <int T, int NC, int RPW, bool IDS, bool RAG, bool XA, bool BIGK>
-static hipError_t launch_one(const MmArgs &a, int grid_y, int grid_z, hipStream_t st) {
-    const size_t lds = mmvq_lds_bytes(a.K, NC);
-    auto kern = mmvq_kernel<T, NC, RPW, IDS, RAG, XA, BIGK>;
+template <int T, int NC, int LPR, int RPW, bool IDS, bool RAG, bool XA, bool BIGK>
+static hipError_t launch_one(const MmArgs &a0, int grid_y, int grid_z, hipStream_t st) {
+    const size_t lds = mmvq_lds_bytes(a0.K, NC);
+    auto kern = mmvq_kernel<T, NC, LPR, RPW, IDS, RAG, XA, BIGK>;
+    MmArgs a = a0;
+    a.n_it = ((a.K + 63) / 64 + LPR - 1) / LPR;
     static bool attr_set = false;   // per-instantiation
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    const int rows_per_group = MMVQ_WAVES * RPW;
+    const int rows_per_group = MMVQ_WAVES * (WAVE / LPR) * RPW;
     const int n_groups = (a.N + rows_per_group - 1) / rows_per_group;
     // enough workgroups to fill 256 CUs ~4 deep; beyond that each workgroup walks more groups
     const int64_t others = (int64_t)grid_y * grid_z;
@@ -41,45 +51,47 @@ static hipError_t launch_one(const MmArgs &a, int grid_y, int grid_z, hipStream_
 // K > 8192 (activations need more than two preloaded quantization rounds)
 static bool is_bigk(const MmArgs &a) { return ((a.K + 63) & ~63) / 32 > 2 * XR_STRIDE; }
 
-template <int T, int NC, int RPW, bool IDS>
+template <int T, int NC, int LPR, int RPW, bool IDS>
 static hipError_t launch_flags(const MmArgs &a, int grid_y, int grid_z, hipStream_t st) {
     const bool rag = (a.K % 64) != 0;
     if (is_bigk(a)) {
-        if constexpr (NC == 1) {
+        if constexpr (NC == 1 && LPR == 64) {
             if constexpr (T == T_Q4_0 || T == T_Q8_0) {
-                if (rag) return launch_one<T, 1, RPW, IDS, true, false, true>(a, grid_y, grid_z, st);
+                if (rag) return launch_one<T, 1, 64, RPW, IDS, true, false, true>(a, grid_y, grid_z, st);
             }
-            return a.x_aligned16 ? launch_one<T, 1, RPW, IDS, false, true, true>(a, grid_y, grid_z, st)
-                                 : launch_one<T, 1, RPW, IDS, false, false, true>(a, grid_y, grid_z, st);
+            return a.x_aligned16 ? launch_one<T, 1, 64, RPW, IDS, false, true, true>(a, grid_y, grid_z, st)
+                                 : launch_one<T, 1, 64, RPW, IDS, false, false, true>(a, grid_y, grid_z, st);
         }
-        return hipErrorInvalidValue;   // host splits big-K launches into single columns
+        return hipErrorInvalidValue;   // host splits big-K launches into single columns of 64-lane rows
     }
     if constexpr (T == T_Q4_0 || T == T_Q8_0) {
         if (rag) {
-            return a.x_aligned16 ? launch_one<T, NC, RPW, IDS, true, true, false>(a, grid_y, grid_z, st)
-                                 : launch_one<T, NC, RPW, IDS, true, false, false>(a, grid_y, grid_z, st);
+            return a.x_aligned16 ? launch_one<T, NC, LPR, RPW, IDS, true, true, false>(a, grid_y, grid_z, st)
+                                 : launch_one<T, NC, LPR, RPW, IDS, true, false, false>(a, grid_y, grid_z, st);
         }
     }
-    return a.x_aligned16 ? launch_one<T, NC, RPW, IDS, false, true, false>(a, grid_y, grid_z, st)
-                         : launch_one<T, NC, RPW, IDS, false, false, false>(a, grid_y, grid_z, st);
+    return a.x_aligned16 ? launch_one<T, NC, LPR, RPW, IDS, false, true, false>(a, grid_y, grid_z, st)
+                         : launch_one<T, NC, LPR, RPW, IDS, false, false, false>(a, grid_y, grid_z, st);
 }
 
-template <int T, int RPW>
+template <int T, int LPR, int RPW>
 static hipError_t launch_nc(const MmArgs &a, int nc, int grid_y, int grid_z, hipStream_t st) {
     switch (nc) {
-        case 1: return launch_flags<T, 1, RPW, false>(a, grid_y, grid_z, st);
-        case 2: return launch_flags<T, 2, RPW, false>(a, grid_y, grid_z, st);
-        case 3: return launch_flags<T, 3, RPW, false>(a, grid_y, grid_z, st);
-        case 4: return launch_flags<T, 4, RPW, false>(a, grid_y, grid_z, st);
-        case 8: return launch_flags<T, 8, RPW, false>(a, grid_y, grid_z, st);
+        case 1: return launch_flags<T, 1, LPR, RPW, false>(a, grid_y, grid_z, st);
+        case 2: return launch_flags<T, 2, LPR, RPW, false>(a, grid_y, grid_z, st);
+        case 3: return launch_flags<T, 3, LPR, RPW, false>(a, grid_y, grid_z, st);
+        case 4: return launch_flags<T, 4, LPR, RPW, false>(a, grid_y, grid_z, st);
+        case 8: return launch_flags<T, 8, LPR, RPW, false>(a, grid_y, grid_z, st);
         default: return hipErrorInvalidValue;
     }
 }
 
+// 16-lane rows only with one row per lane group (the small-K decode shapes)
 template <int T>
 static hipError_t launch_type(const MmArgs &a, int nc, int grid_y, int grid_z, int rpw, hipStream_t st) {
-    if (rpw <= 1) return launch_nc<T, 1>(a, nc, grid_y, grid_z, st);
-    return launch_nc<T, 2>(a, nc, grid_y, grid_z, st);
+    if (mmvq_pick_lpr(a.K) == 16 && !is_bigk(a)) return launch_nc<T, 16, 1>(a, nc, grid_y, grid_z, st);
+    if (rpw <= 1) return launch_nc<T, 64, 1>(a, nc, grid_y, grid_z, st);
+    return launch_nc<T, 64, 2>(a, nc, grid_y, grid_z, st);
 }
 
 // column-group widths that have kernels (dispatch.cpp splits M into these)
@@ -104,12 +116,13 @@ hipError_t mmvq_launch(int type, const MmArgs &a, int nc, int rpw, hipStream_t s
 hipError_t mmvq_id_launch(int type, const MmArgs &a, int rpw, hipStream_t st) {
     const int grid_y = a.n_used * a.n_tok;
     (void)rpw;
+    const bool l16 = mmvq_pick_lpr(a.K) == 16 && !is_bigk(a);
     switch (type) {
-        case T_Q4_0: return launch_flags<T_Q4_0, 1, 1, true>(a, grid_y, 1, st);
-        case T_Q8_0: return launch_flags<T_Q8_0, 1, 1, true>(a, grid_y, 1, st);
-        case T_Q4_K: return launch_flags<T_Q4_K, 1, 1, true>(a, grid_y, 1, st);
-        case T_Q5_K: return launch_flags<T_Q5_K, 1, 1, true>(a, grid_y, 1, st);
-        case T_Q6_K: return launch_flags<T_Q6_K, 1, 1, true>(a, grid_y, 1, st);
+        case T_Q4_0: return l16 ? launch_flags<T_Q4_0, 1, 16, 1, true>(a, grid_y, 1, st) : launch_flags<T_Q4_0, 1, 64, 1, true>(a, grid_y, 1, st);
+        case T_Q8_0: return l16 ? launch_flags<T_Q8_0, 1, 16, 1, true>(a, grid_y, 1, st) : launch_flags<T_Q8_0, 1, 64, 1, true>(a, grid_y, 1, st);
+        case T_Q4_K: return l16 ? launch_flags<T_Q4_K, 1, 16, 1, true>(a, grid_y, 1, st) : launch_flags<T_Q4_K, 1, 64, 1, true>(a, grid_y, 1, st);
+        case T_Q5_K: return l16 ? launch_flags<T_Q5_K, 1, 16, 1, true>(a, grid_y, 1, st) : launch_flags<T_Q5_K, 1, 64, 1, true>(a, grid_y, 1, st);
+        case T_Q6_K: return l16 ? launch_flags<T_Q6_K, 1, 16, 1, true>(a, grid_y, 1, st) : launch_flags<T_Q6_K, 1, 64, 1, true>(a, grid_y, 1, st);
         default: return hipErrorInvalidValue;
     }
 }

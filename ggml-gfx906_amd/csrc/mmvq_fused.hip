@@ -12,64 +12,74 @@
 namespace mi355x {
 
 size_t mmvq_lds_bytes(int K, int nc);
+int mmvq_pick_lpr(int K);
 
 namespace {
 
 // prepare_only: just raise the instantiation's dynamic-LDS limit. That is not a stream
 // operation and fails inside a hipGraph capture, so mmvq_fused_prepare() runs it for every
 // instantiation before the engine captures a decode step.
-template <int T, int NC, int RPW>
-hipError_t fused_one(const MmArgs &a, int grid_z, hipStream_t st, bool prepare_only = false) {
-    auto kern = mmvq_kernel<T, NC, RPW, false, false, true, false, true>;
+template <int T, int NC, int LPR, int RPW>
+hipError_t fused_one(const MmArgs &a0, int grid_z, hipStream_t st, bool prepare_only = false) {
+    auto kern = mmvq_kernel<T, NC, LPR, RPW, false, false, true, false, true>;
     static bool attr_set = false;   // per-instantiation
     if (!attr_set) {
-        // 160 KB of LDS per CU minus the prologue's static reduction array
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);
+        // 160 KB of LDS per CU minus the static arrays (layer-norm and argmax reductions)
+        hipFuncAttributes fa{};
+        hipError_t e = hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kern));
+        if (e != hipSuccess) return e;
+        e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(160 * 1024 - fa.sharedSizeBytes));
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     if (prepare_only) return hipSuccess;
-    const int rows_per_group = MMVQ_WAVES * RPW;
+    MmArgs a = a0;
+    a.n_it = ((a.K + 63) / 64 + LPR - 1) / LPR;
+    const int rows_per_group = MMVQ_WAVES * (WAVE / LPR) * RPW;
     const int n_groups = (a.N + rows_per_group - 1) / rows_per_group;
-    const int want = std::max(1, 2048 / grid_z);
+    const int want = std::max(1, std::min(ARGMAX_SLOTS, 2048 / grid_z));   // EPI_ARGMAX: one partial slot per workgroup
     dim3 grid(std::min(n_groups, want), 1, grid_z);
     hipLaunchKernelGGL(kern, grid, dim3(MMVQ_THREADS), mmvq_lds_bytes(a.K, NC), st, a);
     return hipGetLastError();
 }
 
-template <int T, int RPW>
+template <int T, int LPR, int RPW>
 hipError_t fused_nc(const MmArgs &a, int nc, int grid_z, hipStream_t st) {
     switch (nc) {
-        case 1: return fused_one<T, 1, RPW>(a, grid_z, st);
-        case 2: return fused_one<T, 2, RPW>(a, grid_z, st);
-        case 3: return fused_one<T, 3, RPW>(a, grid_z, st);
-        case 4: return fused_one<T, 4, RPW>(a, grid_z, st);
-        case 8: return fused_one<T, 8, RPW>(a, grid_z, st);
+        case 1: return fused_one<T, 1, LPR, RPW>(a, grid_z, st);
+        case 2: return fused_one<T, 2, LPR, RPW>(a, grid_z, st);
+        case 3: return fused_one<T, 3, LPR, RPW>(a, grid_z, st);
+        case 4: return fused_one<T, 4, LPR, RPW>(a, grid_z, st);
+        case 8: return fused_one<T, 8, LPR, RPW>(a, grid_z, st);
         default: return hipErrorInvalidValue;
     }
 }
 
 template <int T>
 hipError_t fused_type(const MmArgs &a, int nc, int rpw, int grid_z, hipStream_t st) {
-    return rpw <= 1 ? fused_nc<T, 1>(a, nc, grid_z, st) : fused_nc<T, 2>(a, nc, grid_z, st);
+    if (mmvq_pick_lpr(a.K) == 16) return fused_nc<T, 16, 1>(a, nc, grid_z, st);
+    return rpw <= 1 ? fused_nc<T, 64, 1>(a, nc, grid_z, st) : fused_nc<T, 64, 2>(a, nc, grid_z, st);
 }
 
-template <int T, int RPW>
+template <int T, int LPR, int RPW>
 hipError_t prepare_nc() {
     MmArgs a{};
     hipError_t e = hipSuccess;
-    if (e == hipSuccess) e = fused_one<T, 1, RPW>(a, 1, nullptr, true);
-    if (e == hipSuccess) e = fused_one<T, 2, RPW>(a, 1, nullptr, true);
-    if (e == hipSuccess) e = fused_one<T, 3, RPW>(a, 1, nullptr, true);
-    if (e == hipSuccess) e = fused_one<T, 4, RPW>(a, 1, nullptr, true);
-    if (e == hipSuccess) e = fused_one<T, 8, RPW>(a, 1, nullptr, true);
+    if (e == hipSuccess) e = fused_one<T, 1, LPR, RPW>(a, 1, nullptr, true);
+    if (e == hipSuccess) e = fused_one<T, 2, LPR, RPW>(a, 1, nullptr, true);
+    if (e == hipSuccess) e = fused_one<T, 3, LPR, RPW>(a, 1, nullptr, true);
+    if (e == hipSuccess) e = fused_one<T, 4, LPR, RPW>(a, 1, nullptr, true);
+    if (e == hipSuccess) e = fused_one<T, 8, LPR, RPW>(a, 1, nullptr, true);
     return e;
 }
 
 template <int T>
 hipError_t prepare_type() {
-    const hipError_t e = prepare_nc<T, 1>();
-    return e != hipSuccess ? e : prepare_nc<T, 2>();
+    hipError_t e = prepare_nc<T, 64, 1>();
+    if (e == hipSuccess) e = prepare_nc<T, 64, 2>();
+    if (e == hipSuccess) e = prepare_nc<T, 16, 1>();
+    return e;
 }
 
 }  // namespace

@@ -350,17 +350,17 @@ template <int T> struct XdCount { static constexpr int n = 2; };
 template <> struct XdCount<T_Q6_K> { static constexpr int n = 4; };
 
 // ------------------------------------------------------------------------------------------
-// butterfly-transpose wave reduction: V (power of two, <= 64) partial sums per lane.
-// On return lane L holds the full sum of value index (L >> (6 - log2 V)).
+// butterfly-transpose reduction over groups of LPR lanes (LPR = 16 / 32 / 64, lane bits
+// 0 .. log2(LPR)-1): V (power of two, <= LPR) partial sums per lane. Distances run from LPR/2
+// down to 1, so the exchanges never leave the group. On return lane L holds the group's full
+// sum of value index ((L % LPR) >> (log2(LPR) - log2(V))).
 // ------------------------------------------------------------------------------------------
 template <int x> struct Log2 { static constexpr int v = 1 + Log2<x / 2>::v; };
 template <> struct Log2<1> { static constexpr int v = 0; };
 constexpr int pow2ceil(int x) { return x <= 1 ? 1 : 2 * pow2ceil((x + 1) / 2); }
 
-template <int V, int STEP>
+template <int V, int DIST, int HALF>
 __device__ __forceinline__ void butterfly_step(float (&v)[V], int lane) {
-    constexpr int HALF = V >> (STEP + 1);
-    constexpr int DIST = 32 >> STEP;
     const bool upper = (lane & DIST) != 0;
 #pragma unroll
     for (int i = 0; i < HALF; ++i) {
@@ -370,24 +370,28 @@ __device__ __forceinline__ void butterfly_step(float (&v)[V], int lane) {
     }
 }
 
-template <int V>
-__device__ inline float wave_reduce_transpose(float (&v)[V]) {
-    constexpr int LV = Log2<V>::v;
+template <int V, int LPR, int DIST>
+__device__ __forceinline__ float reduce_rest(float (&v)[V], int lane, float r) {
+    if constexpr (DIST == 0) {
+        return r;
+    } else {
+        // the transposing steps consume log2(V) distances from the top; the rest plain-sum
+        constexpr int STEP = Log2<LPR>::v - 1 - Log2<DIST>::v;   // 0 for DIST = LPR/2
+        if constexpr (STEP < Log2<V>::v) {
+            butterfly_step<V, DIST, (V >> (STEP + 1))>(v, lane);
+            return reduce_rest<V, LPR, DIST / 2>(v, lane, v[0]);
+        } else {
+            r += xchg<DIST>(r);
+            return reduce_rest<V, LPR, DIST / 2>(v, lane, r);
+        }
+    }
+}
+
+template <int V, int LPR>
+__device__ inline float group_reduce_transpose(float (&v)[V]) {
+    static_assert(V <= LPR, "more partial sums than lanes in the group");
     const int lane = threadIdx.x & 63;
-    if constexpr (LV > 0) butterfly_step<V, 0>(v, lane);
-    if constexpr (LV > 1) butterfly_step<V, 1>(v, lane);
-    if constexpr (LV > 2) butterfly_step<V, 2>(v, lane);
-    if constexpr (LV > 3) butterfly_step<V, 3>(v, lane);
-    if constexpr (LV > 4) butterfly_step<V, 4>(v, lane);
-    if constexpr (LV > 5) butterfly_step<V, 5>(v, lane);
-    float r = v[0];
-    if constexpr (LV <= 0) r += xchg<32>(r);
-    if constexpr (LV <= 1) r += xchg<16>(r);
-    if constexpr (LV <= 2) r += xchg<8>(r);
-    if constexpr (LV <= 3) r += xchg<4>(r);
-    if constexpr (LV <= 4) r += xchg<2>(r);
-    if constexpr (LV <= 5) r += xchg<1>(r);
-    return r;
+    return reduce_rest<V, LPR, LPR / 2>(v, lane, v[0]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -456,28 +460,77 @@ __device__ __forceinline__ void layer_norm_cols(const MmArgs &a, int kb0, float4
 }
 
 // ------------------------------------------------------------------------------------------
+// fused argmax epilogue (FUSE kernels, a.epi & EPI_ARGMAX): every thread offers the best
+// (value, row) it stored for its column (col < 0: stored nothing); wave 0 reduces them per
+// column and writes the workgroup's partial. Ties go to the lowest row (greedy sampling of
+// the reference's examples take the first maximum).
+// ------------------------------------------------------------------------------------------
+template <int NC>
+__device__ __forceinline__ void argmax_epilogue(const MmArgs &a, float bv, int bi, int col) {
+    __shared__ float sv[MMVQ_THREADS];
+    __shared__ int si[MMVQ_THREADS], sc[MMVQ_THREADS];
+    sv[threadIdx.x] = bv;
+    si[threadIdx.x] = bi;
+    sc[threadIdx.x] = col;
+    __syncthreads();
+    if (threadIdx.x >= WAVE) return;
+    const int lane = threadIdx.x;
+#pragma unroll
+    for (int m = 0; m < NC; ++m) {
+        float v = -INFINITY;
+        int i = 0x7fffffff;
+#pragma unroll
+        for (int k = 0; k < MMVQ_WAVES; ++k) {
+            const int t = lane + k * WAVE;
+            const float tv = sv[t];
+            const int ti = si[t];
+            if (sc[t] == m && (tv > v || (tv == v && ti < i))) { v = tv; i = ti; }
+        }
+#pragma unroll
+        for (int d = 1; d < WAVE; d <<= 1) {
+            const float ov = __shfl_xor(v, d);
+            const int oi = __shfl_xor(i, d);
+            if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+        }
+        if (lane == 0) {
+            const int c = blockIdx.z * NC + m;
+            a.amax_v[c * ARGMAX_SLOTS + blockIdx.x] = v;
+            a.amax_i[c * ARGMAX_SLOTS + blockIdx.x] = i;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // the kernel
+//   LPR : lanes per weight row (16 or 64). A wave covers 64/LPR rows side by side; a lane walks
+//         K slots s = lane % LPR + it * LPR, it < n_it = ceil(nslots / LPR). Small K (GPT-2's
+//         768: 12 slots) uses 16-lane rows so 75% of the lanes carry weights instead of 19%.
 //   RAG : K % 64 == 32 (only possible for the 32-block types): last slot holds one block
 //   XA  : src1 rows and strides are 16-byte aligned (float4 activation loads)
 //
 // Work: blockIdx.y selects the matrix / column group (batch entry, or (expert, token) for
 // MUL_MAT_ID); the workgroup quantizes that column group into LDS ONCE, then walks row groups
-// g = blockIdx.x, blockIdx.x + gridDim.x, ... (8 waves x RPW rows each). Each unit of work
-// = (row group, 64-slot iteration of K); the weights of unit u+1 are in flight while unit u
-// is computed (two register buffers), so a workgroup keeps HBM busy across its whole life and
-// the activation quantization is amortized over every row it covers.
+// g = blockIdx.x, blockIdx.x + gridDim.x, ... (8 waves x 64/LPR x RPW rows each). Each unit of
+// work = (row group, K iteration); the weights of unit u+1 are in flight while unit u is
+// computed (two register buffers). The unit walk is incremental (no integer division in the
+// kernel: n_it comes from the host), and a workgroup with a single unit — the single-matrix
+// decode shapes — takes a straight-line path with no prefetch.
 // ------------------------------------------------------------------------------------------
-template <int T, int NC, int RPW, bool IDS, bool RAG, bool XA, bool BIGK, bool FUSE = false>
+template <int T, int NC, int LPR, int RPW, bool IDS, bool RAG, bool XA, bool BIGK, bool FUSE = false>
 __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr int NX = XdCount<T>::n;
     constexpr int V = pow2ceil(RPW * NC);
-    constexpr int ROWS_PER_GROUP = MMVQ_WAVES * RPW;
+    constexpr int GPW = WAVE / LPR;                       // row groups side by side in a wave
+    constexpr int ROWS_PER_WAVE = GPW * RPW;
+    constexpr int ROWS_PER_GROUP = MMVQ_WAVES * ROWS_PER_WAVE;
+    static_assert(V <= LPR, "RPW * NC partial sums must fit the lanes of a row");
 
     const int Kpad = (a.K + 63) & ~63;
     const int nslots = Kpad / 64;
     const int nblk = a.K / QT<T>::blck;           // quant blocks per row
     const int nxblk = Kpad / 32;
+    const int n_it = a.n_it;                      // host: ceil(nslots / LPR)
     const XSmem sm = xsmem(smem, Kpad, NC);
 
     // ---- which matrix / columns this workgroup serves
@@ -501,20 +554,17 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
 
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
+    const int sl = lane % LPR;                    // slot lane inside the row group
+    const int wrow = wave * ROWS_PER_WAVE + (lane / LPR) * RPW;   // this lane's first row in a group
     const int n_groups = (a.N + ROWS_PER_GROUP - 1) / ROWS_PER_GROUP;
-    const int n_it = (nslots + WAVE - 1) / WAVE;
-    const int my_groups = (n_groups - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-    const int n_units = my_groups * n_it;
     const bool stamp = a.stamps != nullptr && threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
     if (stamp) { a.stamps[blockIdx.x * 8 + 0] = __builtin_amdgcn_s_memrealtime(); a.stamps[blockIdx.x * 8 + 4] = __builtin_amdgcn_s_memtime(); }
 
-    // unit u -> first row of this wave and K slot of this lane (slot clamped: straight-line
-    // loads; dead lanes / rows read valid memory and are masked out of the sums)
-    auto unit_row0 = [&](int u) { return ((int)blockIdx.x + (u / n_it) * (int)gridDim.x) * ROWS_PER_GROUP + wave * RPW; };
-    auto unit_slot = [&](int u) { return lane + (u % n_it) * WAVE; };
-    auto load_unit = [&](Frag<T> (&f)[RPW], int u) {
-        const int r0 = unit_row0(u);
-        const int s = min(unit_slot(u), nslots - 1);
+    // unit (g, it): rows g * ROWS_PER_GROUP + wrow + r, slot sl + it * LPR (clamped: dead
+    // lanes / rows read valid memory and are masked out of the sums)
+    auto load_unit = [&](Frag<T> (&f)[RPW], int g, int it) {
+        const int r0 = g * ROWS_PER_GROUP + wrow;
+        const int s = min(sl + it * LPR, nslots - 1);
 #pragma unroll
         for (int r = 0; r < RPW; ++r) f[r].template load<RAG>(wmat + (int64_t)min(r0 + r, a.N - 1) * a.nb01, s, nblk);
     };
@@ -525,14 +575,20 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
     // up to two rounds (K <= 8192) are preloaded; BIGK kernels loop over the rest
     const int kb0 = threadIdx.x >> 2;
     constexpr int PRE = BIGK ? 1 : 2;
+    const bool round2 = !BIGK && nxblk > XR_STRIDE;   // uniform: skip the second round for K <= 4096
     float4 xa[NC][PRE], xb[NC][PRE];
 #pragma unroll
-    for (int m = 0; m < NC; ++m)
-#pragma unroll
-        for (int r = 0; r < PRE; ++r) xblock_load<XA>(a, xcol0 + (int64_t)m * a.nb11, kb0 + r * XR_STRIDE, xa[m][r], xb[m][r]);
+    for (int m = 0; m < NC; ++m) {
+        xblock_load<XA>(a, xcol0 + (int64_t)m * a.nb11, kb0, xa[m][0], xb[m][0]);
+        if constexpr (PRE > 1) {
+            if (round2) xblock_load<XA>(a, xcol0 + (int64_t)m * a.nb11, kb0 + XR_STRIDE, xa[m][1], xb[m][1]);
+            else xa[m][1] = xb[m][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
 
     Frag<T> fa[RPW], fb[RPW];
-    load_unit(fa, 0);
+    int g = blockIdx.x, it = 0;                   // the unit being computed (grid.x <= n_groups)
+    load_unit(fa, g, it);
     __builtin_amdgcn_sched_barrier(0);
 
     // fused prologue: layer norm of each column over its K values (ggml_norm, reference
@@ -569,9 +625,11 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
     float acc[V];
 #pragma unroll
     for (int i = 0; i < V; ++i) acc[i] = 0.f;
+    float best_v = -INFINITY;                     // EPI_ARGMAX: this lane's best stored value
+    int best_i = 0x7fffffff, best_c = -1;
 
-    auto compute_unit = [&](const Frag<T> (&f)[RPW], int u) {
-        const int s_raw = unit_slot(u);
+    auto compute_unit = [&](const Frag<T> (&f)[RPW], int gg, int itt) {
+        const int s_raw = sl + itt * LPR;
         const int s = min(s_raw, nslots - 1);
         const float live = s_raw < nslots ? 1.f : 0.f;
         int xb0, x16b;
@@ -604,13 +662,13 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
 #pragma unroll
             for (int r = 0; r < RPW; ++r) acc[r * NC + m] += live * f[r].dot(X, dx, sx);
         }
-        // last K iteration of this row group: reduce across the wave and store
-        if (u % n_it == n_it - 1) {
-            const float sum = wave_reduce_transpose<V>(acc);
-            constexpr int SHIFT = 6 - Log2<V>::v;
-            const int idx = lane >> SHIFT;
-            const int r0 = unit_row0(u);
-            if ((lane & ((1 << SHIFT) - 1)) == 0 && idx < RPW * NC) {
+        // last K iteration of this row group: reduce across the row's lanes and store
+        if (itt == n_it - 1) {
+            const float sum = group_reduce_transpose<V, LPR>(acc);
+            constexpr int SHIFT = Log2<LPR>::v - Log2<V>::v;
+            const int idx = sl >> SHIFT;
+            const int r0 = gg * ROWS_PER_GROUP + wrow;
+            if ((sl & ((1 << SHIFT) - 1)) == 0 && idx < RPW * NC) {
                 const int r = idx / NC, m = idx % NC;
                 if (r0 + r < a.N) {
                     float *out = reinterpret_cast<float *>(dcol0 + (int64_t)m * a.nb1) + r0 + r;
@@ -620,6 +678,10 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
                         if (a.bias != nullptr) v += a.bias[r0 + r];
                         if (a.epi & EPI_GELU) v = gelu_ggml(v);
                         if (a.epi & EPI_RESID) v += *out;
+                        if (a.epi & EPI_ARGMAX) {
+                            if (v > best_v || best_c < 0) { best_v = v; best_i = r0 + r; }   // rows ascend per lane
+                            best_c = m;
+                        }
                     }
                     *out = v;
                 }
@@ -629,18 +691,37 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
         }
     };
 
-    // prefetches are unconditional (clamped to the last unit: a repeat of addresses already
-    // in flight, served on-chip) so the load stream never sits under a branch
-    // sched_barrier pins each prefetch ahead of the compute that follows it (left alone, the
-    // scheduler sinks the loads below the compute to save registers and the overlap is lost)
-    for (int u = 0; u < n_units; u += 2) {
-        load_unit(fb, min(u + 1, n_units - 1));
-        __builtin_amdgcn_sched_barrier(0);
-        compute_unit(fa, u);
-        if (u + 1 >= n_units) break;
-        load_unit(fa, min(u + 2, n_units - 1));
-        __builtin_amdgcn_sched_barrier(0);
-        compute_unit(fb, u + 1);
+    // next unit after (g, it); uniform scalar arithmetic
+    int ng = g, nit = it + 1;
+    if (nit == n_it) { nit = 0; ng += gridDim.x; }
+    if (ng >= n_groups) {
+        // single unit per workgroup (e.g. a 4096-row matrix at K <= 4096): no prefetch at all
+        compute_unit(fa, g, it);
+    } else {
+        // prefetches are unconditional (clamped to the current unit once the walk ends: a
+        // repeat of addresses already in flight, served on-chip) so the load stream never sits
+        // under a branch; sched_barrier pins each prefetch ahead of the compute that follows it
+        // (left alone, the scheduler sinks the loads below the compute to save registers and
+        // the overlap is lost)
+        for (;;) {
+            bool more = ng < n_groups;
+            load_unit(fb, more ? ng : g, more ? nit : it);
+            __builtin_amdgcn_sched_barrier(0);
+            compute_unit(fa, g, it);
+            if (!more) break;
+            g = ng; it = nit;
+            if (++nit == n_it) { nit = 0; ng += gridDim.x; }
+            more = ng < n_groups;
+            load_unit(fa, more ? ng : g, more ? nit : it);
+            __builtin_amdgcn_sched_barrier(0);
+            compute_unit(fb, g, it);
+            if (!more) break;
+            g = ng; it = nit;
+            if (++nit == n_it) { nit = 0; ng += gridDim.x; }
+        }
+    }
+    if constexpr (FUSE) {
+        if (a.epi & EPI_ARGMAX) argmax_epilogue<NC>(a, best_v, best_i, best_c);
     }
     if (stamp) { a.stamps[blockIdx.x * 8 + 2] = a.stamps[blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime(); a.stamps[blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memtime(); }
 }

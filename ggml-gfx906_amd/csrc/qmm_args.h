@@ -9,7 +9,10 @@
 
 namespace mi355x {
 
-enum { EPI_GELU = 1, EPI_RESID = 2 };
+enum { EPI_GELU = 1, EPI_RESID = 2, EPI_ARGMAX = 4 };
+
+// EPI_ARGMAX: per-workgroup partial argmax slots per output column (GPT-2 greedy sampling)
+constexpr int ARGMAX_SLOTS = 2048;
 
 struct MmArgs {
     const uint8_t *w;      // src0, quantized rows (nb00 == block bytes)
@@ -31,6 +34,7 @@ struct MmArgs {
     int ne11_b;            // b->ne[1]
     int n_expert;          // as->ne[2]
     int x_aligned16;       // src1 rows / strides are 16-byte aligned
+    int n_it;              // mat-vec: K iterations per row = ceil(ceil(K/64) / lanes per row)
     // fused decode-layer variant (gpt2.cpp; plain MUL_MAT leaves all of these zero):
     //   prologue, ln_g != nullptr: each src1 column is layer-normalized before quantization,
     //     x <- (x - mean) / sqrt(var + ln_eps) * ln_g + ln_b  (ggml_norm + mul + add)
@@ -39,6 +43,10 @@ struct MmArgs {
     float ln_eps;
     const float *bias;
     int epi;
+    //   epi & EPI_ARGMAX: every workgroup also writes the (max, lowest row) of the rows it
+    //     produced, per column c, to amax_v / amax_i [c * ARGMAX_SLOTS + blockIdx.x]
+    float *amax_v;
+    int32_t *amax_i;
     int fused;
     // diagnostics (GGML_MI355X_STAMPS): per-workgroup s_memrealtime stamps, or nullptr
     unsigned long long *stamps;

@@ -35,6 +35,9 @@ for step in "$@"; do
         prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --no-extra --cpu-seconds 1 ;;
         pmc)   run pmc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/pmc -o pmc -- python bench.py --no-extra --cpu-seconds 1 --steps 5 --warmup 1 ;;
         pmcw)  run pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/pmcw -o pmcw -- python bench.py --no-extra --cpu-seconds 1 --steps 5 --warmup 1 ;;
+        profsingles) run profsingles 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsingles -o run -- python scripts/prof_singles.py ;;
+        profgpt2) run profgpt2 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profgpt2 -o run -- python scripts/gpt2_bench.py 1 256 1 ;;
+        gpt2b) run gpt2b 300 python scripts/gpt2_bench.py 1 256 1 ;;
         *) echo "unknown step $step" ;;
     esac
 done
