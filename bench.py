@@ -13,9 +13,14 @@ kernel already costs 1.4-1.6 us of device time and dependent launches on one str
 every ~2.8 us (scripts/hbm_probe.hip); the per-matrix numbers are reported beside it
 (configs.*_single) so both regimes are visible.
 
-Multi-GPU (torchrun, one rank per GPU): every rank runs the same per-GPU workload on its own
-weights (weak scaling, no data-path collective — independent matrices partition with no
-exchange); barriers + max-over-ranks timing go through torch.distributed (RCCL).
+Multi-GPU (one process per GPU over torch.distributed / RCCL): `python bench.py --gpus N`
+starts the N ranks itself (a torch.distributed.run child process, before any GPU call) unless
+it is already running under torchrun; a rank count different from --gpus is an error. The
+headline: every rank runs the same per-GPU workload on its own weights (weak scaling, no
+data-path collective — independent matrices partition with no exchange); barriers +
+max-over-ranks timing go through torch.distributed. The row-sharded configs (configs.*_rowsplit,
+rowsplit.py) split ONE matrix's rows over the N ranks and all-gather dst (RCCL) every call:
+strong scaling of a single GEMM with its one exchange step.
 
 Extra fields on the single JSON line:
   roofline      the mat-vec kernel: algorithmic bytes per launch / mean launch duration
@@ -126,7 +131,7 @@ class MatVecSet:
                 self.launch(i)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, stream=s):   # capture on the warmed-up stream: its scratch is sized
             for i in range(n):
                 self.launch(i)
         g.replay()
@@ -161,9 +166,59 @@ def measured_traffic(key: str):
         return None
 
 
+def rowsplit_configs(torch, world: int, rank: int, reps: int = 20) -> dict:
+    """configs.*_rowsplit: ONE matrix row-sharded over the `world` ranks (rowsplit.py, the
+    split-buffer partition) and dst all-gathered over RCCL every call — strong scaling of a
+    single GEMM with its one exchange step. Collective: every rank calls it. Timed per call
+    (barrier + sync around `reps` calls, slowest rank); GB/s counts the whole matrix's
+    algorithmic bytes."""
+    import rowsplit as RS
+    import torch.distributed as dist
+    out = {}
+    dev = torch.device("cuda", torch.cuda.current_device())
+    for name, t, K, N, Mc in (("q4_K_4096x11008_m1_rowsplit", M.Q4_K, 4096, 11008, 1),
+                              ("q8_0_4096x4096_m512_rowsplit", M.Q8_0, 4096, 4096, 512)):
+        lo, hi = RS.row_split(N, world)[rank]
+        copies = 8                                 # rotated weight copies: HBM-cold per call
+        w = [torch.from_numpy(synthetic_weights(t, max(hi - lo, 1), K, 1234 + rank).reshape(-1)).to(dev) for _ in range(copies)]
+        x = torch.from_numpy(np.random.default_rng(5).uniform(-1, 1, (Mc, K)).astype(np.float32)).to(dev)
+        y = torch.zeros((Mc, N), dtype=torch.float32, device=dev)
+        mms = [RS.ShardedMatMul(torch, t, K, N, rank, world, wi) for wi in w]
+
+        def sync():
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+
+        for i in range(3):
+            mms[i % copies].forward(x, y)
+        sync()
+        t0 = time.perf_counter()
+        for i in range(reps):
+            mms[i % copies].forward(x, y)
+        sync()
+        el = time.perf_counter() - t0
+        t_max = max_over_ranks(el, dev) if world > 1 else el
+        us = t_max / reps * 1e6
+        gbytes = alg_bytes(t, K, N, Mc)
+        out[name] = {"us": round(us, 3), "GB/s": round(gbytes / us / 1e3, 1), "TFLOP/s": round(2.0 * K * N * Mc / us / 1e6, 3),
+                     "shards": world, "rows_per_shard": [b - a for a, b in RS.row_split(N, world)],
+                     "allgather_bytes": 4 * N * Mc if world > 1 else 0, "scaling": "strong",
+                     "timing": "host wall per call incl. the RCCL all-gather, slowest rank"}
+        del w, mms, x, y
+        torch.cuda.empty_cache()
+    return out
+
+
+def cpu_threads() -> int:
+    """Host threads for the CPU baseline: the CPU share the GPU box gives one GPU (its harness
+    exports OMP_NUM_THREADS=16 and allows no more: 128 cores / 8 GPUs), else all cores here."""
+    return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+
+
 def cpu_baseline(seconds: float) -> dict:
     """Reference ggml-cpu (oracle/_ref) on the host cores, bounded sample of the same config."""
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_cpu_bench")
     sample = f"Q4_0 K=4096 N=4096 M=1 mat-vec, 32 rotated weight copies (302 MB), ~{seconds:.0f} s"
     if os.path.exists(exe):
@@ -173,7 +228,8 @@ def cpu_baseline(seconds: float) -> dict:
         if out.returncode == 0:
             r = json.loads(out.stdout.strip().splitlines()[-1])
             return {"value": round(r["GBps"], 3), "unit": "GB/s", "cores": threads, "kind": "reference",
-                    "sample": sample, "us_per_mul_mat": round(r["sec_per_mul_mat"] * 1e6, 2)}
+                    "sample": sample, "us_per_mul_mat": round(r["sec_per_mul_mat"] * 1e6, 2),
+                    "host_cpus_visible": os.cpu_count()}
     # fallback: the C oracle restatement (scalar generic-order dots)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import qref
@@ -288,10 +344,68 @@ def cpu_gpt2_baseline(threads: int, tokens: int = 128) -> dict | None:
             "ms_per_token": round(j["ms_per_token"], 4)}
 
 
+def cpu_gpt2_example_baseline(threads: int, n_predict: int = 128) -> dict | None:
+    """the reference example itself (oracle/_ref/gpt-2-sched = examples/gpt-2/main-sched.cpp,
+    unmodified, CPU backend) greedy-decoding the synthetic 117M Q4_0 checkpoint: its own
+    'predict time ... ms per token' line"""
+    exe = os.path.join(ROOT, "oracle", "_ref", "gpt-2-sched")
+    if not os.path.exists(exe):
+        return None
+    sys.path[:0] = [os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+    import re
+    import tempfile
+
+    import gpt2_synth
+    import qref
+    path = os.path.join(tempfile.gettempdir(), f"bench_gpt2_example_{os.getpid()}.bin")
+    gpt2_synth.write_model(path, gpt2_synth.GPT2_117M, qref.Q4_0, 1234)
+    try:
+        r = subprocess.run([exe, "-m", path, "-p", "This is an example", "-n", str(n_predict), "--top_k", "1", "-s", "1",
+                            "-t", str(threads)], capture_output=True, text=True, timeout=600)
+        m = re.search(r"predict time =\s*([\d.]+) ms / ([\d.]+) ms per token", r.stdout)
+        if r.returncode != 0 or not m:
+            return None
+    finally:
+        os.remove(path)
+    ms = float(m.group(2))
+    return {"value": round(1e3 / ms, 2), "unit": "tokens/s", "cores": threads, "kind": "reference",
+            "sample": f"examples/gpt-2/main-sched.cpp itself, GPT-2 117M Q4_0 (synthetic), prompt 'This is an example' "
+                      f"(18 tokens) + {n_predict} greedy tokens, its predict-time average", "ms_per_token": ms}
+
+
 def launch_env():
     """(world, rank, local_rank) as torch.distributed.run exports them; 1 process by default"""
     return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
             int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def spawn_ranks(n: int) -> int:
+    """run this script under torch.distributed.run with n local ranks (127.0.0.1 rendezvous)"""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def dry_run(args, world: int, rank: int) -> None:
+    """--dry-run: the multi-rank plumbing on CPU (gloo) — launcher, barrier, slowest-rank
+    timing and the JSON line's n_gpus — without any GPU work"""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    t = 0.01 * (rank + 1)
+    t_max = max_over_ranks(t, torch.device("cpu")) if world > 1 else t
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run", "value": 0.0, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(t_max * 1e3, 4), "ranks_seen": world,
+                          "dry_run": True}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def max_over_ranks(seconds: float, device) -> float:
@@ -319,12 +433,24 @@ def main() -> None:
     ap.add_argument("--no-extra", action="store_true", help="skip the secondary configs")
     ap.add_argument("--no-gpt2", action="store_true", help="skip the GPT-2 decode leg")
     ap.add_argument("--gpt2-ticks", type=int, default=256, help="timed pipeline ticks of the GPT-2 leg")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU/gloo: only the launcher, rank plumbing and timing reduction (no GPU)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: start the ranks as a child torch.distributed.run (this process has
+        # not touched the GPU) and return its exit status
+        sys.exit(spawn_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
 
     world, rank, local = launch_env()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
+    if args.dry_run:
+        dry_run(args, world, rank)
+        return
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -391,6 +517,9 @@ def main() -> None:
             del s2
             torch.cuda.empty_cache()
 
+    if not args.no_extra:
+        extra.update(rowsplit_configs(torch, world, rank))
+
     cpu = cpu_baseline(args.cpu_seconds) if (rank == 0 and world == 1) else None
 
     # ---------------- GPT-2 117M Q4_0 decode, layers pipeline-split over the ranks ------------
@@ -414,7 +543,7 @@ def main() -> None:
             gpt2["single_stream_ms_per_token"] = round(r1["latency_ms_per_token"], 4)
             gpt2["single_stream_tokens_per_s"] = round(1e3 / r1["latency_ms_per_token"], 1)
         if cpu is not None:
-            cpu["gpt2"] = cpu_gpt2_baseline(cpu["cores"])
+            cpu["gpt2"] = cpu_gpt2_example_baseline(cpu["cores"]) or cpu_gpt2_baseline(cpu["cores"])
 
     if rank == 0:
         line = {

@@ -26,6 +26,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <array>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -47,6 +50,8 @@ struct GgmlBase {
     int (*graph_n_nodes)(struct ggml_cgraph *) = nullptr;
     struct ggml_tensor *(*graph_node)(struct ggml_cgraph *, int) = nullptr;
     size_t (*nbytes)(const struct ggml_tensor *) = nullptr;
+    ggml_backend_buffer_t (*cpu_buffer_from_ptr)(void *, size_t) = nullptr;
+    ggml_backend_buffer_type_t (*cpu_buffer_type)(void) = nullptr;
     bool ok = false;
 };
 
@@ -57,6 +62,8 @@ const GgmlBase &ggml_base() {
         g.graph_n_nodes = reinterpret_cast<decltype(g.graph_n_nodes)>(dlsym(RTLD_DEFAULT, "ggml_graph_n_nodes"));
         g.graph_node = reinterpret_cast<decltype(g.graph_node)>(dlsym(RTLD_DEFAULT, "ggml_graph_node"));
         g.nbytes = reinterpret_cast<decltype(g.nbytes)>(dlsym(RTLD_DEFAULT, "ggml_nbytes"));
+        g.cpu_buffer_from_ptr = reinterpret_cast<decltype(g.cpu_buffer_from_ptr)>(dlsym(RTLD_DEFAULT, "ggml_backend_cpu_buffer_from_ptr"));
+        g.cpu_buffer_type = reinterpret_cast<decltype(g.cpu_buffer_type)>(dlsym(RTLD_DEFAULT, "ggml_backend_cpu_buffer_type"));
         g.ok = g.buffer_init && g.graph_n_nodes && g.graph_node && g.nbytes;
         return g;
     }();
@@ -93,6 +100,7 @@ void logf(const char *fmt, ...) {
 // ------------------------------------------------------------------------------------------
 struct DeviceCtx {
     int device = 0;
+    std::vector<int> peers;          // devices this one reaches by peer access (enabled at init)
     std::string name, desc;
     struct ggml_backend_buffer_type buft {};
     std::string buft_name;
@@ -103,11 +111,21 @@ struct BufferCtx {
     void *base;
 };
 
+// per-shard state of one backend for split (row-sharded) mat-muls
+struct ShardLane {
+    int device = -1;
+    hipStream_t stream = nullptr;     // on `device`
+    hipEvent_t done = nullptr;        // recorded on `stream` after the shard's result landed in dst
+    Scratch src1, dst, mm;            // src1 copy, the shard's [rows x cols] result, mat-mat scratch; on `device`
+};
+
 struct BackendCtx {
     int device;
     hipStream_t stream = nullptr;
     std::string name;
     Scratch scratch;
+    hipEvent_t src1_ready = nullptr;  // recorded on `stream` before shards start (split mat-mul)
+    std::vector<std::unique_ptr<ShardLane>> shards;
 };
 
 const char *BUFT_TAG = "MI355X";
@@ -272,6 +290,254 @@ const struct ggml_backend_buffer_type_i BUFT_IFACE = {
 bool is_our_buft(ggml_backend_buffer_type_t buft) { return buft && buft->iface.get_name == buft_name; }
 
 // ------------------------------------------------------------------------------------------
+// row-split ("tensor parallel") buffer type: ggml_backend_split_buffer_type(main, tensor_split)
+// (reference ggml-cuda.cu:763-1094). A weight matrix in such a buffer is cut by rows into one
+// shard per device; MUL_MAT on it runs each shard's rows on that shard's device against a copy
+// of src1 and writes the shard's rows of dst on the main device (be_split_mul_mat). Same
+// partition rule as the reference's get_row_split (cumulative fractions, rows rounded down to
+// a multiple of SPLIT_ROW_ROUND except at the end), no padding (our kernels never over-read).
+//
+// GGML_MI355X_SPLIT_SHARDS=k sets the number of shards (default: one per device). With more
+// shards than devices, shard i lives on device i % n_devices: on a one-GPU box that runs the
+// whole multi-shard path (separate allocations, stream / event hand-offs, src1 copies, strided
+// gathers of dst) against one GPU, which is how the 1-GPU test box exercises it.
+// ------------------------------------------------------------------------------------------
+constexpr int SPLIT_MAX = 16;            // the reference's GGML_CUDA_MAX_DEVICES
+constexpr int64_t SPLIT_ROW_ROUND = 16;  // one 16-lane mat-vec row group
+
+int n_devices();
+int device_of(int idx);
+ggml_backend_dev_t dev_handle(int idx);
+
+int n_shards() {
+    static const int forced = getenv("GGML_MI355X_SPLIT_SHARDS") ? atoi(getenv("GGML_MI355X_SPLIT_SHARDS")) : 0;
+    const int n = forced > 0 ? forced : n_devices();
+    return std::max(1, std::min(n, SPLIT_MAX));
+}
+int shard_device(int i) { return device_of(i % std::max(1, n_devices())); }
+
+struct SplitBuftCtx {
+    int main_device;                   // our device index
+    std::array<float, SPLIT_MAX> split;   // cumulative start fraction of each shard
+    std::string name;
+};
+
+struct SplitExtra {
+    std::array<void *, SPLIT_MAX> data{};
+    std::array<int64_t, SPLIT_MAX> lo{}, hi{};
+    int device[SPLIT_MAX] = {};
+};
+
+struct SplitBufCtx {
+    std::vector<SplitExtra *> extras;
+};
+
+// rows [lo, hi) of shard id (get_row_split, ggml-cuda.cu:778-791)
+void split_rows(int64_t nrows, const SplitBuftCtx &bc, int id, int64_t &lo, int64_t &hi) {
+    const int n = n_shards();
+    lo = id == 0 ? 0 : (int64_t)(nrows * bc.split[id]);
+    lo -= lo % SPLIT_ROW_ROUND;
+    if (id == n - 1) {
+        hi = nrows;
+    } else {
+        hi = (int64_t)(nrows * bc.split[id + 1]);
+        hi -= hi % SPLIT_ROW_ROUND;
+    }
+    hi = std::max(hi, lo);
+}
+
+int64_t nrows_of(const struct ggml_tensor *t) { return t->ne[1] * t->ne[2] * t->ne[3]; }
+
+bool is_contiguous_rows(const struct ggml_tensor *t) {
+    return (int64_t)t->nb[2] == (int64_t)t->nb[1] * t->ne[1] && (int64_t)t->nb[3] == (int64_t)t->nb[2] * t->ne[2];
+}
+
+const char *split_buft_name(ggml_backend_buffer_type_t bt) { return static_cast<SplitBuftCtx *>(bt->context)->name.c_str(); }
+bool is_split_buft(ggml_backend_buffer_type_t bt) { return bt && bt->iface.get_name == split_buft_name; }
+
+void split_buf_free(ggml_backend_buffer_t b) {
+    auto *c = static_cast<SplitBufCtx *>(b->context);
+    for (SplitExtra *e : c->extras) {
+        for (int i = 0; i < SPLIT_MAX; ++i) {
+            if (e->data[i]) {
+                HIP_OK(hipSetDevice(e->device[i]));
+                HIP_OK(hipFree(e->data[i]));
+            }
+        }
+        delete e;
+    }
+    delete c;
+}
+
+void *split_buf_base(ggml_backend_buffer_t) { return reinterpret_cast<void *>(0x1000); }   // never dereferenced
+
+enum ggml_status split_buf_init_tensor(ggml_backend_buffer_t b, struct ggml_tensor *t) {
+    if (t->view_src != nullptr || !is_contiguous_rows(t)) {
+        fprintf(stderr, "[ggml-mi355x] split buffers hold whole contiguous tensors only (%s)\n", t->name);
+        return GGML_STATUS_FAILED;
+    }
+    const auto &bc = *static_cast<SplitBuftCtx *>(b->buft->context);
+    auto *e = new SplitExtra();
+    static_cast<SplitBufCtx *>(b->context)->extras.push_back(e);
+    const int64_t nrows = nrows_of(t);
+    for (int i = 0; i < n_shards(); ++i) {
+        split_rows(nrows, bc, i, e->lo[i], e->hi[i]);
+        e->device[i] = shard_device(i);
+        if (e->hi[i] <= e->lo[i]) continue;
+        HIP_OK(hipSetDevice(e->device[i]));
+        if (hipMalloc(&e->data[i], (size_t)(e->hi[i] - e->lo[i]) * t->nb[1]) != hipSuccess) {
+            (void)hipGetLastError();
+            e->data[i] = nullptr;
+            return GGML_STATUS_ALLOC_FAILED;
+        }
+    }
+    t->extra = e;
+    return GGML_STATUS_SUCCESS;
+}
+
+// whole-tensor set / get only, like the reference (ggml-cuda.cu:888-964)
+void split_buf_set(ggml_backend_buffer_t, struct ggml_tensor *t, const void *data, size_t off, size_t n) {
+    auto *e = static_cast<SplitExtra *>(t->extra);
+    if (off != 0 || n != ggml_base().nbytes(t)) {
+        fprintf(stderr, "[ggml-mi355x] split tensors must be set in their entirety\n");
+        abort();
+    }
+    for (int i = 0; i < n_shards(); ++i) {
+        if (!e->data[i]) continue;
+        HIP_OK(hipSetDevice(e->device[i]));
+        HIP_OK(hipMemcpy(e->data[i], static_cast<const uint8_t *>(data) + e->lo[i] * t->nb[1], (size_t)(e->hi[i] - e->lo[i]) * t->nb[1],
+                         hipMemcpyHostToDevice));
+    }
+}
+
+void split_buf_get(ggml_backend_buffer_t, const struct ggml_tensor *t, void *data, size_t off, size_t n) {
+    auto *e = static_cast<SplitExtra *>(t->extra);
+    if (off != 0 || n != ggml_base().nbytes(t)) {
+        fprintf(stderr, "[ggml-mi355x] split tensors must be read in their entirety\n");
+        abort();
+    }
+    for (int i = 0; i < n_shards(); ++i) {
+        if (!e->data[i]) continue;
+        HIP_OK(hipSetDevice(e->device[i]));
+        HIP_OK(hipMemcpy(static_cast<uint8_t *>(data) + e->lo[i] * t->nb[1], e->data[i], (size_t)(e->hi[i] - e->lo[i]) * t->nb[1],
+                         hipMemcpyDeviceToHost));
+    }
+}
+
+void split_buf_clear(ggml_backend_buffer_t, uint8_t) {}
+
+const struct ggml_backend_buffer_i SPLIT_BUFFER_IFACE = {
+    split_buf_free, split_buf_base, split_buf_init_tensor, nullptr, split_buf_set, split_buf_get, nullptr, split_buf_clear, nullptr,
+};
+
+ggml_backend_buffer_t split_buft_alloc(ggml_backend_buffer_type_t bt, size_t size) {
+    // the shards are allocated per tensor in init_tensor; `size` is the ggml-alloc bound
+    return ggml_base().buffer_init(bt, SPLIT_BUFFER_IFACE, new SplitBufCtx(), size);
+}
+
+size_t split_buft_align(ggml_backend_buffer_type_t) { return 128; }
+
+size_t split_buft_alloc_size(ggml_backend_buffer_type_t bt, const struct ggml_tensor *t) {
+    const auto &bc = *static_cast<SplitBuftCtx *>(bt->context);
+    size_t total = 0;
+    for (int i = 0; i < n_shards(); ++i) {
+        int64_t lo, hi;
+        split_rows(nrows_of(t), bc, i, lo, hi);
+        total += (size_t)(hi - lo) * t->nb[1];
+    }
+    return total;
+}
+
+bool split_buft_is_host(ggml_backend_buffer_type_t) { return false; }
+
+const struct ggml_backend_buffer_type_i SPLIT_BUFT_IFACE = {
+    split_buft_name, split_buft_alloc, split_buft_align, nullptr, split_buft_alloc_size, split_buft_is_host,
+};
+
+// the proc-address entry point (reference ggml_backend_cuda_split_buffer_type, ggml-cuda.cu:1054)
+extern "C" ggml_backend_buffer_type_t mi355x_split_buffer_type(int main_device, const float *tensor_split) {
+    static std::mutex mu;
+    static std::map<std::pair<int, std::array<float, SPLIT_MAX>>, std::unique_ptr<ggml_backend_buffer_type>> types;
+    std::lock_guard<std::mutex> lock(mu);
+    if (main_device < 0 || main_device >= n_devices()) return nullptr;
+    const int n = n_shards();
+    std::array<float, SPLIT_MAX> cum{};
+    bool all_zero = tensor_split == nullptr;
+    if (!all_zero) {
+        all_zero = true;
+        for (int i = 0; i < n; ++i) all_zero = all_zero && tensor_split[i] == 0.f;
+    }
+    float sum = 0.f;
+    for (int i = 0; i < n; ++i) {
+        cum[i] = sum;
+        sum += all_zero ? 1.f : tensor_split[i];   // default: equal shares (identical devices)
+    }
+    for (int i = 0; i < n; ++i) cum[i] /= sum;
+    auto &slot = types[{main_device, cum}];
+    if (!slot) {
+        auto *ctx = new SplitBuftCtx{main_device, cum, "MI355X" + std::to_string(main_device) + "_Split"};
+        slot.reset(new ggml_backend_buffer_type{SPLIT_BUFT_IFACE, dev_handle(main_device), ctx});
+    }
+    return slot.get();
+}
+
+// ------------------------------------------------------------------------------------------
+// pinned host buffer type (reference ggml_backend_cuda_host_buffer_type, ggml-cuda.cu:1096-1160):
+// page-locked memory behind ggml's own CPU buffer interface, so the CPU backend computes on
+// it and set/get_tensor_async become real DMA. Falls back to a plain CPU buffer when pinning
+// fails (GGML_MI355X_NO_PINNED disables it, like GGML_CUDA_NO_PINNED).
+// ------------------------------------------------------------------------------------------
+const char *host_buft_name(ggml_backend_buffer_type_t) { return "MI355X_Host"; }
+
+void host_buf_free(ggml_backend_buffer_t b) { HIP_OK(hipHostFree(b->context)); }
+
+ggml_backend_buffer_t host_buft_alloc(ggml_backend_buffer_type_t bt, size_t size) {
+    const GgmlBase &gb = ggml_base();
+    if (!gb.cpu_buffer_from_ptr || !gb.cpu_buffer_type) return nullptr;
+    void *p = nullptr;
+    if (getenv("GGML_MI355X_NO_PINNED") == nullptr && hipHostMalloc(&p, size ? size : 1, hipHostMallocPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        p = nullptr;
+    }
+    if (!p) {
+        ggml_backend_buffer_type_t cpu = gb.cpu_buffer_type();
+        return cpu->iface.alloc_buffer(cpu, size);
+    }
+    ggml_backend_buffer_t b = gb.cpu_buffer_from_ptr(p, size);
+    b->buft = bt;
+    b->context = p;                       // the CPU buffer keeps its base pointer in context
+    b->iface.free_buffer = host_buf_free;
+    return b;
+}
+
+size_t host_buft_align(ggml_backend_buffer_type_t) { return 64; }   // TENSOR_ALIGNMENT of the CPU buffer
+size_t host_buft_alloc_size(ggml_backend_buffer_type_t, const struct ggml_tensor *t) { return ggml_base().nbytes(t); }
+bool host_buft_is_host(ggml_backend_buffer_type_t) { return true; }
+
+ggml_backend_buffer_type_t host_buft() {
+    static struct ggml_backend_buffer_type bt = {
+        {host_buft_name, host_buft_alloc, host_buft_align, nullptr, host_buft_alloc_size, host_buft_is_host},
+        nullptr,
+        nullptr,
+    };
+    if (!bt.device) bt.device = dev_handle(0);
+    return &bt;
+}
+
+// ggml_backend_register_host_buffer / unregister (reference ggml-cuda.cu:3733-3740): pin
+// caller-owned memory for fast transfers
+extern "C" bool mi355x_register_host_buffer(void *buffer, size_t size) {
+    if (getenv("GGML_MI355X_NO_PINNED") != nullptr) return false;
+    const hipError_t e = hipHostRegister(buffer, size, hipHostRegisterPortable | hipHostRegisterReadOnly);
+    if (e != hipSuccess) (void)hipGetLastError();
+    return e == hipSuccess;
+}
+
+extern "C" void mi355x_unregister_host_buffer(void *buffer) {
+    if (hipHostUnregister(buffer) != hipSuccess) (void)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
 // backend (stream)
 // ------------------------------------------------------------------------------------------
 ggml_guid BACKEND_GUID = {0x6d, 0x69, 0x33, 0x35, 0x35, 0x78, 0x2d, 0x67, 0x66, 0x78, 0x39, 0x35, 0x30, 0x2d, 0x71, 0x6d};
@@ -285,6 +551,17 @@ void be_free(ggml_backend_t b) {
     HIP_OK(hipSetDevice(c->device));
     HIP_OK(hipStreamSynchronize(c->stream));
     HIP_OK(hipStreamDestroy(c->stream));
+    if (c->src1_ready) HIP_OK(hipEventDestroy(c->src1_ready));
+    for (auto &L : c->shards) {
+        if (!L || L->device < 0) continue;
+        HIP_OK(hipSetDevice(L->device));
+        HIP_OK(hipStreamSynchronize(L->stream));
+        HIP_OK(hipStreamDestroy(L->stream));
+        HIP_OK(hipEventDestroy(L->done));
+        L->src1.release();   // on the shard's device
+        L->dst.release();
+        L->mm.release();
+    }
     delete c;
     delete b;
 }
@@ -332,6 +609,73 @@ void be_sync(ggml_backend_t b) {
     HIP_OK(hipStreamSynchronize(c->stream));
 }
 
+// MUL_MAT whose src0 lives in a split buffer (reference ggml_cuda_op_mul_mat's split branch,
+// ggml-cuda.cu:1441-1700, restructured): the shard on the main device computes its rows of
+// dst in place on the backend stream; every other shard, on its own device and stream, waits
+// for src1, copies it over xGMI (peer DMA), runs its rows into a local [rows x cols] block and
+// writes that block into its rows of dst on the main device with one strided peer copy. The
+// backend stream then waits for every shard. src1 / dst must be contiguous (checked by
+// supports_op); src0 is 2-D.
+int be_split_mul_mat(BackendCtx *c, struct ggml_tensor *node) {
+    const struct ggml_tensor *a = node->src[0], *b = node->src[1];
+    auto *e = static_cast<const SplitExtra *>(a->extra);
+    const size_t row_b = a->nb[1];
+    const int64_t cols = node->ne[1] * node->ne[2] * node->ne[3];   // dst rows of ne0 floats
+    const size_t src1_bytes = ggml_base().nbytes(b);
+    if (!c->src1_ready) HIP_OK(hipEventCreateWithFlags(&c->src1_ready, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(c->src1_ready, c->stream));
+    int main_shard = -1;
+    for (int i = 0; i < n_shards(); ++i)
+        if (e->data[i] && e->device[i] == c->device) { main_shard = i; break; }
+    int rc = GGML_MI355X_OK;
+    for (int i = 0; i < n_shards() && rc == GGML_MI355X_OK; ++i) {
+        if (!e->data[i]) continue;
+        const int64_t rows = e->hi[i] - e->lo[i];
+        TensorView wa = tv(a);
+        wa.data = e->data[i];
+        wa.ne[1] = rows;
+        wa.nb[2] = wa.nb[3] = row_b * rows;
+        if (i == main_shard) {
+            TensorView d = tv(node);
+            d.data = static_cast<uint8_t *>(node->data) + e->lo[i] * sizeof(float);
+            d.ne[0] = rows;
+            rc = mul_mat(wa, tv(b), d, c->stream, c->scratch);
+            continue;
+        }
+        if ((int)c->shards.size() <= i) c->shards.resize(i + 1);
+        if (!c->shards[i]) c->shards[i] = std::make_unique<ShardLane>();
+        ShardLane &L = *c->shards[i];
+        HIP_OK(hipSetDevice(e->device[i]));
+        if (L.device != e->device[i]) {
+            L.device = e->device[i];
+            HIP_OK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
+            HIP_OK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
+        }
+        HIP_OK(hipStreamWaitEvent(L.stream, c->src1_ready, 0));
+        void *x = L.src1.get(src1_bytes, L.stream);
+        void *y = L.dst.get((size_t)rows * cols * sizeof(float), L.stream);
+        if (!x || !y) { rc = GGML_MI355X_ENOMEM; break; }
+        HIP_OK(hipMemcpyPeerAsync(x, e->device[i], b->data, c->device, src1_bytes, L.stream));
+        TensorView xb = tv(b);
+        xb.data = x;
+        TensorView d = tv(node);
+        d.data = y;
+        d.ne[0] = rows;
+        d.nb[1] = rows * sizeof(float);
+        d.nb[2] = d.nb[1] * node->ne[1];
+        d.nb[3] = d.nb[2] * node->ne[2];
+        rc = mul_mat(wa, xb, d, L.stream, L.mm);
+        if (rc != GGML_MI355X_OK) break;
+        HIP_OK(hipMemcpy2DAsync(static_cast<uint8_t *>(node->data) + e->lo[i] * sizeof(float), node->nb[1], y, rows * sizeof(float),
+                                rows * sizeof(float), cols, hipMemcpyDefault, L.stream));
+        HIP_OK(hipEventRecord(L.done, L.stream));
+        HIP_OK(hipSetDevice(c->device));
+        HIP_OK(hipStreamWaitEvent(c->stream, L.done, 0));
+    }
+    HIP_OK(hipSetDevice(c->device));
+    return rc;
+}
+
 enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
     BackendCtx *c = be_ctx(b);
     const GgmlBase &gb = ggml_base();
@@ -343,7 +687,9 @@ enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
         if (is_empty(node) || is_view_op(node->op)) continue;
         int rc;
         GraphOp gop;
-        if (node->op == GGMLABI_OP_MUL_MAT && is_hot_quant(node->src[0]->type)) {
+        if (node->op == GGMLABI_OP_MUL_MAT && node->src[0]->buffer && is_split_buft(node->src[0]->buffer->buft)) {
+            rc = be_split_mul_mat(c, node);
+        } else if (node->op == GGMLABI_OP_MUL_MAT && is_hot_quant(node->src[0]->type)) {
             rc = mul_mat(tv(node->src[0]), tv(node->src[1]), tv(node), c->stream, c->scratch);
         } else if (node->op == GGMLABI_OP_MUL_MAT_ID) {
             rc = mul_mat_id(tv(node->src[0]), tv(node->src[1]), tv(node->src[2]), tv(node), c->stream, c->scratch);
@@ -404,7 +750,7 @@ void dv_props(ggml_backend_dev_t d, struct ggml_backend_dev_props *p) {
     p->type = GGML_BACKEND_DEVICE_TYPE_GPU;
     dv_memory(d, &p->memory_free, &p->memory_total);
     p->caps.async = true;
-    p->caps.host_buffer = false;
+    p->caps.host_buffer = true;
     p->caps.buffer_from_host_ptr = false;
     p->caps.events = true;
 }
@@ -426,6 +772,8 @@ ggml_backend_t dv_init_backend(ggml_backend_dev_t d, const char *) {
 
 ggml_backend_buffer_type_t dv_buft(ggml_backend_dev_t d) { return &dev_ctx(d)->buft; }
 
+ggml_backend_buffer_type_t dv_host_buft(ggml_backend_dev_t) { return host_buft(); }
+
 bool supports_mm_operands(const struct ggml_tensor *a, const struct ggml_tensor *b) {
     if (!is_hot_quant(a->type) || b->type != GGMLABI_TYPE_F32) return false;
     if (a->ne[0] % type_blck(a->type) != 0 || (int64_t)a->nb[0] != type_bytes(a->type) || b->nb[0] != 4) return false;
@@ -441,7 +789,17 @@ bool supports_mm_operands(const struct ggml_tensor *a, const struct ggml_tensor 
 
 // mirrors the MUL_MAT arm of ggml_backend_cuda_device_supports_op (ggml-cuda.cu:3270-3330):
 // only the quantized hot path is claimed; everything else stays on the CPU backend.
-bool dv_supports_op(ggml_backend_dev_t, const struct ggml_tensor *op) {
+bool dv_supports_op(ggml_backend_dev_t d, const struct ggml_tensor *op) {
+    // split buffers only feed MUL_MAT (reference ggml-cuda.cu:3215-3222), as a 2-D src0 against
+    // contiguous f32 src1 / dst, with this device as the main device
+    for (int i = 0; i < GGMLABI_MAX_SRC; ++i) {
+        const struct ggml_tensor *t = op->src[i];
+        if (!t || !t->buffer || !is_split_buft(t->buffer->buft)) continue;
+        if (op->op != GGMLABI_OP_MUL_MAT || i != 0) return false;
+        if (t->buffer->buft->device != d || t->ne[2] != 1 || t->ne[3] != 1) return false;
+        if (!is_contiguous_rows(op->src[1]) || op->src[1]->nb[1] != op->src[1]->nb[0] * op->src[1]->ne[0]) return false;
+        if (!is_contiguous_rows(op) || op->nb[1] != op->nb[0] * op->ne[0]) return false;
+    }
     switch (op->op) {
         case GGMLABI_OP_NONE:
         case GGMLABI_OP_RESHAPE:
@@ -472,6 +830,7 @@ bool dv_supports_op(ggml_backend_dev_t, const struct ggml_tensor *op) {
 }
 
 bool dv_supports_buft(ggml_backend_dev_t d, ggml_backend_buffer_type_t bt) {
+    if (is_split_buft(bt)) return bt->device == d;
     return is_our_buft(bt) && static_cast<DeviceCtx *>(bt->context)->device == dev_ctx(d)->device;
 }
 
@@ -503,7 +862,7 @@ void dv_event_sync(ggml_backend_dev_t d, ggml_backend_event_t ev) {
 
 const struct ggml_backend_device_i DEVICE_IFACE = {
     dv_name, dv_desc, dv_memory, dv_type, dv_props, dv_init_backend, dv_buft,
-    nullptr, nullptr,
+    dv_host_buft, nullptr,
     dv_supports_op, dv_supports_buft, dv_offload_op,
     dv_event_new, dv_event_free, dv_event_sync,
 };
@@ -539,6 +898,9 @@ struct ggml_backend_feature *rg_features(ggml_backend_reg_t) { return FEATURES; 
 
 void *rg_proc(ggml_backend_reg_t, const char *name) {
     if (strcmp(name, "ggml_backend_get_features") == 0) return reinterpret_cast<void *>(rg_features);
+    if (strcmp(name, "ggml_backend_split_buffer_type") == 0) return reinterpret_cast<void *>(mi355x_split_buffer_type);
+    if (strcmp(name, "ggml_backend_register_host_buffer") == 0) return reinterpret_cast<void *>(mi355x_register_host_buffer);
+    if (strcmp(name, "ggml_backend_unregister_host_buffer") == 0) return reinterpret_cast<void *>(mi355x_unregister_host_buffer);
     if (strcmp(name, "ggml_mi355x_mul_mat") == 0) return reinterpret_cast<void *>(ggml_mi355x_mul_mat);
     if (strcmp(name, "ggml_mi355x_mul_mat_id") == 0) return reinterpret_cast<void *>(ggml_mi355x_mul_mat_id);
     if (strcmp(name, "ggml_mi355x_dequantize") == 0) return reinterpret_cast<void *>(ggml_mi355x_dequantize);
@@ -571,6 +933,30 @@ Registry &registry() {
             R->ctxs.push_back(std::move(dc));
             R->devs.push_back(std::move(dev));
         }
+        // peer access between every pair of our devices, once, at registry init: the scheduler's
+        // cross-device hand-off (be_cpy_async) and the split buffer's row shards then move over
+        // xGMI by direct DMA / direct loads. The reference enables it lazily around multi-device
+        // mat-muls (ggml_cuda_set_peer_access, ggml-cuda.cu:1363-1393); an MI355X node is a full
+        // xGMI mesh, so there is nothing to toggle per batch size.
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        for (auto &a : R->ctxs) {
+            for (auto &b : R->ctxs) {
+                if (a->device == b->device) continue;
+                int can = 0;
+                if (hipDeviceCanAccessPeer(&can, a->device, b->device) != hipSuccess || !can) {
+                    (void)hipGetLastError();
+                    continue;
+                }
+                (void)hipSetDevice(a->device);
+                const hipError_t e = hipDeviceEnablePeerAccess(b->device, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+                    fprintf(stderr, "[ggml-mi355x] peer access %d -> %d: %s\n", a->device, b->device, hipGetErrorString(e));
+                (void)hipGetLastError();
+                a->peers.push_back(b->device);
+            }
+        }
+        (void)hipSetDevice(prev);
         R->reg.api_version = GGMLABI_API_VERSION;
         R->reg.iface = {rg_name, rg_count, rg_dev, rg_proc};
         R->reg.context = nullptr;
@@ -578,6 +964,10 @@ Registry &registry() {
     }();
     return *r;
 }
+
+int n_devices() { return (int)registry().devs.size(); }
+int device_of(int idx) { return registry().ctxs[idx]->device; }
+ggml_backend_dev_t dev_handle(int idx) { return registry().devs[idx].get(); }
 
 }  // namespace
 

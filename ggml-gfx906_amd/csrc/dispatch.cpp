@@ -10,6 +10,9 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 
@@ -155,6 +158,7 @@ int mul_mat(const TensorView &a, const TensorView &b, const TensorView &d, hipSt
     hipError_t e;
     if (m.M > 8 && mmq_supported(a.type, m)) e = mmq_launch(a.type, m, st, scratch);
     else e = run_mmvq(a.type, m, 0, m.M, st);
+    if (e == hipErrorOutOfMemory) return GGML_MI355X_ENOMEM;
     return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
 }
 
@@ -199,6 +203,7 @@ int mul_mat_id(const TensorView &as, const TensorView &b, const TensorView &ids,
     static const int min_pairs = getenv("GGML_MI355X_MMQ_ID_MIN") ? atoi(getenv("GGML_MI355X_MMQ_ID_MIN")) : MMQ_ID_MIN_PAIRS;
     const bool grouped = m.n_used * m.n_tok >= min_pairs && mmq_id_supported(as.type, m);
     const hipError_t e = grouped ? mmq_id_launch(as.type, m, st, scratch) : mmvq_id_launch(as.type, m, 1, st);
+    if (e == hipErrorOutOfMemory) return GGML_MI355X_ENOMEM;
     return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
 }
 
@@ -265,8 +270,18 @@ int quantize(const TensorView &s, const TensorView &d, hipStream_t st) {
 // ------------------------------------------------------------------------------------------
 void *Scratch::get(size_t bytes, hipStream_t st) {
     if (bytes <= cap) return ptr;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess) {
+        (void)hipGetLastError();
+        cs = hipStreamCaptureStatusNone;
+    }
+    if (cs != hipStreamCaptureStatusNone) {
+        fprintf(stderr, "[ggml-mi355x] scratch of %zu bytes needed inside a hipGraph capture: run the launch once "
+                        "eagerly on this stream before capturing it\n", bytes);
+        return nullptr;
+    }
     if (ptr) {
-        (void)hipStreamSynchronize(st);    // previous users of the old buffer on this stream
+        (void)hipStreamSynchronize(st);    // the only users of the old buffer are on this stream
         (void)hipFree(ptr);
         ptr = nullptr;
         cap = 0;
@@ -274,15 +289,32 @@ void *Scratch::get(size_t bytes, hipStream_t st) {
     size_t want = std::max(bytes, (size_t)1 << 20);
     want = (want + 0xFFFFF) & ~(size_t)0xFFFFF;
     if (hipMalloc(&ptr, want) != hipSuccess) {
+        (void)hipGetLastError();
         ptr = nullptr;
         return nullptr;
     }
+    (void)hipGetDevice(&device);
     cap = want;
     return ptr;
 }
 
-Scratch::~Scratch() {
+void Scratch::release() {
     if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+}
+
+Scratch::~Scratch() { release(); }
+
+Scratch &scratch_for(hipStream_t st) {
+    static std::mutex mu;
+    static auto *reg = new std::map<std::pair<int, hipStream_t>, std::unique_ptr<Scratch>>();   // never destroyed: outlives HIP teardown
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lock(mu);
+    auto &p = (*reg)[{dev, st}];
+    if (!p) p = std::make_unique<Scratch>();
+    return *p;
 }
 
 }  // namespace mi355x
@@ -303,25 +335,21 @@ static TensorView view_of(const ggml_mi355x_tensor *t) {
     return v;
 }
 
-static Scratch &api_scratch() {
-    // one scratch per host thread for the direct API (the ggml backend owns its own per stream)
-    static thread_local Scratch s;
-    return s;
-}
 
 extern "C" {
 
 int ggml_mi355x_mul_mat(const ggml_mi355x_tensor *src0, const ggml_mi355x_tensor *src1, ggml_mi355x_tensor *dst,
                         void *stream) {
     if (!src0 || !src1 || !dst) return GGML_MI355X_EINVAL;
-    return mul_mat(view_of(src0), view_of(src1), view_of(dst), static_cast<hipStream_t>(stream), api_scratch());
+    return mul_mat(view_of(src0), view_of(src1), view_of(dst), static_cast<hipStream_t>(stream),
+                  scratch_for(static_cast<hipStream_t>(stream)));
 }
 
 int ggml_mi355x_mul_mat_id(const ggml_mi355x_tensor *as, const ggml_mi355x_tensor *b, const ggml_mi355x_tensor *ids,
                            ggml_mi355x_tensor *dst, void *stream) {
     if (!as || !b || !ids || !dst) return GGML_MI355X_EINVAL;
     return mul_mat_id(view_of(as), view_of(b), view_of(ids), view_of(dst), static_cast<hipStream_t>(stream),
-                      api_scratch());
+                      scratch_for(static_cast<hipStream_t>(stream)));
 }
 
 int ggml_mi355x_dequantize(int32_t type, const void *src, float *dst, int64_t n, void *stream) {
@@ -367,7 +395,7 @@ const char *ggml_mi355x_strerror(int status) {
     switch (status) {
         case GGML_MI355X_OK: return "ok";
         case GGML_MI355X_EINVAL: return "unsupported type or inconsistent shapes/strides";
-        case GGML_MI355X_ENOMEM: return "device scratch allocation failed";
+        case GGML_MI355X_ENOMEM: return "device scratch allocation failed (or needed growth inside a hipGraph capture)";
         case GGML_MI355X_EHIP: return "HIP runtime error";
         case GGML_MI355X_ENODEV: return "no gfx950 device";
         default: return "unknown status";

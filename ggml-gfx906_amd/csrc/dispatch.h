@@ -17,13 +17,22 @@ struct TensorView {
     size_t nb[4];
 };
 
-// grow-only device scratch owned by one stream user
+// grow-only device scratch owned by ONE (device, stream) pair: only work queued on that stream
+// touches it, so growing it (synchronize that stream, free, allocate) never races another
+// stream. Growing is refused (nullptr, the launch then fails with GGML_MI355X_ENOMEM) while the
+// stream is being captured into a hipGraph: hipFree / hipMalloc are not capturable, so a
+// captured launch must have been run once eagerly on the same stream first.
 struct Scratch {
     void *ptr = nullptr;
     size_t cap = 0;
+    int device = -1;
     void *get(size_t bytes, hipStream_t st);
+    void release();                   // free now (on the current device)
     ~Scratch();
 };
+
+// the process-wide scratch of (current device, st) for callers without a backend object
+Scratch &scratch_for(hipStream_t st);
 
 int type_blck(int t);
 int type_bytes(int t);

@@ -251,6 +251,11 @@ class Pipeline:
 
     def __init__(self, rank: int, world: int, n_micro: int, msg_elems: int, device, group=None):
         import torch
+        if n_micro != world:
+            # the tick schedule below keeps exactly one micro-batch per stage in flight: with
+            # fewer, stage 0 would read the ring before the last stage has produced a token; with
+            # more, a token arriving on the ring would be dropped for the next prompt
+            raise ValueError(f"Pipeline needs n_micro == world (got n_micro={n_micro}, world={world})")
         self.rank, self.world, self.n_micro = rank, world, n_micro
         self.next, self.prev = (rank + 1) % world, (rank - 1) % world
         self.recv = [torch.zeros(msg_elems, dtype=torch.float32, device=device) for _ in range(2)]

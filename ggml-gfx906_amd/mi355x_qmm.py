@@ -50,6 +50,13 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise Mi355xError(f"{LIB_PATH} missing: run `make -C ggml-gfx906_amd` (HIP extension not built)")
+        # torch-ROCm ships its own libamdhip64.so.7 (same soname as /opt/rocm's). Import torch
+        # first so the process holds ONE HIP runtime, torch's: loaded the other way round, our
+        # library would pull in /opt/rocm's runtime and torch's HIP init then finds no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         P = C.POINTER(MmTensor)
         L.ggml_mi355x_mul_mat.argtypes = [P, P, P, C.c_void_p]

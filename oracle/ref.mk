@@ -17,6 +17,10 @@
 #   _ref/ref_cpu_bench        our CPU-baseline timer (oracle/ref_cpu_bench.cpp) linked to the above
 #   _ref/gpt2_ref             GPT-2 logits / decode timing through the reference ggml graph
 #                             (oracle/gpt2_ref.cpp), CPU or the reference scheduler + our plugin
+#   _ref/gpt-2-sched          the reference example itself, unmodified: examples/gpt-2/main-sched.cpp
+#                             + examples/common{,-ggml}.cpp (CPU backend; pins gpt2_ref's greedy stream)
+#   _ref/split_check          MUL_MAT with src0 in our split (row-sharded) buffer type vs ggml-cpu,
+#                             driven through the reference's backend API (oracle/split_check.cpp)
 #
 # ISA: x86-64-v3 (AVX2/FMA/F16C) so the binaries also run on the GPU box's EPYC host;
 # -march=native here could emit AVX-512/AMX the box may lack.
@@ -45,7 +49,8 @@ CPU_CXX  := ggml-cpu/ggml-cpu.cpp ggml-cpu/repack.cpp ggml-cpu/hbm.cpp ggml-cpu/
 
 OBJS := $(patsubst %.c,$(OBJ)/%.c.o,$(BASE_C) $(CPU_C)) $(patsubst %.cpp,$(OBJ)/%.cpp.o,$(BASE_CXX) $(CPU_CXX))
 
-all: $(OUT)/libggml-ref.so $(OUT)/test-backend-ops $(OUT)/test-quantize-fns $(OUT)/gen_golden $(OUT)/ref_cpu_bench $(OUT)/gpt2_ref
+all: $(OUT)/libggml-ref.so $(OUT)/test-backend-ops $(OUT)/test-quantize-fns $(OUT)/gen_golden $(OUT)/ref_cpu_bench $(OUT)/gpt2_ref \
+     $(OUT)/gpt-2-sched $(OUT)/split_check
 
 $(OBJ)/ggml-cpu/%.c.o: $(REF)/src/ggml-cpu/%.c
 	@mkdir -p $(dir $@)
@@ -81,6 +86,13 @@ $(OUT)/ref_cpu_bench: oracle/ref_cpu_bench.cpp $(OUT)/libggml-ref.so
 	g++ $(CXXFLAGS) $< -o $@ $(LINK)
 
 $(OUT)/gpt2_ref: oracle/gpt2_ref.cpp $(OUT)/libggml-ref.so
+	g++ $(CXXFLAGS) $< -o $@ $(LINK)
+
+$(OUT)/gpt-2-sched: $(REF)/examples/gpt-2/main-sched.cpp $(REF)/examples/common.cpp $(REF)/examples/common-ggml.cpp $(OUT)/libggml-ref.so
+	g++ -O3 -pthread -std=gnu++17 -w $(ARCH) -DNDEBUG -I$(REF)/include -I$(REF)/examples $(REF)/examples/gpt-2/main-sched.cpp \
+	    $(REF)/examples/common.cpp $(REF)/examples/common-ggml.cpp -o $@ $(LINK)
+
+$(OUT)/split_check: oracle/split_check.cpp $(OUT)/libggml-ref.so
 	g++ $(CXXFLAGS) $< -o $@ $(LINK)
 
 clean:

@@ -54,3 +54,29 @@ def test_single_process_defaults(monkeypatch):
         monkeypatch.delenv(k, raising=False)
     assert bench.launch_env() == (1, 0, 0)
     assert bench.job_gbps(1e9, 10, 1, 2.0) == pytest.approx(5.0)
+
+
+def _bench_json(args, env=None):
+    import json
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(bench.ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=300, env=env)
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    return r.returncode, (json.loads(line[-1]) if line else None), r.stderr
+
+
+def test_bench_gpus_2_starts_two_ranks():
+    """`bench.py --gpus 2` with no launcher starts its own torch.distributed.run child with two
+    ranks (gloo dry run: rank plumbing only) and reports n_gpus = 2 from the slowest rank"""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    rc, line, err = _bench_json(["--gpus", "2", "--dry-run"], env)
+    assert rc == 0, err[-2000:]
+    assert line["n_gpus"] == 2 and line["ranks_seen"] == 2
+    assert line["ms_per_step"] == pytest.approx(20.0)    # max over ranks (rank 1: 20 ms)
+
+
+def test_bench_rejects_rank_count_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    rc, line, err = _bench_json(["--gpus", "2", "--dry-run"], env)
+    assert rc != 0 and line is None and "--gpus 2" in err

@@ -184,7 +184,13 @@ def _ring_worker(rank, world, port, n_micro, n_ticks, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_micro", [(2, 2), (3, 3), (2, 1)])
+@pytest.mark.parametrize("world,n_micro", [(2, 1), (2, 3), (3, 2)])
+def test_pipeline_rejects_unsupported_micro_batching(world, n_micro):
+    with pytest.raises(ValueError):
+        G.Pipeline(0, world, n_micro, 8, "cpu")
+
+
+@pytest.mark.parametrize("world,n_micro", [(2, 2), (3, 3), (4, 4)])
 def test_pipeline_ring_gloo(world, n_micro):
     """ring protocol on CPU/gloo: every micro-batch's token advances by sum(r+1) per lap"""
     import multiprocessing as mp
@@ -207,9 +213,9 @@ def test_pipeline_ring_gloo(world, n_micro):
     seen = {}
     for mb, tok in res[0][1]:
         seen.setdefault(mb, []).append(tok)
+    assert sorted(seen) == list(range(n_micro))
     for mb, toks in seen.items():
-        if n_micro == world:
-            assert toks == [100 * mb + i * inc for i in range(len(toks))], (mb, toks)
+        assert toks == [100 * mb + i * inc for i in range(len(toks))], (mb, toks)
     assert res[0][0] == n_ticks
     for r in range(world):
         assert res[r][0] == n_ticks - r

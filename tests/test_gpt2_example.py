@@ -1,0 +1,105 @@
+"""GPT-2 greedy decode pinned to the REFERENCE EXAMPLE ITSELF.
+
+oracle/_ref/gpt-2-sched is examples/gpt-2/main-sched.cpp + examples/common{,-ggml}.cpp compiled
+unmodified from /root/reference (oracle/ref.mk; CPU backend, since the example only reaches a
+GPU through ggml-cuda). Run with --top_k 1 its sampler (gpt_sample_top_k_top_p, examples/
+common.cpp:401-478) keeps only the largest logit, i.e. greedy decoding. It prints the prompt and
+the generated tokens as text; the synthetic vocabulary (tests/gpt2_synth.py: ids 0-94 are the
+printable ASCII characters, the rest "<tN>") makes that text parse back into ids exactly.
+
+  * CPU: oracle/gpt2_ref (our restatement of the example's graph on the reference ggml, which
+    the golden logits come from) teacher-forced with the example's own stream must put its
+    argmax on every token the example chose — this pins the restatement to the example.
+  * GPU: the MI355X engine's device-resident greedy loop must generate the example's stream.
+"""
+import json
+import os
+import re
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import gpt2_synth
+import qref
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXAMPLE = os.path.join(ROOT, "oracle", "_ref", "gpt-2-sched")
+REF_BIN = os.path.join(ROOT, "oracle", "_ref", "gpt2_ref")
+MANIFEST = json.load(open(os.path.join(ROOT, "tests", "golden", "gpt2_manifest.json")))
+SMALL = MANIFEST["hparams"]
+PROMPT = "This is an example"   # main-sched.cpp's own default prompt in the README runs
+N_NEW = 24
+
+needs_example = pytest.mark.skipif(not (os.path.exists(EXAMPLE) and os.path.exists(REF_BIN)),
+                                   reason="oracle/_ref not built (make -f oracle/ref.mk)")
+
+
+def prompt_ids(text: str) -> list:
+    """the example's tokenization of an ASCII prompt under the synthetic vocabulary: one
+    character per token (gpt_tokenize, examples/common.cpp:259-351, longest match = 1 char)"""
+    return [ord(c) - 32 for c in text]
+
+
+def parse_generated(stdout: str, prompt: str) -> list:
+    text = stdout.split(f"main: prompt: '{prompt}'", 1)[1]
+    text = text.split("\n\n", 1)[1]                    # after "number of tokens in prompt ..."
+    text = text.split("\n\nmain:", 1)[0]
+    assert text.startswith(prompt), text[:80]
+    gen = text[len(prompt):]
+    return [int(m.group(1)) if m.group(1) else ord(m.group(2)) - 32 for m in re.finditer(r"<t(\d+)>|(.)", gen, re.S)]
+
+
+_streams = {}
+
+
+def model_and_stream(name: str):
+    """(checkpoint path, prompt ids, the example's greedy ids) for golden case `name`"""
+    if name not in _streams:
+        path = os.path.join(tempfile.gettempdir(), f"gpt2_example_{name}_{os.getpid()}.bin")
+        sha = gpt2_synth.write_model(path, SMALL, qref.BY_NAME[name], MANIFEST["seed"])
+        assert sha == MANIFEST["cases"][name]["model_sha256"]
+        r = subprocess.run([EXAMPLE, "-m", path, "-p", PROMPT, "-n", str(N_NEW), "--top_k", "1", "-s", "1", "-t", "4"],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        gen = parse_generated(r.stdout, PROMPT)
+        assert len(gen) == N_NEW, gen
+        _streams[name] = (path, prompt_ids(PROMPT), gen)
+    return _streams[name]
+
+
+def test_parse_generated():
+    out = "main: prompt: 'ab'\nmain: number of tokens in prompt = 2, first 8 tokens: 65 66 \n\nab<t145>c<t7>\n\nmain:  load"
+    assert parse_generated(out, "ab") == [145, ord("c") - 32, 7]
+
+
+@needs_example
+@pytest.mark.parametrize("name", ["q4_0", "q4_K", "q6_K"])
+def test_gpt2_ref_pinned_to_reference_example(name):
+    path, prompt, gen = model_and_stream(name)
+    seq = prompt + gen
+    out = path + ".logits"
+    subprocess.run([REF_BIN, path, "--tokens", ",".join(map(str, seq[:-1])), "--out", out, "--threads", "4"], check=True,
+                   capture_output=True, timeout=300)
+    logits = np.fromfile(out, np.float32).reshape(len(seq) - 1, SMALL["n_vocab"])
+    os.remove(out)
+    # position i predicts token i + 1; the example sampled from the last prompt position on
+    got = logits[len(prompt) - 1:].argmax(1).tolist()
+    assert got == gen
+
+
+@pytest.mark.gpu
+@needs_example
+@pytest.mark.parametrize("name", ["q4_0", "q4_K", "q6_K"])
+def test_engine_greedy_matches_reference_example(name):
+    import gpt2 as G
+    path, prompt, gen = model_and_stream(name)
+    hp = G.read_hparams(path)
+    st = G.Stage(hp)
+    st.load(path)
+    ctx = G.Context(st, 1)
+    got = G.greedy_generate(ctx, [prompt], N_NEW)[0]
+    ctx.free()
+    st.free()
+    assert got == gen
