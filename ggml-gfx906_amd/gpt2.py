@@ -249,7 +249,10 @@ class Pipeline:
     the output buffer to forward (a torch tensor of `msg_elems` f32). The protocol is
     independent of the compute, so it is tested on CPU with gloo and a numpy stage."""
 
-    def __init__(self, rank: int, world: int, n_micro: int, msg_elems: int, device, group=None):
+    def __init__(self, rank: int, world: int, n_micro: int, msg_elems: int, device, group=None, comm_device=None):
+        """device: where stage outputs live; comm_device: where the exchange happens (default
+        = device; "cpu" stages every message through host memory, for process groups whose
+        backend cannot move device tensors, e.g. gloo with two ranks sharing one GPU)"""
         import torch
         if n_micro != world:
             # the tick schedule below keeps exactly one micro-batch per stage in flight: with
@@ -258,7 +261,8 @@ class Pipeline:
             raise ValueError(f"Pipeline needs n_micro == world (got n_micro={n_micro}, world={world})")
         self.rank, self.world, self.n_micro = rank, world, n_micro
         self.next, self.prev = (rank + 1) % world, (rank - 1) % world
-        self.recv = [torch.zeros(msg_elems, dtype=torch.float32, device=device) for _ in range(2)]
+        self.comm_device = torch.device(comm_device if comm_device is not None else device)
+        self.recv = [torch.zeros(msg_elems, dtype=torch.float32, device=self.comm_device) for _ in range(2)]
         self.group = group
         self.cur = 0
         self.k = 0
@@ -276,6 +280,8 @@ class Pipeline:
         else:
             inbuf = self.recv[self.cur]
         out = stage_fn(mb, inbuf, valid)
+        if out.device != self.comm_device:
+            out = out.to(self.comm_device)     # synchronizes the producing stream
         if self.world > 1:
             nxt = 1 - self.cur
             ops = [dist.P2POp(dist.isend, out, self.next, self.group),
@@ -294,3 +300,54 @@ class Pipeline:
             done += self.tick(self.k, stage_fn, first_input_fn)
             self.k += 1
         return done
+
+
+def pipeline_generate(stage: Stage, rank: int, world: int, prompts: list, n_new: int, comm_device=None, group=None,
+                      graph: bool = True):
+    """Greedy generation through the ring pipeline with real stages: micro-batch mb (one
+    sequence, prompt prompts[mb]; n_micro = world) walks the stages every `world` ticks. Stage
+    0 feeds the prompt one token per visit, then the token the last stage sent round the ring.
+    Returns the n_new generated ids per micro-batch on rank 0 (None elsewhere). Collective:
+    every rank calls it with its own stage."""
+    import torch
+    P = len(prompts[0])
+    assert len(prompts) == world and all(len(p) == P for p in prompts)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    st = torch.cuda.current_stream().cuda_stream
+    E = stage.hp["n_embd"]
+    ctxs = [Context(stage, 1) for _ in range(world)]
+    zero = torch.zeros(1, dtype=torch.int32, device=dev)
+    for c in ctxs:
+        c.set_pos(zero.data_ptr(), st)
+    send = [torch.zeros(E, dtype=torch.float32, device=dev) for _ in range(world)]
+    steps = [0] * world
+    gen = [[] for _ in range(world)]
+    host_tok = torch.zeros(1, dtype=torch.int32)
+
+    def stage_fn(mb, inbuf, valid):
+        if valid and steps[mb] < P + n_new:
+            c = ctxs[mb]
+            k = steps[mb]
+            if stage.first:
+                if k < P:
+                    tok = torch.tensor([prompts[mb][k]], dtype=torch.int32, device=dev)
+                else:
+                    host_tok.copy_(inbuf.view(torch.int32)[:1].cpu())
+                    gen[mb].append(int(host_tok[0]))
+                    tok = host_tok.to(dev)
+                c.set_tokens(tok.data_ptr(), st)
+            else:
+                c._copy(c.hidden_ptr, inbuf.data_ptr(), c.hidden_bytes, st)
+            c.decode(st, graph)
+            steps[mb] += 1
+            src = c.tokens_ptr if stage.last else c.hidden_ptr
+            c._copy(send[mb].data_ptr(), src, 4 if stage.last else c.hidden_bytes, st)
+        return send[mb]
+
+    pipe = Pipeline(rank, world, world, E, dev, group=group, comm_device=comm_device)
+    first = lambda mb: send[mb]  # noqa: E731  (stage 0 ignores its input while in the prompt)
+    pipe.run(world * (P + n_new) + world, stage_fn, first)
+    torch.cuda.synchronize()
+    for c in ctxs:
+        c.free()
+    return gen if rank == 0 else None
