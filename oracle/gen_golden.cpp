@@ -239,20 +239,50 @@ static void gen_mul_mat(ggml_type ta, int64_t m, int64_t n, int64_t k, int bs0, 
     char name[160];
     snprintf(name, sizeof name, "mm_%03d_%s_m%lld_n%lld_k%lld", g_mm_id, ggml_type_name(ta), (long long)m, (long long)n, (long long)k);
     size_t nstore = res.size();
-    if (store_cols > 0 && store_cols < cols) nstore = (size_t)(store_cols * out->ne[0]);
-    write_bin(std::string(name) + ".out.f32", res.data(), nstore * 4);
-    char js[1024];
+    std::string sample_js, colsum_js;
+    if (store_cols > 0 && store_cols < cols) {
+        // big case: the reference's output is stored for a strided sample of columns that
+        // touches every 128-column tile (its first 8 columns, every 16th, the tile edges), and
+        // every column is pinned by its (sum, sum of squares) in f64
+        std::vector<int64_t> pick;
+        for (int64_t c = 0; c < cols; ++c)
+            if (c < store_cols || c % 16 == 15 || c % 128 == 0 || c % 128 == 127 || c == cols - 1) pick.push_back(c);
+        std::vector<float> sub;
+        for (int64_t c : pick) sub.insert(sub.end(), res.begin() + c * out->ne[0], res.begin() + (c + 1) * out->ne[0]);
+        write_bin(std::string(name) + ".out.f32", sub.data(), sub.size() * 4);
+        nstore = sub.size();
+        sample_js = ", \"sample_cols\": [";
+        for (size_t i = 0; i < pick.size(); ++i) sample_js += (i ? ", " : "") + std::to_string(pick[i]);
+        sample_js += "]";
+        std::vector<double> cs(2 * cols);
+        for (int64_t c = 0; c < cols; ++c) {
+            double s1 = 0, s2 = 0;
+            for (int64_t i = 0; i < out->ne[0]; ++i) {
+                const double v = res[c * out->ne[0] + i];
+                s1 += v;
+                s2 += v * v;
+            }
+            cs[2 * c] = s1;
+            cs[2 * c + 1] = s2;
+        }
+        write_bin(std::string(name) + ".colsums.f64", cs.data(), cs.size() * 8);
+        colsum_js = ", \"colsums\": \"" + std::string(name) + ".colsums.f64\"";
+    } else {
+        write_bin(std::string(name) + ".out.f32", res.data(), nstore * 4);
+    }
+    char js[4096];
     snprintf(js, sizeof js,
              "{\"kind\": \"mul_mat\", \"name\": \"%s\", \"type\": \"%s\", \"type_id\": %d, \"m\": %lld, \"n\": %lld, \"k\": %lld, "
              "\"bs\": [%d, %d], \"nr\": [%d, %d], \"per\": [%d, %d, %d, %d], \"view\": %s, "
              "\"a_ne\": [%lld, %lld, %lld, %lld], \"b_ne\": [%lld, %lld, %lld, %lld], \"seed_a\": %llu, \"seed_b\": %llu, "
-             "\"out_ne\": [%lld, %lld, %lld, %lld], \"stored_floats\": %zu}",
+             "\"out_ne\": [%lld, %lld, %lld, %lld], \"stored_floats\": %zu%s%s}",
              name, ggml_type_name(ta), (int)ta, (long long)m, (long long)n, (long long)k, bs0, bs1, nr0, nr1,
              per[0], per[1], per[2], per[3], view ? "true" : "false",
              (long long)a_phys->ne[0], (long long)a_phys->ne[1], (long long)a_phys->ne[2], (long long)a_phys->ne[3],
              (long long)b_phys->ne[0], (long long)b_phys->ne[1], (long long)b_phys->ne[2], (long long)b_phys->ne[3],
              (unsigned long long)sa, (unsigned long long)sb,
-             (long long)out->ne[0], (long long)out->ne[1], (long long)out->ne[2], (long long)out->ne[3], nstore);
+             (long long)out->ne[0], (long long)out->ne[1], (long long)out->ne[2], (long long)out->ne[3], nstore,
+             sample_js.c_str(), colsum_js.c_str());
     record(js);
     ++g_mm_id;
 }

@@ -7,6 +7,8 @@ from its sources (oracle/ref.mk). Bars:
   * SIMD vec_dot / full CPU-backend MUL_MAT and MUL_MAT_ID: NMSE <= 5e-6 (the oracle keeps the
     generic fp32 summation order; the x86 SIMD order differs in the last bits).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -89,3 +91,18 @@ def test_mul_mat_id_matches_reference_cpu(r):
     got = G.oracle_mul_mat_id(a, b, ids, out_ne)
     want = G.load_bin(r["name"] + ".out.f32", np.float32)
     assert qref.nmse(got, want) <= 5e-6
+
+
+@pytest.mark.parametrize("r", [r for r in _recs("mul_mat") if "sample_cols" in r], ids=lambda r: r["name"])
+def test_big_mul_mat_oracle_vs_reference_sample_and_column_sums(r):
+    """the BASELINE Q8_0 4096x4096x512 record: the oracle (threaded) matches the reference's
+    sampled columns (every 128-column tile) and every column's f64 (sum, sum of squares)"""
+    a, b, out_ne = G.mul_mat_operands(r)
+    got = G.oracle_mul_mat(a, b, out_ne, threads=os.cpu_count() or 8).reshape(-1, out_ne[0])
+    want = G.load_bin(r["name"] + ".out.f32", np.float32).reshape(len(r["sample_cols"]), -1)
+    assert sorted({c // 128 for c in r["sample_cols"]}) == list(range((out_ne[1] + 127) // 128))
+    assert qref.nmse(got[r["sample_cols"]], want) <= 5e-6
+    cs = G.load_bin(r["colsums"], np.float64).reshape(-1, 2)
+    g64 = got.astype(np.float64)
+    assert np.all(np.abs(g64.sum(1) - cs[:, 0]) <= 1e-4 * np.sqrt(cs[:, 1]))
+    assert np.all(np.abs((g64 ** 2).sum(1) / cs[:, 1] - 1) <= 1e-5)
