@@ -25,6 +25,7 @@ hipError_t mmvq_launch(int type, const MmArgs &a, int nc, int rpw, hipStream_t s
 hipError_t mmvq_id_launch(int type, const MmArgs &a, int rpw, hipStream_t st);
 size_t mmvq_lds_bytes(int K, int nc);
 bool mmvq_has_nc(int nc);
+int mmvq_max_k_for_nc(int nc);
 bool mmvq_bigk(int K);
 hipError_t dequant_launch(int type, const void *src, float *dst, int64_t n, hipStream_t st);
 hipError_t mmq_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
@@ -87,7 +88,8 @@ static int pick_rpw(int64_t rows_total) {
 static unsigned long long *g_stamps = nullptr;
 static const size_t STAMP_SLOTS = 8 * 65536;
 
-static unsigned long long *stamps_buffer() {
+unsigned long long *stamps_buffer();
+unsigned long long *stamps_buffer() {
     static const bool on = getenv("GGML_MI355X_STAMPS") != nullptr;
     if (!on) return nullptr;
     if (!g_stamps && hipMalloc(&g_stamps, STAMP_SLOTS * sizeof(unsigned long long)) != hipSuccess) g_stamps = nullptr;
@@ -136,7 +138,7 @@ static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st
     const int rpw = pick_rpw((int64_t)m.N * m.ne12 * m.ne13);
     while (ncols > 0) {
         int nc = mmvq_bigk(m.K) ? 1 : std::min(ncols, 8);
-        while (nc > 1 && (!mmvq_has_nc(nc) || mmvq_lds_bytes(m.K, nc) > LDS_LIMIT)) --nc;
+        while (nc > 1 && (!mmvq_has_nc(nc) || mmvq_lds_bytes(m.K, nc) > LDS_LIMIT || m.K > mmvq_max_k_for_nc(nc))) --nc;
         MmArgs g = m;
         g.x = m.x + (int64_t)c0 * m.nb11;
         g.dst = m.dst + (int64_t)c0 * m.nb1;

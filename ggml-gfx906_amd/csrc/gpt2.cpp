@@ -18,6 +18,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <map>
@@ -31,9 +32,10 @@
 namespace mi355x {
 hipError_t mmvq_fused_launch(int type, const MmArgs &a, int nc, int rpw, hipStream_t st);
 hipError_t mmvq_fused_prepare(int type);
+unsigned long long *stamps_buffer();
 hipError_t gpt2_embed_launch(int wtype, const void *wte, int64_t wte_nb1, const float *wpe, const int32_t *tokens,
                              const int32_t *pos, float *x, int n_seq, int n_embd, int n_vocab, int n_ctx, hipStream_t st);
-hipError_t gpt2_attn_launch(const float *qkv, float *kc, float *vc, const int32_t *pos, float *out, int n_seq, int n_head,
+hipError_t gpt2_attn_launch(const float *qkv, float *kc, float *vc, const int32_t *pos, float *part, int n_seq, int n_head,
                             int n_embd, int n_ctx, float scale, hipStream_t st);
 hipError_t gpt2_argmax_launch(const float *pv, const int32_t *pi, int n_seq, int32_t *tokens, int32_t *pos, hipStream_t st);
 hipError_t gpt2_argmax_reset(float *pv, int32_t *pi, int n_seq, hipStream_t st);
@@ -98,6 +100,7 @@ struct ggml_mi355x_gpt2_ctx {
     int32_t *tokens = nullptr, *pos = nullptr;
     float *x = nullptr, *qkv = nullptr, *attn = nullptr, *h = nullptr, *logits = nullptr;
     float *kc = nullptr, *vc = nullptr;        // [layer][seq][n_ctx][n_embd]
+    float *part = nullptr;                     // attention partials [seq][head][ATTN_SPLITS][ATTN_PART_STRIDE]
     float *amax_v = nullptr;                   // lm_head per-workgroup argmax partials [seq][ARGMAX_SLOTS]
     int32_t *amax_i = nullptr;
     std::map<hipStream_t, hipGraphExec_t> graphs;
@@ -112,16 +115,16 @@ int hip_status_at(hipError_t e, const char *where) {
 }
 #define hip_status(e) hip_status_at((e), #e)
 
-// widest column group with a kernel that divides n_seq
-int pick_nc(int n) {
+// widest column group with a kernel that divides n_seq (groups of 4 / 8 serve K <= 4096)
+int pick_nc(int n, int K) {
     for (int nc : {8, 4, 3, 2, 1})
-        if (n % nc == 0) return nc;
+        if (n % nc == 0 && (nc < 4 || K <= 4096)) return nc;
     return 1;
 }
 
 // y[n_seq][N] (+)= W[N][K] . x[n_seq][K] with the fused prologue / epilogue
 int fused_matvec(const ggml_mi355x_gpt2_ctx *c, const Tensor &w, const float *x, float *y, const Tensor *ln_g, const Tensor *ln_b,
-                 const Tensor *bias, int epi, hipStream_t st) {
+                 const Tensor *bias, int epi, hipStream_t st, const float *attn_part = nullptr) {
     // EPI_ARGMAX writes one partial per workgroup: ARGMAX_SLOTS bounds the grid (mmvq_fused.hip)
     MmArgs a{};
     const int K = (int)w.ne0, N = (int)w.ne1, M = c->n_seq;
@@ -146,8 +149,18 @@ int fused_matvec(const ggml_mi355x_gpt2_ctx *c, const Tensor &w, const float *x,
     a.epi = epi;
     a.amax_v = c->amax_v;
     a.amax_i = c->amax_i;
+    a.attn_part = attn_part;                   // c_proj: activations = merged attention partials
+    a.n_head = c->m->hp.n_head;
+    // diagnostics: GGML_MI355X_STAMPS=1 + GGML_MI355X_STAMP_MV=i stamps the i-th fused mat-vec of
+    // a decode step (0 = first layer's c_attn); scripts/gpt2_stamps.py reads them
+    static const int stamp_mv = getenv("GGML_MI355X_STAMP_MV") ? atoi(getenv("GGML_MI355X_STAMP_MV")) : -1;
+    static thread_local int mv_counter = 0;
+    if (mv_counter++ == stamp_mv) a.stamps = stamps_buffer();
+    if (epi & EPI_ARGMAX) mv_counter = 0;      // the last mat-vec of a step
     a.fused = 1;
-    return hip_status(mmvq_fused_launch(w.type, a, pick_nc(M), N >= 16384 ? 2 : 1, st));
+    // the attention-merge prologue (c_proj) keeps its partials in registers: groups of <= 3 columns
+    const int nc = attn_part ? (M % 3 == 0 ? 3 : M % 2 == 0 ? 2 : 1) : pick_nc(M, K);
+    return hip_status(mmvq_fused_launch(w.type, a, nc, N >= 16384 ? 2 : 1, st));
 }
 
 int run_step(ggml_mi355x_gpt2_ctx *c, hipStream_t st) {
@@ -167,8 +180,8 @@ int run_step(ggml_mi355x_gpt2_ctx *c, hipStream_t st) {
         float *kc = c->kc + (size_t)(l - m->l0) * cache_layer;
         float *vc = c->vc + (size_t)(l - m->l0) * cache_layer;
         if ((rc = fused_matvec(c, L.attn_w, c->x, c->qkv, &L.ln1_g, &L.ln1_b, &L.attn_b, 0, st))) return rc;
-        if ((rc = hip_status(gpt2_attn_launch(c->qkv, kc, vc, c->pos, c->attn, c->n_seq, hp.n_head, E, hp.n_ctx, kq_scale, st)))) return rc;
-        if ((rc = fused_matvec(c, L.proj_w, c->attn, c->x, nullptr, nullptr, &L.proj_b, EPI_RESID, st))) return rc;
+        if ((rc = hip_status(gpt2_attn_launch(c->qkv, kc, vc, c->pos, c->part, c->n_seq, hp.n_head, E, hp.n_ctx, kq_scale, st)))) return rc;
+        if ((rc = fused_matvec(c, L.proj_w, c->attn, c->x, nullptr, nullptr, &L.proj_b, EPI_RESID, st, c->part))) return rc;
         if ((rc = fused_matvec(c, L.fc_w, c->x, c->h, &L.ln2_g, &L.ln2_b, &L.fc_b, EPI_GELU, st))) return rc;
         if ((rc = fused_matvec(c, L.mproj_w, c->h, c->x, nullptr, nullptr, &L.mproj_b, EPI_RESID, st))) return rc;
     }
@@ -388,7 +401,8 @@ int ggml_mi355x_gpt2_ctx_init(ggml_mi355x_gpt2_model *m, int32_t n_seq, ggml_mi3
     const size_t b_logits = m->last ? al(4 * S * hp.n_vocab) : 0;
     const size_t b_cache = al(4 * n_layers * S * hp.n_ctx * E);
     const size_t b_amax = m->last ? al(4 * S * ARGMAX_SLOTS) : 0;
-    const size_t total = 2 * b_tok + 2 * b_x + b_qkv + b_h + b_logits + 2 * b_cache + 2 * b_amax;
+    const size_t b_part = al(4 * S * hp.n_head * ATTN_SPLITS * ATTN_PART_STRIDE);
+    const size_t total = 2 * b_tok + 2 * b_x + b_qkv + b_h + b_logits + 2 * b_cache + 2 * b_amax + b_part;
     if (mmvq_fused_prepare(m->wtype) != hipSuccess) return GGML_MI355X_EHIP;   // before any capture
     auto *c = new ggml_mi355x_gpt2_ctx();
     c->m = m;
@@ -408,6 +422,7 @@ int ggml_mi355x_gpt2_ctx_init(ggml_mi355x_gpt2_model *m, int32_t n_seq, ggml_mi3
     c->logits = m->last ? reinterpret_cast<float *>(take(b_logits)) : nullptr;
     c->kc = reinterpret_cast<float *>(take(b_cache));
     c->vc = reinterpret_cast<float *>(take(b_cache));
+    c->part = reinterpret_cast<float *>(take(b_part));
     if (m->last) {
         c->amax_v = reinterpret_cast<float *>(take(b_amax));
         c->amax_i = reinterpret_cast<int32_t *>(take(b_amax));

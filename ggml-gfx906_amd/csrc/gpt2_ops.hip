@@ -47,22 +47,24 @@ __global__ __launch_bounds__(256) void embed_kernel(const uint8_t *__restrict__ 
     }
 }
 
-// Decode attention, one workgroup of 8 waves per (head, sequence), no cross-workgroup traffic.
-// The p + 1 visible keys (p = pos[s], read on the device, so one captured launch serves every
-// position) are cut into 8 contiguous chunks, one per wave; inside a wave each lane owns keys
-// j = j0 + lane + 64 t and keeps a flash-decoding state of its own (running max m, sum l and
-// the 64-wide o = sum_j exp(s_j - m) V_j in registers). The lane states merge with one
-// butterfly transpose over the wave (64 partial o vectors -> lane d holds o[d]); the 8 wave
-// states merge in LDS. Every K/V row is read once, as 16 dwordx4 per lane, K and V of a pass
-// in flight together. Numerically this is the reference's softmax(K.q * scale) . V
-// (main-sched.cpp:685-735) evaluated in the rescaling order of online softmax.
-__global__ __launch_bounds__(512) void attn_decode_kernel(const float *__restrict__ qkv, float *__restrict__ kc, float *__restrict__ vc,
-                                                          const int32_t *__restrict__ pos, float *__restrict__ out, int n_embd, int n_ctx,
-                                                          float scale) {
+// Decode attention as flash-decoding partials: workgroup (h, s, c) of 4 waves takes split c of
+// the p + 1 visible keys (p = pos[s], read on the device, so one captured launch serves every
+// position), cut into ATTN_SPLITS contiguous chunks and each chunk into 4 wave ranges. Inside a
+// wave every lane owns keys j = j0 + lane + 64 t with its own online-softmax state (running max
+// m, sum l, o = sum_j e^(s_j - m) V_j as 64 registers); one butterfly transpose merges the lanes
+// (lane d ends with o[d]), LDS merges the 4 waves, and the workgroup writes its (m, l, o[64])
+// record. The consumer — the c_proj mat-vec's prologue (mmvq_impl.h attn_merge_load) — merges
+// the ATTN_SPLITS records per head, so the attention output never makes its own HBM round trip
+// and no workgroup waits on another. K and V rows are read once, 16 dwordx4 per lane each, in
+// flight together. Numerically: softmax(K.q * scale) . V of main-sched.cpp:685-735, evaluated in
+// the rescaling order of online softmax.
+__global__ __launch_bounds__(256) void attn_partial_kernel(const float *__restrict__ qkv, float *__restrict__ kc, float *__restrict__ vc,
+                                                           const int32_t *__restrict__ pos, float *__restrict__ part, int n_embd, int n_ctx,
+                                                           float scale) {
     __shared__ float4 qs[HEAD_DIM / 4];
-    __shared__ float wo[8][HEAD_DIM];
-    __shared__ float wm[8], wl[8];
-    const int h = blockIdx.x, s = blockIdx.y;
+    __shared__ float wo[4][HEAD_DIM];
+    __shared__ float wm[4], wl[4];
+    const int h = blockIdx.x, s = blockIdx.y, c = blockIdx.z, n_head = gridDim.x;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int p = min(max(pos[s], 0), n_ctx - 1);
     const int nk = p + 1;
@@ -72,21 +74,23 @@ __global__ __launch_bounds__(512) void attn_decode_kernel(const float *__restric
     float *K = kc + (int64_t)s * n_ctx * n_embd + h * HEAD_DIM;
     float *V = vc + (int64_t)s * n_ctx * n_embd + h * HEAD_DIM;
 
-    // q (pre-scaled) to LDS; the new token's K and V to the cache (the reference's ggml_cpy
-    // into memory_k / memory_v). This launch reads them from qkv, later launches from the cache.
+    // q (pre-scaled) to LDS; split 0 stores the new token's K and V into the cache (the
+    // reference's ggml_cpy into memory_k / memory_v); this launch reads them from qkv
     if (tid < HEAD_DIM / 4) {
         float4 v = reinterpret_cast<const float4 *>(q)[tid];
         v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale;
         qs[tid] = v;
-    } else if (tid >= 64 && tid < 64 + HEAD_DIM / 4) {
+    } else if (c == 0 && tid >= 64 && tid < 64 + HEAD_DIM / 4) {
         const int i = tid - 64;
         reinterpret_cast<float4 *>(K + (int64_t)p * n_embd)[i] = reinterpret_cast<const float4 *>(kcur)[i];
         reinterpret_cast<float4 *>(V + (int64_t)p * n_embd)[i] = reinterpret_cast<const float4 *>(vcur)[i];
     }
     __syncthreads();
 
-    const int chunk = (nk + 7) >> 3;
-    const int j0 = wave * chunk, j1 = min(nk, j0 + chunk);
+    const int chunk = (nk + ATTN_SPLITS - 1) / ATTN_SPLITS;
+    const int c0 = min(nk, c * chunk), c1 = min(nk, c0 + chunk);
+    const int wchunk = (c1 - c0 + 3) >> 2;
+    const int j0 = min(c1, c0 + wave * wchunk), j1 = min(c1, j0 + wchunk);
     float m = -INFINITY, l = 0.f;
     float o[HEAD_DIM];
 #pragma unroll
@@ -110,15 +114,15 @@ __global__ __launch_bounds__(512) void attn_decode_kernel(const float *__restric
         }
         if (live) {
             const float mn = fmaxf(m, sc);
-            const float c = expf(m - mn);                 // 0 on the first key (m = -inf)
+            const float cr = expf(m - mn);                // 0 on the first key (m = -inf)
             const float e = expf(sc - mn);
-            l = l * c + e;
+            l = l * cr + e;
 #pragma unroll
             for (int i = 0; i < HEAD_DIM / 4; ++i) {
-                o[4 * i + 0] = o[4 * i + 0] * c + e * vv[i].x;
-                o[4 * i + 1] = o[4 * i + 1] * c + e * vv[i].y;
-                o[4 * i + 2] = o[4 * i + 2] * c + e * vv[i].z;
-                o[4 * i + 3] = o[4 * i + 3] * c + e * vv[i].w;
+                o[4 * i + 0] = o[4 * i + 0] * cr + e * vv[i].x;
+                o[4 * i + 1] = o[4 * i + 1] * cr + e * vv[i].y;
+                o[4 * i + 2] = o[4 * i + 2] * cr + e * vv[i].z;
+                o[4 * i + 3] = o[4 * i + 3] * cr + e * vv[i].w;
             }
             m = mn;
         }
@@ -138,17 +142,22 @@ __global__ __launch_bounds__(512) void attn_decode_kernel(const float *__restric
     if (wave == 0) {
         float MX = -INFINITY;
 #pragma unroll
-        for (int w = 0; w < 8; ++w) if (wl[w] > 0.f) MX = fmaxf(MX, wm[w]);
+        for (int w = 0; w < 4; ++w) if (wl[w] > 0.f) MX = fmaxf(MX, wm[w]);
         float L = 0.f, O = 0.f;
 #pragma unroll
-        for (int w = 0; w < 8; ++w) {
+        for (int w = 0; w < 4; ++w) {
             if (wl[w] > 0.f) {
                 const float g = expf(wm[w] - MX);
                 L += g * wl[w];
                 O += g * wo[w][lane];
             }
         }
-        out[(int64_t)s * n_embd + h * HEAD_DIM + lane] = O / L;
+        float *rec = part + ((int64_t)(s * n_head + h) * ATTN_SPLITS + c) * ATTN_PART_STRIDE;
+        rec[4 + lane] = O;                                // unnormalized: the consumer divides by sum l
+        if (lane == 0) {
+            rec[0] = MX;
+            rec[1] = L;                                   // 0 for an empty split (skipped by the merge)
+        }
     }
 }
 
@@ -211,10 +220,11 @@ hipError_t gpt2_embed_launch(int wtype, const void *wte, int64_t wte_nb1, const 
     return hipGetLastError();
 }
 
-hipError_t gpt2_attn_launch(const float *qkv, float *kc, float *vc, const int32_t *pos, float *out, int n_seq, int n_head,
+hipError_t gpt2_attn_launch(const float *qkv, float *kc, float *vc, const int32_t *pos, float *part, int n_seq, int n_head,
                             int n_embd, int n_ctx, float scale, hipStream_t st) {
     if (n_embd != n_head * HEAD_DIM) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(attn_decode_kernel, dim3(n_head, n_seq), dim3(512), 0, st, qkv, kc, vc, pos, out, n_embd, n_ctx, scale);
+    hipLaunchKernelGGL(attn_partial_kernel, dim3(n_head, n_seq, ATTN_SPLITS), dim3(256), 0, st, qkv, kc, vc, pos, part, n_embd,
+                       n_ctx, scale);
     return hipGetLastError();
 }
 

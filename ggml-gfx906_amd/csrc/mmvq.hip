@@ -15,6 +15,8 @@ size_t mmvq_lds_bytes(int K, int nc) {
 // lanes per weight row: the width (16 or 64) that leaves the fewest idle slot lanes for this K;
 // ties go to 64 (fewer K iterations per row)
 int mmvq_pick_lpr(int K) {
+    static const int force = getenv("GGML_MI355X_LPR") ? atoi(getenv("GGML_MI355X_LPR")) : 0;   // diagnostics
+    if (force == 16 || force == 64) return force;
     const int nslots = (K + 63) / 64;
     const int u16 = 16 * ((nslots + 15) / 16), u64 = 64 * ((nslots + 63) / 64);
     return u16 < u64 ? 16 : 64;
@@ -94,8 +96,10 @@ static hipError_t launch_type(const MmArgs &a, int nc, int grid_y, int grid_z, i
     return launch_nc<T, 64, 2>(a, nc, grid_y, grid_z, st);
 }
 
-// column-group widths that have kernels (dispatch.cpp splits M into these)
+// column-group widths that have kernels (dispatch.cpp splits M into these); groups of 4 and 8
+// columns hold one activation round in registers, so they serve K <= 4096 only
 bool mmvq_has_nc(int nc) { return nc == 1 || nc == 2 || nc == 3 || nc == 4 || nc == 8; }
+int mmvq_max_k_for_nc(int nc) { return nc >= 4 ? 32 * XR_STRIDE : 64 * XR_STRIDE; }
 bool mmvq_bigk(int K) { MmArgs a{}; a.K = K; return is_bigk(a); }
 
 // plain MUL_MAT: a.M columns in groups of nc (a.M % nc == 0)

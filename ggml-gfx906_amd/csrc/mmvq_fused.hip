@@ -19,9 +19,9 @@ namespace {
 // prepare_only: just raise the instantiation's dynamic-LDS limit. That is not a stream
 // operation and fails inside a hipGraph capture, so mmvq_fused_prepare() runs it for every
 // instantiation before the engine captures a decode step.
-template <int T, int NC, int LPR, int RPW>
+template <int T, int NC, int LPR, int RPW, bool ATTN = false>
 hipError_t fused_one(const MmArgs &a0, int grid_z, hipStream_t st, bool prepare_only = false) {
-    auto kern = mmvq_kernel<T, NC, LPR, RPW, false, false, true, false, true>;
+    auto kern = mmvq_kernel<T, NC, LPR, RPW, false, false, true, false, true, ATTN>;
     static bool attr_set = false;   // per-instantiation
     if (!attr_set) {
         // 160 KB of LDS per CU minus the static arrays (layer-norm and argmax reductions)
@@ -38,26 +38,45 @@ hipError_t fused_one(const MmArgs &a0, int grid_z, hipStream_t st, bool prepare_
     a.n_it = ((a.K + 63) / 64 + LPR - 1) / LPR;
     const int rows_per_group = MMVQ_WAVES * (WAVE / LPR) * RPW;
     const int n_groups = (a.N + rows_per_group - 1) / rows_per_group;
-    const int want = std::max(1, std::min(ARGMAX_SLOTS, 2048 / grid_z));   // EPI_ARGMAX: one partial slot per workgroup
+    // resident-capacity grid (2 workgroups of 8 waves per CU at <= 128 VGPRs): tall matrices
+    // (lm_head) walk their row groups with the prefetch pipeline instead of queueing rounds of
+    // workgroups; EPI_ARGMAX needs one partial slot per workgroup (ARGMAX_SLOTS)
+    static const int target = getenv("GGML_MI355X_FUSED_WGS") ? atoi(getenv("GGML_MI355X_FUSED_WGS")) : 256;
+    const int want = std::max(1, std::min(ARGMAX_SLOTS, target / grid_z));
     dim3 grid(std::min(n_groups, want), 1, grid_z);
     hipLaunchKernelGGL(kern, grid, dim3(MMVQ_THREADS), mmvq_lds_bytes(a.K, NC), st, a);
     return hipGetLastError();
 }
 
-template <int T, int LPR, int RPW>
+template <int T, int LPR, int RPW, bool ATTN = false>
 hipError_t fused_nc(const MmArgs &a, int nc, int grid_z, hipStream_t st) {
     switch (nc) {
-        case 1: return fused_one<T, 1, LPR, RPW>(a, grid_z, st);
-        case 2: return fused_one<T, 2, LPR, RPW>(a, grid_z, st);
-        case 3: return fused_one<T, 3, LPR, RPW>(a, grid_z, st);
-        case 4: return fused_one<T, 4, LPR, RPW>(a, grid_z, st);
-        case 8: return fused_one<T, 8, LPR, RPW>(a, grid_z, st);
+        case 1: return fused_one<T, 1, LPR, RPW, ATTN>(a, grid_z, st);
+        case 2: return fused_one<T, 2, LPR, RPW, ATTN>(a, grid_z, st);
+        case 3: return fused_one<T, 3, LPR, RPW, ATTN>(a, grid_z, st);
+        case 4: return fused_one<T, 4, LPR, RPW, ATTN>(a, grid_z, st);
+        case 8: return fused_one<T, 8, LPR, RPW, ATTN>(a, grid_z, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <int T, int LPR>
+hipError_t fused_nc_attn(const MmArgs &a, int nc, int grid_z, hipStream_t st) {
+    switch (nc) {
+        case 1: return fused_one<T, 1, LPR, 1, true>(a, grid_z, st);
+        case 2: return fused_one<T, 2, LPR, 1, true>(a, grid_z, st);
+        case 3: return fused_one<T, 3, LPR, 1, true>(a, grid_z, st);
         default: return hipErrorInvalidValue;
     }
 }
 
 template <int T>
 hipError_t fused_type(const MmArgs &a, int nc, int rpw, int grid_z, hipStream_t st) {
+    if (a.attn_part != nullptr) {   // c_proj with the attention merge prologue (K = n_embd)
+        if (a.K > 4096) return hipErrorInvalidValue;
+        if (nc > 3) return hipErrorInvalidValue;   // (the merge partials of >3 columns would spill)
+        return mmvq_pick_lpr(a.K) == 16 ? fused_nc_attn<T, 16>(a, nc, grid_z, st) : fused_nc_attn<T, 64>(a, nc, grid_z, st);
+    }
     if (mmvq_pick_lpr(a.K) == 16) return fused_nc<T, 16, 1>(a, nc, grid_z, st);
     return rpw <= 1 ? fused_nc<T, 64, 1>(a, nc, grid_z, st) : fused_nc<T, 64, 2>(a, nc, grid_z, st);
 }
@@ -74,11 +93,23 @@ hipError_t prepare_nc() {
     return e;
 }
 
+template <int T, int LPR>
+hipError_t prepare_attn() {
+    MmArgs a{};
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = fused_one<T, 1, LPR, 1, true>(a, 1, nullptr, true);
+    if (e == hipSuccess) e = fused_one<T, 2, LPR, 1, true>(a, 1, nullptr, true);
+    if (e == hipSuccess) e = fused_one<T, 3, LPR, 1, true>(a, 1, nullptr, true);
+    return e;
+}
+
 template <int T>
 hipError_t prepare_type() {
     hipError_t e = prepare_nc<T, 64, 1>();
     if (e == hipSuccess) e = prepare_nc<T, 64, 2>();
     if (e == hipSuccess) e = prepare_nc<T, 16, 1>();
+    if (e == hipSuccess) e = prepare_attn<T, 16>();
+    if (e == hipSuccess) e = prepare_attn<T, 64>();
     return e;
 }
 

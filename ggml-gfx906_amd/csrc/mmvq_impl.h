@@ -74,10 +74,12 @@ __device__ __forceinline__ XSmem xsmem(uint8_t *smem, int Kpad, int nc) {
 
 constexpr int XR_STRIDE = MMVQ_THREADS / 4;
 
-// Branch-free: the address is clamped into the row and out-of-range values are zeroed by a
-// select, so every lane issues the same loads. (A load under a branch makes the compiler's
-// in-order vmcnt bookkeeping ambiguous and it then waits for ALL outstanding loads — which
-// would include the weight stream.)
+// Branch-free: the address is clamped into the row, so every lane issues the same loads (a
+// load under a branch makes the compiler's in-order vmcnt bookkeeping ambiguous and it then
+// waits for ALL outstanding loads). The loaded values are NOT touched here: out-of-range
+// lanes are zeroed by xblock_mask once the weight stream is in flight too — a select right
+// behind the load would make the compiler wait for the activations before it issues the
+// weights, serializing two memory latencies.
 template <bool XA>
 __device__ __forceinline__ void xblock_load(const MmArgs &a, const uint8_t *xcol, int kb, float4 &v0, float4 &v1) {
     const int k0 = kb * 32 + (threadIdx.x & 3) * 8;
@@ -89,9 +91,54 @@ __device__ __forceinline__ void xblock_load(const MmArgs &a, const uint8_t *xcol
         v0 = make_float4(src[0], src[1], src[2], src[3]);
         v1 = make_float4(src[4], src[5], src[6], src[7]);
     }
-    const bool in = k0 < a.K;
+}
+
+__device__ __forceinline__ void xblock_mask(const MmArgs &a, int kb, float4 &v0, float4 &v1) {
+    const bool in = kb * 32 + (int)(threadIdx.x & 3) * 8 < a.K;
     v0.x = in ? v0.x : 0.f; v0.y = in ? v0.y : 0.f; v0.z = in ? v0.z : 0.f; v0.w = in ? v0.w : 0.f;
     v1.x = in ? v1.x : 0.f; v1.y = in ? v1.y : 0.f; v1.z = in ? v1.z : 0.f; v1.w = in ? v1.w : 0.f;
+}
+
+// FUSE, a.attn_part != nullptr: the 8 activations of this lane are elements k0 .. k0+7 of the
+// attention output of column `col` (one head: k0 % 8 == 0), merged from the ATTN_SPLITS
+// partials by the usual rescaling: O = sum_i e^(m_i - M) o_i / sum_i e^(m_i - M) l_i.
+// Loaded in the issue phase (attn_part_load), combined after the weights are in flight.
+struct AttnPart {
+    float m[ATTN_SPLITS], l[ATTN_SPLITS];
+    float4 o0[ATTN_SPLITS], o1[ATTN_SPLITS];
+};
+
+__device__ __forceinline__ void attn_part_load(const MmArgs &a, int col, int kb, AttnPart &p) {
+    const int k0 = min(kb * 32 + (int)(threadIdx.x & 3) * 8, a.K - 8);
+    const int h = k0 >> 6, d0 = k0 & 63;
+    const float *pb = a.attn_part + (int64_t)(col * a.n_head + h) * ATTN_SPLITS * ATTN_PART_STRIDE;
+#pragma unroll
+    for (int i = 0; i < ATTN_SPLITS; ++i) {
+        const float *q = pb + i * ATTN_PART_STRIDE;
+        p.m[i] = q[0];
+        p.l[i] = q[1];
+        p.o0[i] = *reinterpret_cast<const float4 *>(q + 4 + d0);
+        p.o1[i] = *reinterpret_cast<const float4 *>(q + 8 + d0);
+    }
+}
+
+__device__ __forceinline__ void attn_part_combine(const AttnPart &p, float4 &v0, float4 &v1) {
+    float M = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < ATTN_SPLITS; ++i) M = p.l[i] > 0.f ? fmaxf(M, p.m[i]) : M;
+    float L = 0.f;
+    v0 = make_float4(0.f, 0.f, 0.f, 0.f);
+    v1 = v0;
+#pragma unroll
+    for (int i = 0; i < ATTN_SPLITS; ++i) {
+        const float w = p.l[i] > 0.f ? expf(p.m[i] - M) : 0.f;
+        L += w * p.l[i];
+        v0.x += w * p.o0[i].x; v0.y += w * p.o0[i].y; v0.z += w * p.o0[i].z; v0.w += w * p.o0[i].w;
+        v1.x += w * p.o1[i].x; v1.y += w * p.o1[i].y; v1.z += w * p.o1[i].z; v1.w += w * p.o1[i].w;
+    }
+    const float inv = 1.0f / L;
+    v0 = make_float4(v0.x * inv, v0.y * inv, v0.z * inv, v0.w * inv);
+    v1 = make_float4(v1.x * inv, v1.y * inv, v1.z * inv, v1.w * inv);
 }
 
 template <int T>
@@ -399,59 +446,61 @@ __device__ inline float group_reduce_transpose(float (&v)[V]) {
 // xa/xb[m][r] hold values k0 .. k0+7 of column m, k0 = (kb0 + r*XR_STRIDE)*32 + (tid&3)*8.
 // ------------------------------------------------------------------------------------------
 template <int NC, int PRE>
-__device__ __forceinline__ void layer_norm_cols(const MmArgs &a, int kb0, float4 (&xa)[NC][PRE], float4 (&xb)[NC][PRE]) {
-    __shared__ float red[2][MMVQ_WAVES][NC];
+__device__ __forceinline__ void layer_norm_cols(const MmArgs &a, int kb0, float4 (&xa)[NC][PRE], float4 (&xb)[NC][PRE],
+                                                const float4 (&g)[PRE][2], const float4 (&bb)[PRE][2], const float (&shift)[NC]) {
+    // one pass over the register-resident column: sums of (x - c) and (x - c)^2 with c = the
+    // column's first value (so E[(x-c)^2] - E[x-c]^2 does not cancel), ONE workgroup
+    // reduction. gamma / beta arrived with the activations (issued at kernel start).
+    __shared__ float red[MMVQ_WAVES][NC][2];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    auto sum8 = [](const float4 &p, const float4 &q) { return ((p.x + p.y) + (p.z + p.w)) + ((q.x + q.y) + (q.z + q.w)); };
     float mean[NC], rstd[NC];
 #pragma unroll
     for (int m = 0; m < NC; ++m) {
-        float s = 0.f;
-#pragma unroll
-        for (int r = 0; r < PRE; ++r) s += sum8(xa[m][r], xb[m][r]);
-        s = wave_sum(s);
-        if (lane == 0) red[0][wave][m] = s;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < NC; ++m) {
-        float t = 0.f;
-#pragma unroll
-        for (int w = 0; w < MMVQ_WAVES; ++w) t += red[0][w][m];
-        mean[m] = t / (float)a.K;
-        float s = 0.f;
+        const float c = shift[m];
+        float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int r = 0; r < PRE; ++r) {
             const int k0 = (kb0 + r * XR_STRIDE) * 32 + (threadIdx.x & 3) * 8;
             if (k0 < a.K) {
-                const float4 p = xa[m][r], q = xb[m][r];
-                const float mu = mean[m];
-                s += ((p.x - mu) * (p.x - mu) + (p.y - mu) * (p.y - mu)) + ((p.z - mu) * (p.z - mu) + (p.w - mu) * (p.w - mu));
-                s += ((q.x - mu) * (q.x - mu) + (q.y - mu) * (q.y - mu)) + ((q.z - mu) * (q.z - mu) + (q.w - mu) * (q.w - mu));
+                const float v[8] = {xa[m][r].x - c, xa[m][r].y - c, xa[m][r].z - c, xa[m][r].w - c,
+                                    xb[m][r].x - c, xb[m][r].y - c, xb[m][r].z - c, xb[m][r].w - c};
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    s1 += v[i];
+                    s2 = __builtin_fmaf(v[i], v[i], s2);
+                }
             }
         }
-        s = wave_sum(s);
-        if (lane == 0) red[1][wave][m] = s;
+        s1 = wave_sum(s1);
+        s2 = wave_sum(s2);
+        if (lane == 0) {
+            red[wave][m][0] = s1;
+            red[wave][m][1] = s2;
+        }
     }
     __syncthreads();
 #pragma unroll
     for (int m = 0; m < NC; ++m) {
-        float t = 0.f;
+        float t1 = 0.f, t2 = 0.f;
 #pragma unroll
-        for (int w = 0; w < MMVQ_WAVES; ++w) t += red[1][w][m];
-        rstd[m] = 1.0f / sqrtf(t / (float)a.K + a.ln_eps);
+        for (int w = 0; w < MMVQ_WAVES; ++w) {
+            t1 += red[w][m][0];
+            t2 += red[w][m][1];
+        }
+        const float d = t1 / (float)a.K;                 // E[x - c]
+        mean[m] = shift[m] + d;
+        const float var = fmaxf(t2 / (float)a.K - d * d, 0.f);
+        rstd[m] = 1.0f / sqrtf(var + a.ln_eps);
     }
 #pragma unroll
     for (int r = 0; r < PRE; ++r) {
         const int k0 = (kb0 + r * XR_STRIDE) * 32 + (threadIdx.x & 3) * 8;
-        const int kc = min(k0, a.K - 8);
-        const float4 g0 = reinterpret_cast<const float4 *>(a.ln_g + kc)[0], g1 = reinterpret_cast<const float4 *>(a.ln_g + kc)[1];
-        const float4 b0 = reinterpret_cast<const float4 *>(a.ln_b + kc)[0], b1 = reinterpret_cast<const float4 *>(a.ln_b + kc)[1];
         const bool in = k0 < a.K;
+        const float4 g0 = g[r][0], g1 = g[r][1], b0 = bb[r][0], b1 = bb[r][1];
 #pragma unroll
         for (int m = 0; m < NC; ++m) {
             const float mu = mean[m], rs = rstd[m];
-            auto f = [&](float x, float g, float b) { return in ? (x - mu) * rs * g + b : 0.f; };
+            auto f = [&](float x, float gg, float b) { return in ? (x - mu) * rs * gg + b : 0.f; };
             float4 &p = xa[m][r], &q = xb[m][r];
             p = make_float4(f(p.x, g0.x, b0.x), f(p.y, g0.y, b0.y), f(p.z, g0.z, b0.z), f(p.w, g0.w, b0.w));
             q = make_float4(f(q.x, g1.x, b1.x), f(q.y, g1.y, b1.y), f(q.z, g1.z, b1.z), f(q.w, g1.w, b1.w));
@@ -516,7 +565,7 @@ __device__ __forceinline__ void argmax_epilogue(const MmArgs &a, float bv, int b
 // kernel: n_it comes from the host), and a workgroup with a single unit — the single-matrix
 // decode shapes — takes a straight-line path with no prefetch.
 // ------------------------------------------------------------------------------------------
-template <int T, int NC, int LPR, int RPW, bool IDS, bool RAG, bool XA, bool BIGK, bool FUSE = false>
+template <int T, int NC, int LPR, int RPW, bool IDS, bool RAG, bool XA, bool BIGK, bool FUSE = false, bool ATTN = false>
 __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr int NX = XdCount<T>::n;
@@ -559,6 +608,10 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
     const int n_groups = (a.N + ROWS_PER_GROUP - 1) / ROWS_PER_GROUP;
     const bool stamp = a.stamps != nullptr && threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
     if (stamp) { a.stamps[blockIdx.x * 8 + 0] = __builtin_amdgcn_s_memrealtime(); a.stamps[blockIdx.x * 8 + 4] = __builtin_amdgcn_s_memtime(); }
+    // diagnostics: per-wave stamps (lane 0 of every wave of the stamped grid row)
+    const bool wstamp = a.stamps != nullptr && (threadIdx.x & 63) == 0 && blockIdx.y == 0 && blockIdx.z == 0;
+    unsigned long long *const wst = a.stamps + 4 * 65536 + ((int64_t)blockIdx.x * MMVQ_WAVES + (threadIdx.x >> 6)) * 4;
+    if (wstamp) wst[0] = __builtin_amdgcn_s_memrealtime();
 
     // unit (g, it): rows g * ROWS_PER_GROUP + wrow + r, slot sl + it * LPR (clamped: dead
     // lanes / rows read valid memory and are masked out of the sums)
@@ -569,34 +622,118 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
         for (int r = 0; r < RPW; ++r) f[r].template load<RAG>(wmat + (int64_t)min(r0 + r, a.N - 1) * a.nb01, s, nblk);
     };
 
+    // fused epilogue operands of this lane's output (bias[row], and dst[row] for the residual
+    // add), loaded with the weights of the unit so the epilogue waits on nothing. Lanes that
+    // store nothing, and launches without bias / residual, re-read valid addresses.
+    constexpr int ESHIFT = Log2<LPR>::v - Log2<V>::v;
+    const int eidx = sl >> ESHIFT;                               // this lane's (row, column) slot
+    const int er = min(eidx, RPW * NC - 1) / NC, em = min(eidx, RPW * NC - 1) % NC;
+    struct EpiOps { float bias, resid; };
+    auto load_epi = [&](int gg) -> EpiOps {
+        const int row = min(gg * ROWS_PER_GROUP + wrow + er, a.N - 1);
+        const float *bp = a.bias != nullptr ? a.bias + row : reinterpret_cast<const float *>(dcol0 + (int64_t)em * a.nb1) + row;
+        EpiOps e;
+        e.bias = *bp;
+        e.resid = reinterpret_cast<const float *>(dcol0 + (int64_t)em * a.nb1)[row];
+        return e;
+    };
+
     // ---- activation loads of the first round first (L2/MALL hits), then the weight stream of
     // unit 0, so the quantization waits only for the activations (vmcnt is in-order) while the
     // weights stay in flight.
     // up to two rounds (K <= 8192) are preloaded; BIGK kernels loop over the rest
     const int kb0 = threadIdx.x >> 2;
-    constexpr int PRE = BIGK ? 1 : 2;
-    const bool round2 = !BIGK && nxblk > XR_STRIDE;   // uniform: skip the second round for K <= 4096
+    // activation rounds held in registers: 2 (K <= 8192) for narrow column groups; wide groups
+    // (NC >= 4) keep one round (K <= 4096, mmvq_max_k_for_nc) so their registers stay unspilled
+    constexpr int PRE = (BIGK || NC >= 4) ? 1 : 2;
     float4 xa[NC][PRE], xb[NC][PRE];
+    // FUSE + attn_part: the activations are merged attention partials (K = n_embd <= 4096:
+    // one round); their loads are issued here and combined after the weights
+    // (80 registers of partials per column: held across the weight issue for NC <= 2 only;
+    // wider column groups merge each column before the weights are issued)
+    // ATTN kernels only (a template flag: the partial registers would otherwise weigh on every
+    // fused instantiation's occupancy)
+    static_assert(!ATTN || (FUSE && !BIGK), "attention merge is a fused-prologue variant");
+    constexpr bool AP_PRE = ATTN && NC <= 2;
+    constexpr int NAP = AP_PRE ? NC : 1;
+    [[maybe_unused]] AttnPart ap[NAP];
+    constexpr bool attn = ATTN;
+    if constexpr (attn) {
+        if constexpr (AP_PRE) {
 #pragma unroll
-    for (int m = 0; m < NC; ++m) {
-        xblock_load<XA>(a, xcol0 + (int64_t)m * a.nb11, kb0, xa[m][0], xb[m][0]);
-        if constexpr (PRE > 1) {
-            if (round2) xblock_load<XA>(a, xcol0 + (int64_t)m * a.nb11, kb0 + XR_STRIDE, xa[m][1], xb[m][1]);
-            else xa[m][1] = xb[m][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int m = 0; m < NAP; ++m) attn_part_load(a, (int)blockIdx.z * NC + m, kb0, ap[m]);
+        } else {
+#pragma unroll
+            for (int m = 0; m < NC; ++m) {
+                attn_part_load(a, (int)blockIdx.z * NC + m, kb0, ap[0]);
+                attn_part_combine(ap[0], xa[m][0], xb[m][0]);
+                if constexpr (PRE > 1) xa[m][1] = xb[m][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < NC; ++m) {
+#pragma unroll
+            for (int r = 0; r < PRE; ++r) xblock_load<XA>(a, xcol0 + (int64_t)m * a.nb11, kb0 + r * XR_STRIDE, xa[m][r], xb[m][r]);
         }
     }
+
+    // fused prologue operands, issued with the activations: gamma / beta of this lane's 8
+    // values per round and each column's first value (the layer norm's shift). Without a layer
+    // norm the loads re-read the activations (valid addresses, no branch around a load).
+    // (wide column groups hold NC x PRE x 8 activations already: they load gamma / beta after
+    // the weights instead of keeping 32 more registers live across the weight issue)
+    [[maybe_unused]] float4 lg[PRE][2], lb[PRE][2];
+    [[maybe_unused]] float lshift[NC];
+    auto load_ln = [&]() {
+        const bool ln = a.ln_g != nullptr;
+        const float *gp = ln ? a.ln_g : reinterpret_cast<const float *>(a.x);
+        const float *bp = ln ? a.ln_b : reinterpret_cast<const float *>(a.x);
+#pragma unroll
+        for (int r = 0; r < PRE; ++r) {
+            const int kc = min((kb0 + r * XR_STRIDE) * 32 + (int)(threadIdx.x & 3) * 8, a.K - 8);
+            lg[r][0] = reinterpret_cast<const float4 *>(gp + kc)[0];
+            lg[r][1] = reinterpret_cast<const float4 *>(gp + kc)[1];
+            lb[r][0] = reinterpret_cast<const float4 *>(bp + kc)[0];
+            lb[r][1] = reinterpret_cast<const float4 *>(bp + kc)[1];
+        }
+#pragma unroll
+        for (int m = 0; m < NC; ++m) lshift[m] = *reinterpret_cast<const float *>(xcol0 + (int64_t)m * a.nb11);
+    };
+    if constexpr (FUSE && NC <= 2) load_ln();
 
     Frag<T> fa[RPW], fb[RPW];
     int g = blockIdx.x, it = 0;                   // the unit being computed (grid.x <= n_groups)
     load_unit(fa, g, it);
-    __builtin_amdgcn_sched_barrier(0);
+    [[maybe_unused]] EpiOps ea{}, eb{};
+    if constexpr (FUSE) ea = load_epi(g);
+    __builtin_amdgcn_sched_barrier(0);            // ---- everything above is in flight; consume below
+
+    if constexpr (AP_PRE) {
+#pragma unroll
+        for (int m = 0; m < NAP; ++m) {
+            attn_part_combine(ap[m], xa[m][0], xb[m][0]);
+            if constexpr (PRE > 1) xa[m][1] = xb[m][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < NC; ++m)
+#pragma unroll
+        for (int r = 0; r < PRE; ++r) xblock_mask(a, kb0 + r * XR_STRIDE, xa[m][r], xb[m][r]);
+    if (wstamp) {   // diagnostics: the activations have arrived (the mask consumed them)
+        __builtin_amdgcn_sched_barrier(0);
+        float probe = xa[0][0].x + xb[0][PRE - 1].w;
+        asm volatile("" : "+v"(probe));
+        wst[1] = __builtin_amdgcn_s_memrealtime() + (probe == 12345.f);
+    }
 
     // fused prologue: layer norm of each column over its K values (ggml_norm, reference
     // src/ggml-cpu/ops.cpp ggml_compute_forward_norm_f32: mean, then mean of squared
     // deviations, scale 1/sqrt(var + eps)), then * g + b (ggml_mul / ggml_add). The whole
     // column is already in registers (K <= 8192, no BIGK); out-of-range values are zero.
     if constexpr (FUSE) {
-        if (a.ln_g != nullptr) layer_norm_cols<NC, PRE>(a, kb0, xa, xb);
+        if constexpr (NC > 2) load_ln();
+        if (a.ln_g != nullptr) layer_norm_cols<NC, PRE>(a, kb0, xa, xb, lg, lb, lshift);
     }
 
 #pragma unroll
@@ -614,11 +751,13 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
 #pragma unroll
             for (int m = 0; m < NC; ++m) {
                 xblock_load<XA>(a, xcol0 + (int64_t)m * a.nb11, kb, xa[m][0], xb[m][0]);
+                xblock_mask(a, kb, xa[m][0], xb[m][0]);
                 xblock_store<T>(Kpad, kb, xa[m][0], xb[m][0], sm.xq + (size_t)m * Kpad, sm.xd + m * nxblk,
                                 sm.xs + m * nxblk, sm.x16 + m * 2 * nxblk);
             }
         }
     }
+    if (wstamp) wst[2] = __builtin_amdgcn_s_memrealtime();   // quantized, at the barrier
     __syncthreads();
     if (stamp) a.stamps[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
 
@@ -628,7 +767,7 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
     float best_v = -INFINITY;                     // EPI_ARGMAX: this lane's best stored value
     int best_i = 0x7fffffff, best_c = -1;
 
-    auto compute_unit = [&](const Frag<T> (&f)[RPW], int gg, int itt) {
+    auto compute_unit = [&](const Frag<T> (&f)[RPW], int gg, int itt, const EpiOps &eo) {
         const int s_raw = sl + itt * LPR;
         const int s = min(s_raw, nslots - 1);
         const float live = s_raw < nslots ? 1.f : 0.f;
@@ -675,9 +814,10 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
                     float v = sum;
                     if constexpr (FUSE) {
                         // fused epilogue, in ggml's node order: + bias, gelu, + residual
-                        if (a.bias != nullptr) v += a.bias[r0 + r];
+                        // (operands prefetched with the unit's weights: eo)
+                        if (a.bias != nullptr) v += eo.bias;
                         if (a.epi & EPI_GELU) v = gelu_ggml(v);
-                        if (a.epi & EPI_RESID) v += *out;
+                        if (a.epi & EPI_RESID) v += eo.resid;
                         if (a.epi & EPI_ARGMAX) {
                             if (v > best_v || best_c < 0) { best_v = v; best_i = r0 + r; }   // rows ascend per lane
                             best_c = m;
@@ -696,7 +836,7 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
     if (nit == n_it) { nit = 0; ng += gridDim.x; }
     if (ng >= n_groups) {
         // single unit per workgroup (e.g. a 4096-row matrix at K <= 4096): no prefetch at all
-        compute_unit(fa, g, it);
+        compute_unit(fa, g, it, ea);
     } else {
         // prefetches are unconditional (clamped to the current unit once the walk ends: a
         // repeat of addresses already in flight, served on-chip) so the load stream never sits
@@ -706,15 +846,17 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
         for (;;) {
             bool more = ng < n_groups;
             load_unit(fb, more ? ng : g, more ? nit : it);
+            if constexpr (FUSE) eb = load_epi(more ? ng : g);
             __builtin_amdgcn_sched_barrier(0);
-            compute_unit(fa, g, it);
+            compute_unit(fa, g, it, ea);
             if (!more) break;
             g = ng; it = nit;
             if (++nit == n_it) { nit = 0; ng += gridDim.x; }
             more = ng < n_groups;
             load_unit(fa, more ? ng : g, more ? nit : it);
+            if constexpr (FUSE) ea = load_epi(more ? ng : g);
             __builtin_amdgcn_sched_barrier(0);
-            compute_unit(fb, g, it);
+            compute_unit(fb, g, it, eb);
             if (!more) break;
             g = ng; it = nit;
             if (++nit == n_it) { nit = 0; ng += gridDim.x; }

@@ -14,6 +14,10 @@ enum { EPI_GELU = 1, EPI_RESID = 2, EPI_ARGMAX = 4 };
 // EPI_ARGMAX: per-workgroup partial argmax slots per output column (GPT-2 greedy sampling)
 constexpr int ARGMAX_SLOTS = 2048;
 
+// decode attention: key splits per (sequence, head) and the partial record (m, l, o[64])
+constexpr int ATTN_SPLITS = 4;
+constexpr int ATTN_PART_STRIDE = 4 + 64;   // m, l, 2 pad (16-B aligned o), o[64]
+
 struct MmArgs {
     const uint8_t *w;      // src0, quantized rows (nb00 == block bytes)
     int64_t nb01, nb02, nb03;
@@ -47,6 +51,11 @@ struct MmArgs {
     //     produced, per column c, to amax_v / amax_i [c * ARGMAX_SLOTS + blockIdx.x]
     float *amax_v;
     int32_t *amax_i;
+    //   attn_part != nullptr: the activations are the decode attention output, merged here
+    //     from ATTN_SPLITS flash-decoding partials per (column, head) (gpt2_ops.hip):
+    //     part[((col * n_head + h) * ATTN_SPLITS + i) * ATTN_PART_STRIDE + {0: m, 1: l, 4..67: o}]
+    const float *attn_part;
+    int n_head;
     int fused;
     // diagnostics (GGML_MI355X_STAMPS): per-workgroup s_memrealtime stamps, or nullptr
     unsigned long long *stamps;
