@@ -38,6 +38,8 @@ for step in "$@"; do
         profsingles) run profsingles 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsingles -o run -- python scripts/prof_singles.py ;;
         profgpt2) run profgpt2 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profgpt2 -o run -- python scripts/gpt2_bench.py 1 256 1 ;;
         gpt2b) run gpt2b 300 python scripts/gpt2_bench.py 1 256 1 ;;
+        mmq)   run mmq 300 python scripts/mmq_bench.py ;;
+        profmmq) run profmmq 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profmmq -o run -- python scripts/mmq_bench.py q8_0:4096:4096:512 q4_K:4096:4096:512 ;;
         *) echo "unknown step $step" ;;
     esac
 done

@@ -79,7 +79,10 @@ def test_mul_mat_vs_reference(mm, r):
         cs = G.load_bin(r["colsums"], np.float64).reshape(-1, 2)
         c64 = cols.astype(np.float64)
         norm = np.sqrt(cs[:, 1])
-        assert np.all(np.abs(c64.sum(1) - cs[:, 0]) <= 1e-3 * norm), "column sums"
+        # independent per-element errors at the sample's NMSE give a column-sum error with
+        # std sqrt(nmse) * norm; allow 6 sigma (a wrong or missing tile is off by ~norm)
+        tol = 6 * np.sqrt(max(e_ref, 1e-6)) * norm
+        assert np.all(np.abs(c64.sum(1) - cs[:, 0]) <= tol), "column sums"
         assert np.all(np.abs((c64 ** 2).sum(1) / cs[:, 1] - 1) <= 1e-3), "column sums of squares"
     else:
         assert got.size == want.size

@@ -1,0 +1,45 @@
+"""The mat-mat path's f16 range guard (csrc/mmq.hip, mmq_wave_kernel): weights are decoded to
+f16 inside the kernel, so rows whose block scales reach 1.0 (|w| in the hundreds or more, far
+outside what quantized LLM weights hold) take an exact fp32 recomputation instead of
+overflowing. Checked against the CPU oracle on rows mixing ordinary and huge scales, at token
+counts that select the register-decode tile (M <= 64)."""
+import numpy as np
+import pytest
+
+import golden_cases as G
+import qref
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mm():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import mi355x_qmm as M
+    M.build()
+    return M
+
+
+@pytest.mark.parametrize("t,big", [(qref.Q8_0, 7.0e4), (qref.Q4_K, 2.0e3), (qref.Q4_0, 1.0e5)])
+@pytest.mark.parametrize("M", [16, 40])
+def test_huge_scales_match_oracle(mm, t, big, M):
+    K, N = 512, 160
+    f = qref.fill_uniform(N * K, 77).reshape(N, K)
+    f[5::7] *= big                      # every 7th row: block scales >= 1.0
+    w = qref.quantize(t, f.reshape(-1), n_per_row=K)
+    x = qref.fill_uniform(M * K, 78)
+    a = G.Operand(t, w, [K, N, 1, 1], qref.contiguous_nb(t, [K, N, 1, 1]))
+    b = G.Operand(qref.F32, x.view(np.uint8).copy(), [K, M, 1, 1], qref.contiguous_nb(qref.F32, [K, M, 1, 1]))
+    import test_gpu_parity as T
+    got = T.run_mul_mat(mm, a, b, [N, M, 1, 1])
+    want = G.oracle_mul_mat(a, b, [N, M, 1, 1])
+    assert np.all(np.isfinite(got))
+    assert qref.nmse(got, want) <= 5e-4
+    # the ordinary rows stay as accurate as without the huge ones
+    keep = np.ones(N, bool)
+    keep[5::7] = False
+    g2, w2 = got.reshape(M, N)[:, keep], want.reshape(M, N)[:, keep]
+    assert qref.nmse(g2, w2) <= 5e-4
