@@ -938,10 +938,14 @@ template <> struct Deq32<T_Q6_K> {   // super-block 210 B: ql 128, qh 64, int8 s
 // MFMAs run. The groups' accumulators are summed through LDS at the end.
 // Activation run sums (for the offset MFMA) are laid out per group and per 4 of the group's
 // steps: record (step / 8) * 2 + (step & 1) of 16 f16, slot fh * 8 + 2 * ((step % 8) / 2) + hi/lo.
+// Split-K (few tokens, so few token tiles): blockIdx.z = slice * n_split + split; split s runs
+// phases [s * split_np, (s + 1) * split_np) and, with n_split > 1, writes its scaled partial tile
+// to part[split][slice][token][row] for mmq_split_reduce.
 template <int T, int TN, bool IDS, bool STAMP = false>
 __global__ __launch_bounds__(512) void mmq_wave_kernel(const MmArgs a, const _Float16 *__restrict__ x16,
                                                        const _Float16 *__restrict__ xsum, const float *__restrict__ xinv,
-                                                       int Kpad, uint32_t w_extent, const MoeMap moe) {
+                                                       int Kpad, uint32_t w_extent, const MoeMap moe, int n_split,
+                                                       int split_np, float *__restrict__ part) {
     constexpr int BN = 32 * TN;                 // tokens per workgroup
     constexpr int XB = BN * 128;                // bytes of one activation slot (BK = 64 f16)
     constexpr int V = TN;                       // 1-KiB activation pieces per wave per step
@@ -952,7 +956,7 @@ __global__ __launch_bounds__(512) void mmq_wave_kernel(const MmArgs a, const _Fl
     __shared__ __align__(16) uint8_t lds[6 * XB];   // [group][3 slots][XB]
     __shared__ uint32_t g1_bad[4];
 
-    const int slice = blockIdx.z;
+    const int slice = blockIdx.z / n_split, split = blockIdx.z % n_split;
     const int i12 = slice % a.ne12, i13 = slice / a.ne12;
     const uint8_t *wmat;
     const _Float16 *xs, *ss;
@@ -992,7 +996,8 @@ __global__ __launch_bounds__(512) void mmq_wave_kernel(const MmArgs a, const _Fl
     const int fr = lane & 31, fh = lane >> 5;
     const int row = blockIdx.x * 128 + 32 * wq + fr;
     const uint32_t wrow = (uint32_t)row * (uint32_t)a.nb01;   // rows >= N read as zeros
-    const int np = Kpad / (2 * MQ_BK);                           // phases (steps per group)
+    const int p0 = split * split_np;                             // first phase of this split
+    const int np = min(split_np, Kpad / (2 * MQ_BK) - p0);       // phases (steps per group)
     uint8_t *const xslot = lds + grp * 3 * XB;
     uint64_t st_seg[5] = {0, 0, 0, 0, 0}, st_t = 0, st_start = 0;
     auto stamp = [&](int seg) {
@@ -1014,7 +1019,7 @@ __global__ __launch_bounds__(512) void mmq_wave_kernel(const MmArgs a, const _Fl
         const int c = (lane & 7) ^ ((r >> 1) & 7);
         x_off[v] = ((uint32_t)(tok0 + r) * (uint32_t)Kpad + (uint32_t)c * 8u) * 2u;
     }
-    auto step_of = [&](int p) { return 2 * p + grp; };
+    auto step_of = [&](int p) { return 2 * (p0 + p) + grp; };
     // a K tail (32-block types, K % 128 != 0) re-reads the row's last block: its codes meet zero
     // activations and zero run sums, so it adds exactly 0
     auto at_w = [&](Deq32<T> &w, int p) { w.at(wrow, min(step_of(p) * MQ_BK + 32 * fh, a.K - 32)); };
@@ -1028,10 +1033,11 @@ __global__ __launch_bounds__(512) void mmq_wave_kernel(const MmArgs a, const _Fl
     };
     // run-sum fragment of this group's window w (phases 4w .. 4w+3) for token tile j
     u32x4 sfrag[TN];
-    auto load_sums = [&](int w) {
+    auto load_sums = [&](int w) {   // w counts this split's windows (p0 is a multiple of MQ_WIN)
+        const uint32_t rec = (uint32_t)(2 * (w + p0 / MQ_WIN) + grp);
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-            sfrag[j] = bl128(sr, ((uint32_t)(tok0 + 32 * j + fr) * (uint32_t)nrec + (uint32_t)(2 * w + grp)) * 32u + 16u * fh);
+            sfrag[j] = bl128(sr, ((uint32_t)(tok0 + 32 * j + fr) * (uint32_t)nrec + rec) * 32u + 16u * fh);
     };
 
     float16v acc[TN];
@@ -1197,7 +1203,7 @@ __global__ __launch_bounds__(512) void mmq_wave_kernel(const MmArgs a, const _Fl
         // what quantized weights hold). Activations are read back in their stored order pi.
         for (int j = 0; j < TN; ++j)
             for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-        for (int kr = 0; kr < a.K; kr += 32) {
+        for (int kr = p0 * 2 * MQ_BK; kr < min(a.K, (p0 + np) * 2 * MQ_BK); kr += 32) {   // this split's K
             Deq32<T> w;
             w.at(wrow, kr);
             for (int q = 0; q < NLW; ++q) w.part(wr, q);
@@ -1230,6 +1236,8 @@ __global__ __launch_bounds__(512) void mmq_wave_kernel(const MmArgs a, const _Fl
                     if constexpr (IDS) {
                         const int pair = moe.pos_pair[tok];
                         drow = dmat + (int64_t)(pair % moe.n_used) * a.nb1 + (int64_t)(pair / moe.n_used) * a.nb2;
+                    } else if (n_split > 1) {
+                        drow = reinterpret_cast<uint8_t *>(part + (((int64_t)split * gridDim.z / n_split + slice) * a.M + tok) * a.N);
                     } else {
                         drow = dmat + (int64_t)tok * a.nb1;
                     }
@@ -1264,27 +1272,44 @@ static void launch_tile(const MmArgs &a, const _Float16 *x16, const float *xinv,
         hipLaunchKernelGGL((mmq_kernel<T, BM, BN, false, false, NW, TM>), grid, dim3(NW * 64), 0, st, a, x16, xinv, Kpad, w_extent, none);
 }
 
+// dst[slice][token][row] = sum of the split-K partial tiles (mmq_wave_kernel with n_split > 1)
+__global__ __launch_bounds__(256) void mmq_split_reduce(const MmArgs a, const float *__restrict__ part, int n_split,
+                                                        int slices) {
+    const int64_t per_slice = (int64_t)a.M * a.N;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= per_slice * slices) return;
+    const int slice = (int)(i / per_slice);
+    const int64_t rem = i % per_slice;
+    const int tok = (int)(rem / a.N), row = (int)(rem % a.N);
+    float v = 0.f;
+    for (int s = 0; s < n_split; ++s) v += part[((int64_t)s * slices + slice) * per_slice + rem];
+    const int i12 = slice % a.ne12, i13 = slice / a.ne12;
+    reinterpret_cast<float *>(a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3 + (int64_t)tok * a.nb1)[row] = v;
+}
+
 template <int T, int TN>
 static void launch_wave(const MmArgs &a, const _Float16 *x16, const _Float16 *xsum, const float *xinv, int Kpad, int slices,
-                        hipStream_t st) {
-    const dim3 grid((a.N + 127) / 128, (a.M + 32 * TN - 1) / (32 * TN), slices);
+                        int n_split, int split_np, float *part, hipStream_t st) {
+    const dim3 grid((a.N + 127) / 128, (a.M + 32 * TN - 1) / (32 * TN), slices * n_split);
     // dword-aligned windows may end 2 bytes past the last block: round the range up to a dword
     // (buffer range checks are per dword; the extra bytes never leave the last page)
     const uint32_t w_extent = (uint32_t)(((int64_t)(a.N - 1) * a.nb01 + row_bytes(T, a.K) + 3) & ~(int64_t)3);
     const MoeMap none{};
     if (a.stamps && (size_t)grid.x * grid.y * grid.z * 64 <= 8 * 65536)
-        hipLaunchKernelGGL((mmq_wave_kernel<T, TN, false, true>), grid, dim3(512), 0, st, a, x16, xsum, xinv, Kpad, w_extent, none);
+        hipLaunchKernelGGL((mmq_wave_kernel<T, TN, false, true>), grid, dim3(512), 0, st, a, x16, xsum, xinv, Kpad, w_extent, none,
+                           n_split, split_np, part);
     else
-        hipLaunchKernelGGL((mmq_wave_kernel<T, TN, false, false>), grid, dim3(512), 0, st, a, x16, xsum, xinv, Kpad, w_extent, none);
+        hipLaunchKernelGGL((mmq_wave_kernel<T, TN, false, false>), grid, dim3(512), 0, st, a, x16, xsum, xinv, Kpad, w_extent, none,
+                           n_split, split_np, part);
 }
 
 template <int T>
 static void launch_wave_tn(int tile, const MmArgs &a, const _Float16 *x16, const _Float16 *xsum, const float *xinv, int Kpad,
-                           int slices, hipStream_t st) {
+                           int slices, int n_split, int split_np, float *part, hipStream_t st) {
     switch (tile) {
-        case 10: launch_wave<T, 1>(a, x16, xsum, xinv, Kpad, slices, st); break;
-        case 12: launch_wave<T, 4>(a, x16, xsum, xinv, Kpad, slices, st); break;
-        default: launch_wave<T, 2>(a, x16, xsum, xinv, Kpad, slices, st); break;
+        case 10: launch_wave<T, 1>(a, x16, xsum, xinv, Kpad, slices, n_split, split_np, part, st); break;
+        case 12: launch_wave<T, 4>(a, x16, xsum, xinv, Kpad, slices, n_split, split_np, part, st); break;
+        default: launch_wave<T, 2>(a, x16, xsum, xinv, Kpad, slices, n_split, split_np, part, st); break;
     }
 }
 
@@ -1334,24 +1359,42 @@ hipError_t mmq_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratc
     const bool wave = tile >= 10;
     const int kq = wave ? 2 * MQ_BK : MQ_BK;   // the wave kernel's two K-groups take step pairs
     const int Kpad = (a.K + kq - 1) / kq * kq;
+    // split-K for the wave kernel: workgroups for every CU, splits of whole run-sum windows
+    // (MQ_WIN phases = 512 k each)
+    int n_split = 1, split_np = Kpad / kq;
+    if (wave) {
+        const int tn = tile == 10 ? 1 : tile == 12 ? 4 : 2;
+        const int64_t wgs = (int64_t)((a.N + 127) / 128) * ((a.M + 32 * tn - 1) / (32 * tn)) * slices;
+        const int windows = (split_np + MQ_WIN - 1) / MQ_WIN;
+        while (wgs * n_split < 256 && windows >= 2 * n_split) n_split *= 2;
+        split_np = (windows + n_split - 1) / n_split * MQ_WIN;
+        n_split = (Kpad / kq + split_np - 1) / split_np;
+    }
     const size_t x16_bytes = ((size_t)slices * a.M * Kpad * sizeof(_Float16) + 255) & ~(size_t)255;
     const size_t sum_bytes = wave ? (((size_t)slices * a.M * ((Kpad + 511) / 512 * 2) * 32 + 255) & ~(size_t)255) : 0;
+    const size_t part_bytes = n_split > 1 ? (((size_t)n_split * slices * a.M * a.N * sizeof(float) + 255) & ~(size_t)255) : 0;
     const size_t inv_bytes = (size_t)slices * a.M * sizeof(float);
-    uint8_t *buf = static_cast<uint8_t *>(scratch.get(x16_bytes + sum_bytes + inv_bytes, st));
+    uint8_t *buf = static_cast<uint8_t *>(scratch.get(x16_bytes + sum_bytes + part_bytes + inv_bytes, st));
     if (!buf) return hipErrorOutOfMemory;
     _Float16 *x16 = reinterpret_cast<_Float16 *>(buf);
     _Float16 *xsum = reinterpret_cast<_Float16 *>(buf + x16_bytes);
-    float *xinv = reinterpret_cast<float *>(buf + x16_bytes + sum_bytes);
+    float *part = reinterpret_cast<float *>(buf + x16_bytes + sum_bytes);
+    float *xinv = reinterpret_cast<float *>(buf + x16_bytes + sum_bytes + part_bytes);
     const dim3 cgrid(a.M, slices);
     if (wave) {
         hipLaunchKernelGGL(mmq_convert_x<true>, cgrid, dim3(64), 0, st, a, x16, xinv, Kpad, (const int *)nullptr, a.M, xsum);
         switch (type) {
-            case T_Q4_0: launch_wave_tn<T_Q4_0>(tile, a, x16, xsum, xinv, Kpad, slices, st); break;
-            case T_Q8_0: launch_wave_tn<T_Q8_0>(tile, a, x16, xsum, xinv, Kpad, slices, st); break;
-            case T_Q4_K: launch_wave_tn<T_Q4_K>(tile, a, x16, xsum, xinv, Kpad, slices, st); break;
-            case T_Q5_K: launch_wave_tn<T_Q5_K>(tile, a, x16, xsum, xinv, Kpad, slices, st); break;
-            case T_Q6_K: launch_wave_tn<T_Q6_K>(tile, a, x16, xsum, xinv, Kpad, slices, st); break;
+            case T_Q4_0: launch_wave_tn<T_Q4_0>(tile, a, x16, xsum, xinv, Kpad, slices, n_split, split_np, part, st); break;
+            case T_Q8_0: launch_wave_tn<T_Q8_0>(tile, a, x16, xsum, xinv, Kpad, slices, n_split, split_np, part, st); break;
+            case T_Q4_K: launch_wave_tn<T_Q4_K>(tile, a, x16, xsum, xinv, Kpad, slices, n_split, split_np, part, st); break;
+            case T_Q5_K: launch_wave_tn<T_Q5_K>(tile, a, x16, xsum, xinv, Kpad, slices, n_split, split_np, part, st); break;
+            case T_Q6_K: launch_wave_tn<T_Q6_K>(tile, a, x16, xsum, xinv, Kpad, slices, n_split, split_np, part, st); break;
             default: return hipErrorInvalidValue;
+        }
+        if (n_split > 1) {
+            const int64_t n = (int64_t)slices * a.M * a.N;
+            hipLaunchKernelGGL(mmq_split_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, (const float *)part,
+                               n_split, slices);
         }
         return hipGetLastError();
     }

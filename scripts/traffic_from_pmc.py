@@ -1,7 +1,7 @@
 """Turn a `rocprofv3 --pmc FETCH_SIZE --kernel-trace` run of the headline bench into
 profiles/traffic.json: HBM bytes per launch of the mat-vec kernel, with the gfx950 FETCH_SIZE
 correction of MI355X_MICROARCH.md (FETCH_SIZE counts KiB in 64-B units of 128-B requests, so
-bytes = FETCH_SIZE * 1024 * 2). Usage: python scripts/traffic_from_pmc.py <counter_collection.csv>"""
+bytes = FETCH_SIZE * 1024 * 2). Usage: python scripts/traffic_from_pmc.py <counter_collection.csv> [out.json] [round]"""
 import csv
 import json
 import os
@@ -10,15 +10,15 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 rows = [r for r in csv.DictReader(open(sys.argv[1])) if r["Counter_Name"] == "FETCH_SIZE" and "mmvq_kernel" in r["Kernel_Name"]]
-# the headline kernel: the launch shape the bench repeats most (64 stacked matrices)
+# the headline kernel: the launch that streams the 64 stacked matrices (by far the largest fetch)
 by_kernel = {}
 for r in rows:
     by_kernel.setdefault((r["Kernel_Name"], r["Grid_Size"]), []).append(float(r["Counter_Value"]))
-(name, grid), vals = max(by_kernel.items(), key=lambda kv: len(kv[1]))
+(name, grid), vals = max(by_kernel.items(), key=lambda kv: statistics.median(kv[1]))
 kb = statistics.median(vals)
 alg = 4096 * 4096 * 18 // 32 * 64 + 4 * 4096 * 64 + 4 * 4096 * 64
 out = {"q4_0_4096x4096_m1_b64": {
-    "round": 1,
+    "round": int(sys.argv[3][1:]) if len(sys.argv) > 3 else 1,
     "command": "rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -- python bench.py --no-extra "
                "--cpu-seconds 1 --steps 5 --warmup 1",
     "kernel": name, "grid_size": int(grid), "dispatches": len(vals),
@@ -27,6 +27,6 @@ out = {"q4_0_4096x4096_m1_b64": {
                   "bytes = FETCH_SIZE[KB] * 1024 * 2 (MI355X_MICROARCH.md, HBM section)",
     "hbm_bytes_per_launch": kb * 1024 * 2, "algorithmic_bytes_per_launch": alg,
     "traffic_over_algorithmic": kb * 1024 * 2 / alg}}
-with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as f:
+with open(sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "profiles", "traffic.json"), "w") as f:
     json.dump(out, f, indent=1)
 print(json.dumps(out, indent=1))
