@@ -699,6 +699,10 @@ __device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t bi
 __device__ __forceinline__ uint32_t bl32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
 }
+// LDS reads of staged weight rows (mmq_wl_kernel): 16-B aligned, or dword aligned
+__device__ __forceinline__ u32x4 lds16(const uint8_t *p) { return *reinterpret_cast<const u32x4 *>(p); }
+__device__ __forceinline__ uint32_t lds1(const uint8_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
+__device__ __forceinline__ u32x4 lds4u(const uint8_t *p) { return u32x4{lds1(p), lds1(p + 4), lds1(p + 8), lds1(p + 12)}; }
 
 template <> struct Deq32<T_Q4_0> {   // block: d (f16), 16 B of nibbles (w[i] low, w[i+16] high)
     static constexpr int NLOADS = 2;
@@ -715,6 +719,14 @@ template <> struct Deq32<T_Q4_0> {   // block: d (f16), 16 B of nibbles (w[i] lo
     __device__ __forceinline__ void part(__amdgpu_buffer_rsrc_t r, int p) {
         if (p == 0) w0 = bl128(r, b);
         else w4 = bl32(r, b + 16);
+    }
+    static constexpr int SB = 144;   // bytes of 8 blocks (256 k) of one row, staged per row in LDS
+    __device__ __forceinline__ void lds(const uint8_t *rp, int kr) {   // rp: the row's 16-B aligned segment
+        const uint32_t o = (uint32_t)((kr >> 5) & 7) * 18;
+        b = o & ~3u;
+        odd = (o >> 1) & 1;
+        w0 = lds4u(rp + b);
+        w4 = lds1(rp + b + 16);
     }
     __device__ __forceinline__ uint32_t d16() const { return (w0[0] >> (16 * odd)) & 0xFFFFu; }
     // dword i of the 16 nibble bytes: window bytes 2 + 2 odd + 4i ..
@@ -754,6 +766,15 @@ template <> struct Deq32<T_Q8_0> {   // block: d (f16), 32 int8
         else if (p == 1) w4 = bl128(r, b + 16);
         else w8 = bl32(r, b + 32);
     }
+    static constexpr int SB = 272;
+    __device__ __forceinline__ void lds(const uint8_t *rp, int kr) {
+        const uint32_t o = (uint32_t)((kr >> 5) & 7) * 34;
+        b = o & ~3u;
+        odd = (o >> 1) & 1;
+        w0 = lds4u(rp + b);
+        w4 = lds4u(rp + b + 16);
+        w8 = lds1(rp + b + 32);
+    }
     __device__ __forceinline__ uint32_t win(int i) const { return i < 4 ? w0[i] : i < 8 ? w4[i - 4] : w8; }
     __device__ __forceinline__ uint32_t d16() const { return (w0[0] >> (16 * odd)) & 0xFFFFu; }
     // dword i of the 32 quant bytes: window bytes 2 + 2 odd + 4i ..
@@ -790,6 +811,13 @@ template <> struct Deq32<T_Q4_K> {   // super-block 144 B: d, dmin, 12 B scales,
         if (p == 0) hd = bl128(r, b);
         else if (p == 1) q0 = bl128(r, b + 16 + 32 * (j >> 1));
         else q1 = bl128(r, b + 32 + 32 * (j >> 1));
+    }
+    static constexpr int SB = 144;
+    __device__ __forceinline__ void lds(const uint8_t *rp, int kr) {
+        j = (kr & 255) >> 5;
+        hd = lds16(rp);
+        q0 = lds16(rp + 16 + 32 * (j >> 1));
+        q1 = lds16(rp + 32 + 32 * (j >> 1));
     }
     __device__ __forceinline__ uint32_t prep(uint32_t &bad) {
         float d1, m1;
@@ -831,6 +859,15 @@ template <> struct Deq32<T_Q5_K> {   // super-block 176 B: d, dmin, 12 B scales,
         else if (p == 2) q1 = bl128(r, b + 64 + 32 * (j >> 1));
         else if (p == 3) h0 = bl128(r, b + 16);
         else h1 = bl128(r, b + 32);
+    }
+    static constexpr int SB = 176;
+    __device__ __forceinline__ void lds(const uint8_t *rp, int kr) {
+        j = (kr & 255) >> 5;
+        hd = lds16(rp);
+        h0 = lds16(rp + 16);
+        h1 = lds16(rp + 32);
+        q0 = lds16(rp + 48 + 32 * (j >> 1));
+        q1 = lds16(rp + 64 + 32 * (j >> 1));
     }
     __device__ __forceinline__ uint32_t prep(uint32_t &bad) {
         float d1, m1;
@@ -1248,6 +1285,314 @@ __global__ __launch_bounds__(512) void mmq_wave_kernel(const MmArgs a, const _Fl
 }
 
 // ------------------------------------------------------------------------------------------
+// mmq_wl_kernel: mmq_wave_kernel with the weights staged through LDS. The register-decode
+// kernel's per-lane row loads touch 32 rows (32 cache lines) per wave instruction and keep the
+// texture unit busy (§4.2 of DESIGN.md). Here all 8 waves copy each 256-k super-block of the
+// workgroup's 128 rows into an LDS ring with 16-B LDS-DMA pieces that walk the rows in order
+// (a piece covers ~7 consecutive row segments), and each lane then reads its own run from LDS.
+// Needs every row's 256-k segment 16-B aligned: Q4_0 / Q8_0 / Q4_K / Q5_K with K % 256 == 0.
+//   ring: 3 slots of 128 rows x SB bytes; super-block b is consumed by phases 2b, 2b+1 (both
+//   K-groups), its pieces are issued in phases 2b-4 and 2b-3 (half each) and retire with the
+//   activations of phase 2b-2, one barrier before the first decode reads them.
+// ------------------------------------------------------------------------------------------
+template <int T, int TN, bool STAMP = false>
+__global__ __launch_bounds__(512) void mmq_wl_kernel(const MmArgs a, const _Float16 *__restrict__ x16,
+                                                     const _Float16 *__restrict__ xsum, const float *__restrict__ xinv,
+                                                     int Kpad, uint32_t w_extent, int n_split, int split_np,
+                                                     float *__restrict__ part) {
+    constexpr int BN = 32 * TN, XB = BN * 128, V = TN;
+    constexpr int SB = Deq32<T>::SB;            // bytes of one row's 256-k segment
+    constexpr int WSLOT = 128 * SB;             // one ring slot
+    constexpr int NPIECE = WSLOT / 1024;        // 1-KiB pieces per slot
+    static_assert(WSLOT % 1024 == 0 && SB % 16 == 0, "slot made of whole pieces");
+    constexpr int TMAX = (NPIECE + 7) / 8;      // pieces of the busiest wave per slot
+    constexpr int TMIN = NPIECE / 8;            // pieces of the least busy wave per slot
+    constexpr int WMAX0 = (TMAX + 1) / 2, WMAX1 = TMAX / 2;   // per half (even / odd phase)
+    constexpr int WLOW0 = (TMIN + 1) / 2, WLOW1 = TMIN / 2;
+    static_assert(WMAX0 + V + 2 * TN < 64, "vmcnt range");
+    __shared__ __align__(16) uint8_t lds[6 * XB + 3 * WSLOT];   // [group][3][XB] | [3][WSLOT]
+    __shared__ uint32_t g1_bad[4];
+
+    const int slice = blockIdx.z / n_split, split = blockIdx.z % n_split;
+    const int i12 = slice % a.ne12, i13 = slice / a.ne12;
+    const int nrec = (Kpad + 511) / 512 * 2;
+    const uint8_t *wmat = a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03;
+    const _Float16 *xs = x16 + (int64_t)slice * a.M * Kpad;
+    const _Float16 *ss = xsum + (int64_t)slice * a.M * nrec * 16;
+    uint8_t *dmat = a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3;
+    const int tok0 = blockIdx.y * BN, tok_end = a.M;
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void *)wmat, 0, w_extent, RSRC_W3);
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)xs, 0, (uint32_t)tok_end * (uint32_t)Kpad * 2u, RSRC_W3);
+    const __amdgpu_buffer_rsrc_t sr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)ss, 0, (uint32_t)tok_end * (uint32_t)nrec * 32u, RSRC_W3);
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int grp = wave >> 2, wq = wave & 3;
+    const int fr = lane & 31, fh = lane >> 5;
+    const int row0 = blockIdx.x * 128;
+    const int row = row0 + 32 * wq + fr;
+    const uint32_t wrow = (uint32_t)row * (uint32_t)a.nb01;
+    const int p0 = split * split_np;                        // first (global) phase of this split
+    const int np = min(split_np, Kpad / (2 * MQ_BK) - p0);   // phases of this split (even)
+    const int sb_last = (p0 + np - 1) / 2;                  // last super-block of this split
+    uint8_t *const xslot = lds + grp * 3 * XB;
+    uint8_t *const wslot = lds + 6 * XB;
+    uint64_t st_seg[5] = {0, 0, 0, 0, 0}, st_t = 0, st_start = 0;
+    auto stamp = [&](int seg) {
+        if constexpr (STAMP) {
+            __builtin_amdgcn_sched_barrier(0);
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            if (seg >= 0) st_seg[seg] += t - st_t;
+            st_t = t;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    stamp(-1);
+    st_start = st_t;
+
+    uint32_t x_off[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int r = 8 * (wq + 4 * v) + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        x_off[v] = ((uint32_t)(tok0 + r) * (uint32_t)Kpad + (uint32_t)c * 8u) * 2u;
+    }
+    auto step_of = [&](int p) { return 2 * (p0 + p) + grp; };
+    auto dma_x = [&](int p, int slot, int v) {
+        dma16(xr, xslot + slot * XB + (wq + 4 * v) * 1024, x_off[v] + (uint32_t)step_of(p) * MQ_BK * 2u);
+    };
+    // piece q of super-block gsb (data of min(gsb, sb_last)) into ring slot gsb % 3: chunk
+    // c = 64 q + lane is 16-B piece i of row r's segment, rows in order
+    auto dma_w = [&](int gsb, int q) {
+        const int c = q * 64 + lane, r = c / (SB / 16), i = c % (SB / 16);
+        const uint32_t off = (uint32_t)(row0 + r) * (uint32_t)a.nb01 + (uint32_t)min(gsb, sb_last) * SB + 16u * i;
+        dma16(wr, wslot + (gsb % 3) * WSLOT + q * 1024, off);
+    };
+    // the wave's pieces of a slot are q = wave + 8t; half h takes t = h, h + 2, ...
+    auto w_count = [&](int h) { const int tw = (NPIECE - wave + 7) / 8; return (tw - h + 1) / 2; };
+    u32x4 sfrag[TN];
+    auto load_sums = [&](int w) {
+        const uint32_t rec = (uint32_t)(2 * (w + p0 / MQ_WIN) + grp);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+            sfrag[j] = bl128(sr, ((uint32_t)(tok0 + 32 * j + fr) * (uint32_t)nrec + rec) * 32u + 16u * fh);
+    };
+    // this lane's run of local phase p, read from the ring
+    auto fetch = [&](Deq32<T> &w, int p) {
+        const int st = step_of(p), gsb = st >> 2;
+        w.lds(wslot + (gsb % 3) * WSLOT + (32 * wq + fr) * SB, st * MQ_BK + 32 * fh);
+    };
+
+    float16v acc[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    auto compute = [&](const u32x4 (&f)[4], int xsl) {
+        const uint8_t *X = xslot + xsl * XB;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            half8 ax[TN];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) ax[j] = *reinterpret_cast<const half8 *>(X + swz(32 * j + fr, 4 * fh + ks));
+            const half8 bw = __builtin_bit_cast(half8, f[ks]);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax[j], bw, acc[j], 0, 0, 0);
+        }
+    };
+    u32x4 cw = {0u, 0u, 0u, 0u};
+    auto correct = [&]() {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, sfrag[j]), __builtin_bit_cast(half8, cw),
+                                                            acc[j], 0, 0, 0);
+        cw = u32x4{0u, 0u, 0u, 0u};
+    };
+    auto barrier = [&]() {
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    uint32_t bad = 0;
+    const DecK DK = DecK::make();
+    Deq32<T> rw;
+    u32x4 F[4], G[4];
+    // prologue: the split's first two super-blocks, the activations of phases 0 and 1
+    const int gsb0 = p0 / 2;
+    load_sums(0);
+#pragma unroll
+    for (int t = 0; t < TMAX; ++t)
+        if (wave + 8 * t < NPIECE) {
+            dma_w(gsb0, wave + 8 * t);
+            dma_w(gsb0 + 1, wave + 8 * t);
+        }
+#pragma unroll
+    for (int v = 0; v < V; ++v) dma_x(0, 0, v);
+#pragma unroll
+    for (int v = 0; v < V; ++v) dma_x(min(1, np - 1), 1, v);
+    wait_vmcnt<V>();   // everything but phase 1's activations
+    barrier();
+    fetch(rw, 0);
+    cw[0] = rw.prep(bad);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) F[ks] = rw.frag(ks, DK);
+
+    // phase p (SP = window slot of phase p+1, H = half of the super-block pieces it issues):
+    // LDS reads (this step's activation fragments, next step's weight run) first, then NMF chunks
+    // of one MFMA, a share of the DMA pieces (weights for super-block (P/2)+2, then the
+    // activations of phase p+2) and of the decode; the activations of phase p+1 retire and one
+    // barrier ends the phase
+    constexpr int NMF = 4 * TN;
+    auto phase = [&](auto SPc, const u32x4 (&fcur)[4], u32x4 (&fnext)[4], int p, int xs0) {
+        constexpr int SP = decltype(SPc)::value;
+        constexpr int H = (SP + 1) & 1;          // p % 2 (p0 is a multiple of MQ_WIN)
+        constexpr int WMX = H ? WMAX1 : WMAX0, WLOW = H ? WLOW1 : WLOW0;
+        constexpr int VMX = WMX + V;
+        const int xs1 = xs0 == 2 ? 0 : xs0 + 1, xs2 = xs1 == 2 ? 0 : xs1 + 1;
+        const int pl = min(p + 2, np - 1);
+        const int gsb_dma = (p0 + p) / 2 + 2;
+        const int wcnt = w_count(H);
+        stamp(3);
+        const uint8_t *X = xslot + xs0 * XB;
+        half8 ax[4][TN];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) ax[ks][j] = *reinterpret_cast<const half8 *>(X + swz(32 * j + fr, 4 * fh + ks));
+        fetch(rw, p + 1);
+        stamp(0);
+#pragma unroll
+        for (int i = 0; i < NMF; ++i) {
+            const int ks = i / TN, j = i % TN;
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ax[ks][j], __builtin_bit_cast(half8, fcur[ks]), acc[j], 0, 0, 0);
+#pragma unroll
+            for (int l = i * VMX / NMF; l < (i + 1) * VMX / NMF; ++l) {
+                if (l < WMX) {
+                    if (l < wcnt) dma_w(gsb_dma, wave + 8 * (H + 2 * l));
+                } else {
+                    dma_x(pl, xs2, l - WMX);
+                }
+            }
+            constexpr int PER = NMF / 4;
+            if (i % PER == PER - 1) {
+                if (i == PER - 1) cw[SP] = rw.prep(bad);
+                fnext[i / PER] = rw.frag(i / PER, DK);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (SP == MQ_WIN - 1) {
+            correct();
+            load_sums((p + 2) / MQ_WIN);
+        }
+        stamp(1);
+        // retire phase p+1's activations (issued last in the previous phase, after its weight
+        // pieces): younger are at least this phase's pieces and the sums of a closing phase
+        wait_vmcnt<V + WLOW + (SP == MQ_WIN - 1 || SP == 0 ? TN : 0)>();
+        stamp(2);
+        barrier();
+        return xs1;
+    };
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I0 = std::integral_constant<int, 0>;
+    int p = 0, xsl = 0;
+    for (; p + MQ_WIN <= np - 1; p += MQ_WIN) {
+        xsl = phase(I1{}, F, G, p, xsl);
+        xsl = phase(I2{}, G, F, p + 1, xsl);
+        xsl = phase(I3{}, F, G, p + 2, xsl);
+        xsl = phase(I0{}, G, F, p + 3, xsl);
+    }
+    const int rem = np - 1 - p;
+    if (rem >= 1) xsl = phase(I1{}, F, G, p, xsl);
+    if (rem >= 2) xsl = phase(I2{}, G, F, p + 1, xsl);
+    if (rem >= 3) xsl = phase(I3{}, F, G, p + 2, xsl);
+    if (rem & 1) compute(G, xsl);
+    else compute(F, xsl);
+    if (rem != 3) correct();
+    wait_vmcnt<0>();
+    stamp(3);
+    if constexpr (STAMP) {
+        if (lane == 0 && a.stamps) {
+            const int g = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+            unsigned long long *o = a.stamps + ((size_t)g * 8 + wave) * 8;
+            o[0] = st_start;
+            for (int i = 0; i < 5; ++i) o[1 + i] = st_seg[i];
+            o[6] = st_t;
+            o[7] = np;
+        }
+    }
+
+    const bool bad_here = (bad & 0xFFFFu) >= F16_ONE || (bad >> 16) >= F16_ONE;
+    float4 *park = reinterpret_cast<float4 *>(lds) + (size_t)(wq * 64 + lane) * 4 * TN;
+    barrier();
+    if (grp == 1) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                park[4 * j + q] = make_float4(acc[j][4 * q], acc[j][4 * q + 1], acc[j][4 * q + 2], acc[j][4 * q + 3]);
+        const bool b1 = __builtin_amdgcn_ballot_w64(bad_here) != 0;
+        if (lane == 0) g1_bad[wq] = b1;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier();
+    if (grp == 1) return;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 o = park[4 * j + q];
+            acc[j][4 * q] += o.x;
+            acc[j][4 * q + 1] += o.y;
+            acc[j][4 * q + 2] += o.z;
+            acc[j][4 * q + 3] += o.w;
+        }
+
+    auto tok_of = [&](int j, int r) { return tok0 + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * fh; };
+    if ((__builtin_amdgcn_ballot_w64(bad_here) != 0) || g1_bad[wq]) {   // fp32 path, as mmq_wave_kernel
+        for (int j = 0; j < TN; ++j)
+            for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+        for (int kr = p0 * 2 * MQ_BK; kr < min(a.K, (p0 + np) * 2 * MQ_BK); kr += 32) {
+            Deq32<T> w;
+            w.at(wrow, kr);
+            for (int q = 0; q < Deq32<T>::NLOADS; ++q) w.part(wr, q);
+            for (int e = 0; e < 32; ++e) {
+                const float wf = w.w32(e);
+                const int ke = kr + (e & ~3) + ((e & 3) == 1 ? 2 : (e & 3) == 2 ? 1 : (e & 3));
+                for (int j = 0; j < TN; ++j)
+                    for (int r = 0; r < 16; ++r) {
+                        const int t = min(tok_of(j, r), tok_end - 1);
+                        acc[j][r] += wf * (float)xs[(int64_t)t * Kpad + ke];
+                    }
+            }
+        }
+    }
+    const float *xinv_s = xinv + (int64_t)slice * a.M;
+    float inv[TN][16];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) inv[j][r] = xinv_s[min(tok_of(j, r), tok_end - 1)];
+    if (row < a.N) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int tok = tok_of(j, r);
+                if (tok < tok_end) {
+                    float *drow = n_split > 1 ? part + (((int64_t)split * (gridDim.z / n_split) + slice) * a.M + tok) * a.N
+                                              : reinterpret_cast<float *>(dmat + (int64_t)tok * a.nb1);
+                    drow[row] = acc[j][r] * inv[j][r];
+                }
+            }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
 static int64_t row_bytes(int type, int K) { return (int64_t)K / type_blck(type) * type_bytes(type); }
@@ -1303,10 +1648,32 @@ static void launch_wave(const MmArgs &a, const _Float16 *x16, const _Float16 *xs
                            n_split, split_np, part);
 }
 
+template <int T, int TN>
+static void launch_wl(const MmArgs &a, const _Float16 *x16, const _Float16 *xsum, const float *xinv, int Kpad, int slices,
+                      int n_split, int split_np, float *part, hipStream_t st) {
+    const dim3 grid((a.N + 127) / 128, (a.M + 32 * TN - 1) / (32 * TN), slices * n_split);
+    const uint32_t w_extent = (uint32_t)(((int64_t)(a.N - 1) * a.nb01 + row_bytes(T, a.K) + 3) & ~(int64_t)3);
+    if (a.stamps && (size_t)grid.x * grid.y * grid.z * 64 <= 8 * 65536)
+        hipLaunchKernelGGL((mmq_wl_kernel<T, TN, true>), grid, dim3(512), 0, st, a, x16, xsum, xinv, Kpad, w_extent, n_split,
+                           split_np, part);
+    else
+        hipLaunchKernelGGL((mmq_wl_kernel<T, TN, false>), grid, dim3(512), 0, st, a, x16, xsum, xinv, Kpad, w_extent, n_split,
+                           split_np, part);
+}
+
+// mmq_wl_kernel needs every row's 256-k segment 16-B aligned
+static bool wl_ok(int type, const MmArgs &a) {
+    if (!(type == T_Q4_0 || type == T_Q8_0 || type == T_Q4_K || type == T_Q5_K)) return false;
+    return a.K % 256 == 0 && (reinterpret_cast<uintptr_t>(a.w) & 15) == 0 && a.nb01 % 16 == 0 && a.nb02 % 16 == 0 &&
+           a.nb03 % 16 == 0;
+}
+
 template <int T>
 static void launch_wave_tn(int tile, const MmArgs &a, const _Float16 *x16, const _Float16 *xsum, const float *xinv, int Kpad,
                            int slices, int n_split, int split_np, float *part, hipStream_t st) {
     switch (tile) {
+        case 20: if constexpr (T != T_Q6_K) launch_wl<T, 1>(a, x16, xsum, xinv, Kpad, slices, n_split, split_np, part, st); break;
+        case 21: if constexpr (T != T_Q6_K) launch_wl<T, 2>(a, x16, xsum, xinv, Kpad, slices, n_split, split_np, part, st); break;
         case 10: launch_wave<T, 1>(a, x16, xsum, xinv, Kpad, slices, n_split, split_np, part, st); break;
         case 12: launch_wave<T, 4>(a, x16, xsum, xinv, Kpad, slices, n_split, split_np, part, st); break;
         default: launch_wave<T, 2>(a, x16, xsum, xinv, Kpad, slices, n_split, split_np, part, st); break;
@@ -1338,17 +1705,22 @@ static int pick_tile(int type, const MmArgs &a, int slices) {
         if (!strcmp(env, "wave32")) return 10;
         if (!strcmp(env, "wave64")) return 11;
         if (!strcmp(env, "wave128")) return 12;
+        if (!strcmp(env, "wl32")) return wl_ok(type, a) ? 20 : 10;
+        if (!strcmp(env, "wl64")) return wl_ok(type, a) ? 21 : 11;
     }
     auto wgs = [&](int bm, int bn) { return (int64_t)((a.N + bm - 1) / bm) * ((a.M + bn - 1) / bn) * slices; };
-    // measured on MI355X (scripts/mmq_sweep.sh): 128x128 once it fills the chip, otherwise the
-    // 64-row tile (twice the workgroups) unless there are too few tokens for 128-token tiles
-    // few tokens (M <= 128): the register-decode kernel, 32-token tiles, for the types whose
-    // weight runs load in <= 3 vector-memory instructions per K-step (scripts/mmq_compare.sh:
-    // Q4_K M=32 34 vs 47 us, M=128 35 vs 40 us; Q8_0 M=64 48 vs 51 us); beyond that, and for
-    // Q5_K / Q6_K (5 / 8 loads per run), its scattered per-row loads keep the texture unit busier
-    // than the LDS-staged tiles below
+    // register-decode kernels (scripts/mmq_tiles.sh, round 2): with the weights staged through
+    // LDS (mmq_wl_kernel, 16-B aligned 256-k row segments) for Q4_0 / Q4_K / Q5_K below a full
+    // chip of 128x128 tiles and for any of the four at M <= 64 (Q4_K M=32 20 us vs 47,
+    // M=512 45 vs 50); the per-lane-load variant for few tokens of misaligned Q4_0 / Q4_K / Q8_0.
+    // Beyond, Q8_0 above 64 tokens and Q6_K: the LDS-staged f16 tiles.
+    const bool wl = wl_ok(type, a);
+    if (wl && a.M <= 64) return 20;
+    if (wl && type != T_Q8_0 && wgs(128, 128) < 256) return a.M <= 128 ? 20 : 21;
     const bool light = type == T_Q4_0 || type == T_Q4_K || type == T_Q8_0;
     if (light && a.M <= 128 && (a.M <= 64 || type != T_Q8_0)) return 10;
+    // LDS-staged tiles (scripts/mmq_sweep.sh): 128x128 once it fills the chip, otherwise the
+    // 64-row tile (twice the workgroups) unless there are too few tokens for 128-token tiles
     if (wgs(128, 128) >= 256) return 2;
     return a.M > 64 ? 0 : 1;
 }
@@ -1363,7 +1735,7 @@ hipError_t mmq_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratc
     // (MQ_WIN phases = 512 k each)
     int n_split = 1, split_np = Kpad / kq;
     if (wave) {
-        const int tn = tile == 10 ? 1 : tile == 12 ? 4 : 2;
+        const int tn = (tile == 10 || tile == 20) ? 1 : tile == 12 ? 4 : 2;
         const int64_t wgs = (int64_t)((a.N + 127) / 128) * ((a.M + 32 * tn - 1) / (32 * tn)) * slices;
         const int windows = (split_np + MQ_WIN - 1) / MQ_WIN;
         while (wgs * n_split < 256 && windows >= 2 * n_split) n_split *= 2;

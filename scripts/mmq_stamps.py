@@ -30,7 +30,7 @@ for sh in sys.argv[1:] or ["q4_K:4096:4096:128", "q8_0:4096:4096:512"]:
     n = st[:, 7].astype(np.float64)
     tot = (st[:, 6] - st[:, 0]) / n
     names = ["issue loads", "mfma", "decode+ds_write", "wait dma", "barrier"]
-    if os.environ.get("GGML_MI355X_MMQ_TILE", "").startswith("wave"):   # mmq_wave_kernel segments
+    if os.environ.get("GGML_MI355X_MMQ_TILE", "").startswith(("wave", "wl")):   # register-decode kernels
         names = ["top (ds_read issue)", "mfma+loads+decode", "wait dma", "barrier", "-"]
     print(f"{sh}: {len(st)} waves, nsteps={int(n[0])}, cycles per step (median over waves):")
     for i, nm in enumerate(names):

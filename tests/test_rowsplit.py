@@ -93,7 +93,8 @@ def test_all_gather_bookkeeping_two_ranks(case):
                                                (qref.Q8_0, 4096, 4096, 64, 2, [1, 3]), (qref.Q6_K, 1024, 1000, 5, 4, None)])
 def test_hip_shards_reassemble_to_unsharded(t, K, N, M, shards, fr):
     """the HIP kernels run shard by shard on one GPU (virtual ranks) and reassembled equal the
-    unsharded launch to fp32 rounding (the row reduction tree can differ with the launch shape)"""
+    unsharded launch to fp32 rounding (the reduction order can differ with the launch shape: the
+    few-token mat-mat picks its split-K count from the shard's workgroup count)"""
     import mi355x_qmm as Q
     rng = np.random.default_rng(7)
     rb = Q.row_size(t, K)
@@ -116,4 +117,4 @@ def test_hip_shards_reassemble_to_unsharded(t, K, N, M, shards, fr):
     R.assemble(parts, R.row_split(N, shards, fr), out)
     torch.cuda.synchronize()
     assert torch.isfinite(out).all()
-    assert torch.allclose(out, full, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(out, full, rtol=1e-5, atol=1e-5 * float(full.abs().max()))
