@@ -42,7 +42,8 @@ hipError_t fused_one(const MmArgs &a0, int grid_z, hipStream_t st, bool prepare_
     // (lm_head) walk their row groups with the prefetch pipeline instead of queueing rounds of
     // workgroups; EPI_ARGMAX needs one partial slot per workgroup (ARGMAX_SLOTS)
     static const int target = getenv("GGML_MI355X_FUSED_WGS") ? atoi(getenv("GGML_MI355X_FUSED_WGS")) : 256;
-    const int want = std::max(1, std::min(ARGMAX_SLOTS, target / grid_z));
+    static const int tall = getenv("GGML_MI355X_FUSED_TALL") ? atoi(getenv("GGML_MI355X_FUSED_TALL")) : 256;
+    const int want = std::max(1, std::min(ARGMAX_SLOTS, (n_groups > 4 * target ? tall : target) / grid_z));
     dim3 grid(std::min(n_groups, want), 1, grid_z);
     hipLaunchKernelGGL(kern, grid, dim3(MMVQ_THREADS), mmvq_lds_bytes(a.K, NC), st, a);
     return hipGetLastError();
@@ -70,14 +71,21 @@ hipError_t fused_nc_attn(const MmArgs &a, int nc, int grid_z, hipStream_t st) {
     }
 }
 
+// lanes per row of a fused mat-vec: as mmvq_pick_lpr, but short matrices take 64 lanes (8 rows
+// per workgroup instead of 32) so that they spread over more CUs
+static int fused_lpr(const MmArgs &a) {
+    static const int maxn = getenv("GGML_MI355X_FUSED_LPR64_MAXN") ? atoi(getenv("GGML_MI355X_FUSED_LPR64_MAXN")) : 0;
+    return a.N <= maxn ? 64 : mmvq_pick_lpr(a.K);
+}
+
 template <int T>
 hipError_t fused_type(const MmArgs &a, int nc, int rpw, int grid_z, hipStream_t st) {
     if (a.attn_part != nullptr) {   // c_proj with the attention merge prologue (K = n_embd)
         if (a.K > 4096) return hipErrorInvalidValue;
         if (nc > 3) return hipErrorInvalidValue;   // (the merge partials of >3 columns would spill)
-        return mmvq_pick_lpr(a.K) == 16 ? fused_nc_attn<T, 16>(a, nc, grid_z, st) : fused_nc_attn<T, 64>(a, nc, grid_z, st);
+        return fused_lpr(a) == 16 ? fused_nc_attn<T, 16>(a, nc, grid_z, st) : fused_nc_attn<T, 64>(a, nc, grid_z, st);
     }
-    if (mmvq_pick_lpr(a.K) == 16) return fused_nc<T, 16, 1>(a, nc, grid_z, st);
+    if (fused_lpr(a) == 16) return fused_nc<T, 16, 1>(a, nc, grid_z, st);
     return rpw <= 1 ? fused_nc<T, 64, 1>(a, nc, grid_z, st) : fused_nc<T, 64, 2>(a, nc, grid_z, st);
 }
 
