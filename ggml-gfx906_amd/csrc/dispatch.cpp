@@ -45,6 +45,18 @@ hipError_t quantize_launch(int type, const QuantArgs &a, hipStream_t st);
 bool mmq_supported(int type, const MmArgs &a);
 bool mmq_id_supported(int type, const MmArgs &a);
 hipError_t mmq_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
+bool mmq8_supported(int type, const MmArgs &a);
+hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
+
+// mat-mat kernel family: GGML_MI355X_MMQ = i8 (the int8 MFMA path wherever it applies) | f16
+// (the f16 MFMA kernels only); unset: the measured default rule of use_mmq8
+static bool use_mmq8(int type, const MmArgs &m) {
+    const char *env = getenv("GGML_MI355X_MMQ");
+    if (!mmq8_supported(type, m)) return false;
+    if (env && !strcmp(env, "i8")) return true;
+    if (env && !strcmp(env, "f16")) return false;
+    return false;
+}
 
 static constexpr size_t LDS_LIMIT = 160 * 1024;
 
@@ -158,7 +170,8 @@ int mul_mat(const TensorView &a, const TensorView &b, const TensorView &d, hipSt
     if (a.ne[1] == 0 || b.ne[1] == 0 || b.ne[2] == 0 || b.ne[3] == 0) return GGML_MI355X_OK;
     MmArgs m = base_args(a, b, d);
     hipError_t e;
-    if (m.M > 8 && mmq_supported(a.type, m)) e = mmq_launch(a.type, m, st, scratch);
+    if (m.M > 8 && use_mmq8(a.type, m)) e = mmq8_launch(a.type, m, st, scratch);
+    else if (m.M > 8 && mmq_supported(a.type, m)) e = mmq_launch(a.type, m, st, scratch);
     else e = run_mmvq(a.type, m, 0, m.M, st);
     if (e == hipErrorOutOfMemory) return GGML_MI355X_ENOMEM;
     return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
