@@ -40,6 +40,19 @@ hipError_t gpt2_attn_launch(const float *qkv, float *kc, float *vc, const int32_
 hipError_t gpt2_argmax_launch(const float *pv, const int32_t *pi, int n_seq, int32_t *tokens, int32_t *pos, hipStream_t st);
 hipError_t gpt2_argmax_reset(float *pv, int32_t *pi, int n_seq, hipStream_t st);
 hipError_t gpt2_advance_launch(int32_t *pos, int n_seq, hipStream_t st);
+bool gpt2_block_supported(int n_embd, int n_head);
+int gpt2_block_mlp_slices(int n_embd);
+hipError_t gpt2_attn_block_launch(int layer, int type, const float *base, const float *bias_in, const float *parts_in, int n_parts_in,
+                                  float *x_out, const float *ln_g, const float *ln_b, float eps, const uint8_t *w_qkv,
+                                  int64_t nb_qkv, const float *b_qkv, float *kc, float *vc, const int32_t *pos, float scale,
+                                  int n_ctx, const uint8_t *w_o, int64_t nb_o, float *parts_out, int E, int n_head, int n_seq,
+                                  hipStream_t st);
+hipError_t gpt2_mlp_block_launch(int layer, int type, const float *base, const float *bias_in, const float *parts_in, int n_parts_in,
+                                 float *x_out, const float *ln_g, const float *ln_b, float eps, const uint8_t *w_fc,
+                                 int64_t nb_fc, const float *b_fc, const uint8_t *w_mp, int64_t nb_mp, float *parts_out, int E,
+                                 int n_head, int n_seq, hipStream_t st);
+hipError_t gpt2_resid_launch(const float *base, const float *bias_in, const float *parts_in, int n_parts_in, float *x_out, int E,
+                             int n_seq, hipStream_t st);
 }  // namespace mi355x
 
 using namespace mi355x;
@@ -103,6 +116,10 @@ struct ggml_mi355x_gpt2_ctx {
     float *part = nullptr;                     // attention partials [seq][head][ATTN_SPLITS][ATTN_PART_STRIDE]
     float *amax_v = nullptr;                   // lm_head per-workgroup argmax partials [seq][ARGMAX_SLOTS]
     int32_t *amax_i = nullptr;
+    // two-launch layer (gpt2_block.hip): materialized residuals after attention / after the MLP
+    // and the K-split partial slabs [split][seq][n_embd] of c_proj (per head) and the MLP proj
+    bool block = false;
+    float *xr = nullptr, *xm = nullptr, *p_attn = nullptr, *p_mlp = nullptr;
     std::map<hipStream_t, hipGraphExec_t> graphs;
 };
 
@@ -175,6 +192,38 @@ int run_step(ggml_mi355x_gpt2_ctx *c, hipStream_t st) {
     }
     const float kq_scale = 1.0f / sqrtf(float(E) / hp.n_head);   // main-sched.cpp:587
     const size_t cache_layer = (size_t)c->n_seq * hp.n_ctx * E;
+    if (c->block) {
+        // two launches per layer; the residual travels as (base, bias, partial slabs) and is
+        // summed by the next launch's prologue, then materialized into c->x for the stage
+        // boundary / lm_head
+        const float *base = c->x, *bias = nullptr, *parts = nullptr;
+        int np = 0;
+        const int n_sl = gpt2_block_mlp_slices(E);
+        for (int l = m->l0; l < m->l1; ++l) {
+            const Layer &L = m->layers[l - m->l0];
+            float *kc = c->kc + (size_t)(l - m->l0) * cache_layer;
+            float *vc = c->vc + (size_t)(l - m->l0) * cache_layer;
+            auto f = [](const Tensor &t) { return reinterpret_cast<const float *>(t.data); };
+            rc = hip_status(gpt2_attn_block_launch(l - m->l0, m->wtype, base, bias, parts, np, c->xr, f(L.ln1_g), f(L.ln1_b), 1e-5f, L.attn_w.data,
+                                                   row_bytes(m->wtype, E), f(L.attn_b), kc, vc, c->pos, kq_scale, hp.n_ctx,
+                                                   L.proj_w.data, row_bytes(m->wtype, E), c->p_attn, E, hp.n_head, c->n_seq, st));
+            if (rc) return rc;
+            rc = hip_status(gpt2_mlp_block_launch(l - m->l0, m->wtype, c->xr, f(L.proj_b), c->p_attn, hp.n_head, c->xm, f(L.ln2_g), f(L.ln2_b),
+                                                  1e-5f, L.fc_w.data, row_bytes(m->wtype, E), f(L.fc_b), L.mproj_w.data,
+                                                  row_bytes(m->wtype, 4 * E), c->p_mlp, E, hp.n_head, c->n_seq, st));
+            if (rc) return rc;
+            base = c->xm;
+            bias = f(L.mproj_b);
+            parts = c->p_mlp;
+            np = n_sl;
+        }
+        if ((rc = hip_status(gpt2_resid_launch(base, bias, parts, np, c->x, E, c->n_seq, st)))) return rc;
+        if (m->last) {
+            if ((rc = fused_matvec(c, m->lm_head, c->x, c->logits, &m->ln_f_g, &m->ln_f_b, nullptr, EPI_ARGMAX, st))) return rc;
+            return hip_status(gpt2_argmax_launch(c->amax_v, c->amax_i, c->n_seq, c->tokens, c->pos, st));
+        }
+        return hip_status(gpt2_advance_launch(c->pos, c->n_seq, st));
+    }
     for (int l = m->l0; l < m->l1; ++l) {
         const Layer &L = m->layers[l - m->l0];
         float *kc = c->kc + (size_t)(l - m->l0) * cache_layer;
@@ -402,7 +451,12 @@ int ggml_mi355x_gpt2_ctx_init(ggml_mi355x_gpt2_model *m, int32_t n_seq, ggml_mi3
     const size_t b_cache = al(4 * n_layers * S * hp.n_ctx * E);
     const size_t b_amax = m->last ? al(4 * S * ARGMAX_SLOTS) : 0;
     const size_t b_part = al(4 * S * hp.n_head * ATTN_SPLITS * ATTN_PART_STRIDE);
-    const size_t total = 2 * b_tok + 2 * b_x + b_qkv + b_h + b_logits + 2 * b_cache + 2 * b_amax + b_part;
+    // GGML_MI355X_GPT2_BLOCK=0 selects the five-launch layer (A/B and fallback)
+    const char *benv = getenv("GGML_MI355X_GPT2_BLOCK");
+    const bool block = gpt2_block_supported(hp.n_embd, hp.n_head) && !(benv && atoi(benv) == 0);
+    const size_t b_pa = block ? al(4 * S * E * hp.n_head) : 0, b_pm = block ? al(4 * S * E * gpt2_block_mlp_slices(hp.n_embd)) : 0;
+    const size_t b_xb = block ? b_x : 0;
+    const size_t total = 2 * b_tok + 2 * b_x + b_qkv + b_h + b_logits + 2 * b_cache + 2 * b_amax + b_part + 2 * b_xb + b_pa + b_pm;
     if (mmvq_fused_prepare(m->wtype) != hipSuccess) return GGML_MI355X_EHIP;   // before any capture
     auto *c = new ggml_mi355x_gpt2_ctx();
     c->m = m;
@@ -423,6 +477,13 @@ int ggml_mi355x_gpt2_ctx_init(ggml_mi355x_gpt2_model *m, int32_t n_seq, ggml_mi3
     c->kc = reinterpret_cast<float *>(take(b_cache));
     c->vc = reinterpret_cast<float *>(take(b_cache));
     c->part = reinterpret_cast<float *>(take(b_part));
+    c->block = block;
+    if (block) {
+        c->xr = reinterpret_cast<float *>(take(b_xb));
+        c->xm = reinterpret_cast<float *>(take(b_xb));
+        c->p_attn = reinterpret_cast<float *>(take(b_pa));
+        c->p_mlp = reinterpret_cast<float *>(take(b_pm));
+    }
     if (m->last) {
         c->amax_v = reinterpret_cast<float *>(take(b_amax));
         c->amax_i = reinterpret_cast<int32_t *>(take(b_amax));

@@ -478,7 +478,7 @@ __device__ __forceinline__ void layer_norm_cols(const MmArgs &a, int kb0, float4
             red[wave][m][1] = s2;
         }
     }
-    __syncthreads();
+    lds_barrier();   // weights stay in flight
 #pragma unroll
     for (int m = 0; m < NC; ++m) {
         float t1 = 0.f, t2 = 0.f;
@@ -758,7 +758,7 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
         }
     }
     if (wstamp) wst[2] = __builtin_amdgcn_s_memrealtime();   // quantized, at the barrier
-    __syncthreads();
+    lds_barrier();
     if (stamp) a.stamps[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
 
     float acc[V];

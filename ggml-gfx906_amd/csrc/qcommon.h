@@ -116,6 +116,15 @@ template <> __device__ __forceinline__ float xchg<4>(float v) { return dpp_f<DPP
 template <> __device__ __forceinline__ float xchg<2>(float v) { return dpp_f<DPP_XOR2>(v); }
 template <> __device__ __forceinline__ float xchg<1>(float v) { return dpp_f<DPP_XOR1>(v); }
 
+// Workgroup barrier for LDS hand-offs only: this wave's LDS operations complete, then s_barrier.
+// __syncthreads() is a release/acquire fence at workgroup scope, which also waits for every
+// outstanding global load (vmcnt(0)) — it would drain a weight stream issued ahead of the
+// barrier. No kernel here passes data between waves through global memory.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+}
+
 // full 64-lane sum, result in every lane
 __device__ __forceinline__ float wave_sum(float v) {
     v += xchg<1>(v);
