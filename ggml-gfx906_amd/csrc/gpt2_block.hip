@@ -41,7 +41,8 @@ constexpr int BT = MMVQ_THREADS;           // 512 threads = 8 waves
 constexpr int NW = MMVQ_WAVES;
 constexpr int E_MAX = 1024;                // n_embd bound of these kernels (GPT-2 117M / 345M; wider
                                            // models keep the five-launch layer: one slot pass per row here)
-constexpr int MLP_SLICE = 256;             // hidden units per mlp workgroup (one K-quant super-block)
+constexpr int MLP_SLICE = 128;             // hidden units per mlp workgroup (two whole slots of every type;
+                                           // Q6_K: one 128-half of a super-block)
 
 // LDS bytes of one quantized activation vector of K values (XSmem layout, nc = 1)
 constexpr int xs_bytes(int K) { return K + 4 * (K / 32) * 2 + 4 * (K / 16); }
@@ -72,20 +73,20 @@ struct BlockArgs {
     float *parts_out;                      // [blockIdx.x][n_seq][n_embd]
     int E, n_head, n_seq;
     // diagnostics (GGML_MI355X_STAMPS): s_memrealtime phase stamps of workgroups (x, 0),
-    // slot ((2 * layer + kind) * 64 + x) * 8 + phase; nullptr when off
+    // slot ((2 * layer + kind) * 64 + x) * 16 + phase; nullptr when off
     unsigned long long *stamps;
     int layer;
 };
 
 __device__ __forceinline__ void stamp(const BlockArgs &a, int kind, int phase) {
     if (a.stamps != nullptr && threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 64)
-        a.stamps[((2 * a.layer + kind) * 64 + blockIdx.x) * 8 + phase] = __builtin_amdgcn_s_memrealtime();
+        a.stamps[((2 * a.layer + kind) * 64 + blockIdx.x) * 16 + phase] = __builtin_amdgcn_s_memrealtime();
 }
 // shader-clock stamp (s_memtime) into a free slot: the in-kernel clock is
 // (memtime_end - memtime_start) / (realtime_end - realtime_start) x 100 MHz
 __device__ __forceinline__ void stamp_clk(const BlockArgs &a, int kind, int slot) {
     if (a.stamps != nullptr && threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 64)
-        a.stamps[((2 * a.layer + kind) * 64 + blockIdx.x) * 8 + slot] = __builtin_amdgcn_s_memtime();
+        a.stamps[((2 * a.layer + kind) * 64 + blockIdx.x) * 16 + slot] = __builtin_amdgcn_s_memtime();
 }
 
 // The residual of sequence s: rows (base[s], bias, parts[0][s], parts[1][s], ...) summed. All
@@ -94,11 +95,12 @@ __device__ __forceinline__ void stamp_clk(const BlockArgs &a, int kind, int slot
 // G * RROWS rows; each thread sums its rows in order, the row groups meet in LDS and are
 // summed in order rg = 0 .. G-1. The order depends only on (E, number of rows): the resid
 // kernel and every prologue give bit-identical x for the same inputs.
-constexpr int RROWS = 5;                   // rows per thread: one issue round covers G * RROWS rows
+constexpr int RROWS = 6;                   // max rows per thread: one issue round covers G * RR rows
 constexpr int RED_FLOATS = 4096;           // LDS floats of the row-group partials (G * E <= 4096)
 
+template <int RR>
 struct Resid {
-    float4 v[RROWS][2];
+    float4 v[RR][2];
 };
 
 __device__ __forceinline__ int resid_rows(const BlockArgs &a) { return 1 + (a.bias_in != nullptr) + a.n_parts_in; }
@@ -112,26 +114,28 @@ __device__ __forceinline__ const float *resid_row(const BlockArgs &a, int s, int
     return r == 0 ? a.base + (int64_t)s * a.E : p;
 }
 
-__device__ __forceinline__ void resid_issue(const BlockArgs &a, int s, int round, Resid &R) {
+template <int RR>
+__device__ __forceinline__ void resid_issue(const BlockArgs &a, int s, int round, Resid<RR> &R) {
     const int nch = a.E / 8, G = BT / nch;
     const int c = (int)threadIdx.x % nch, rg = min((int)threadIdx.x / nch, G - 1);
     const int nrows = resid_rows(a);
 #pragma unroll
-    for (int i = 0; i < RROWS; ++i) {
-        const int r = min(rg + G * (round * RROWS + i), nrows - 1);
+    for (int i = 0; i < RR; ++i) {
+        const int r = min(rg + G * (round * RR + i), nrows - 1);
         const float *p = resid_row(a, s, r) + 8 * c;
         R.v[i][0] = reinterpret_cast<const float4 *>(p)[0];
         R.v[i][1] = reinterpret_cast<const float4 *>(p)[1];
     }
 }
 
-__device__ __forceinline__ void resid_accum(const BlockArgs &a, int round, const Resid &R, float4 &s0, float4 &s1) {
+template <int RR>
+__device__ __forceinline__ void resid_accum(const BlockArgs &a, int round, const Resid<RR> &R, float4 &s0, float4 &s1) {
     const int nch = a.E / 8, G = BT / nch;
     const int rg = (int)threadIdx.x / nch;
     const int nrows = resid_rows(a);
 #pragma unroll
-    for (int i = 0; i < RROWS; ++i) {
-        if (rg < G && rg + G * (round * RROWS + i) < nrows) {
+    for (int i = 0; i < RR; ++i) {
+        if (rg < G && rg + G * (round * RR + i) < nrows) {
             s0.x += R.v[i][0].x; s0.y += R.v[i][0].y; s0.z += R.v[i][0].z; s0.w += R.v[i][0].w;
             s1.x += R.v[i][1].x; s1.y += R.v[i][1].y; s1.z += R.v[i][1].z; s1.w += R.v[i][1].w;
         }
@@ -142,7 +146,8 @@ __device__ __forceinline__ void resid_accum(const BlockArgs &a, int round, const
 // finish: the loads R were issued by the caller (before its weight stream); the host
 // guarantees one round covers every row (gpt2_block_supported). Thread t < E/8 returns
 // x[8t .. 8t+8) (others zeros). Contains a workgroup barrier.
-__device__ __forceinline__ void resid_finish(const BlockArgs &a, int s, const Resid &R0, float *red, float4 &x0, float4 &x1) {
+template <int RR>
+__device__ __forceinline__ void resid_finish(const BlockArgs &a, int s, const Resid<RR> &R0, float *red, float4 &x0, float4 &x1) {
     const int nch = a.E / 8, G = BT / nch;
     const int c = (int)threadIdx.x % nch, rg = (int)threadIdx.x / nch;
     float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
@@ -210,8 +215,10 @@ struct RowsDot {
     template <class Out>
     __device__ __forceinline__ void compute(const XSmem &sm, int Kpad, int nrows, Out out) const {
         constexpr int NX = XdCount<T>::n;
-        constexpr int V = LPR == 1 ? RPW : pow2ceil(RPW);
-        static_assert(LPR == 1 || V <= LPR, "RPW partial sums must fit the lanes of a row");
+        // V <= LPR: butterfly transpose (one row's sum per lane); otherwise (few lanes per row)
+        // every row is summed over its LPR lanes and the row's first lane stores them all
+        constexpr bool TRANSPOSE = LPR > 1 && pow2ceil(RPW) <= LPR;
+        constexpr int V = TRANSPOSE ? pow2ceil(RPW) : RPW;
         const int lane = threadIdx.x & 63, sl = lane % LPR;
         const int nslots = Kpad / 64;
         float acc[V];
@@ -244,10 +251,19 @@ struct RowsDot {
 #pragma unroll
             for (int r = 0; r < RPW; ++r) acc[r] += live * f[it][r].dot(X, dx, sx);
         }
-        if constexpr (LPR == 1) {
+        if constexpr (!TRANSPOSE) {
 #pragma unroll
-            for (int r = 0; r < RPW; ++r)
-                if (r0 + r < nrows) out(r0 + r, acc[r]);
+            for (int r = 0; r < RPW; ++r) {
+                if constexpr (LPR >= 2) acc[r] += xchg<1>(acc[r]);
+                if constexpr (LPR >= 4) acc[r] += xchg<2>(acc[r]);
+                if constexpr (LPR >= 8) acc[r] += xchg<4>(acc[r]);
+                if constexpr (LPR >= 16) acc[r] += xchg<8>(acc[r]);
+            }
+            if (sl == 0) {
+#pragma unroll
+                for (int r = 0; r < RPW; ++r)
+                    if (r0 + r < nrows) out(r0 + r, acc[r]);
+            }
         } else {
             const float sum = group_reduce_transpose<V, LPR>(acc);
             constexpr int SHIFT = Log2<LPR>::v - Log2<V>::v;
@@ -287,7 +303,7 @@ __device__ __forceinline__ void load_ln(const float *gp, const float *bp, int E,
 constexpr int AGROUPS = NW * 4;            // 16-lane key groups per workgroup
 constexpr int AU = 8;                      // keys per group in flight per round
 
-template <int T, int QNIT>
+template <int T, int QNIT, int RR>
 __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
     __shared__ __align__(16) uint8_t lds_x[xs_bytes(E_MAX)];   // LN1(x), quantized
     __shared__ __align__(16) uint8_t lds_o[xs_bytes(E_MAX)];   // head h's attention output, quantized
@@ -303,7 +319,7 @@ __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
     stamp(a, 0, 0);
 
     // ---- issue: residual rows, LN params, q/k/v bias, position; then the qkv weight stream
-    Resid R0;
+    Resid<RR> R0;
     resid_issue(a, s, 0, R0);
     float4 g[1][2], bb[1][2];
     load_ln(a.ln_g, a.ln_b, E, g, bb);
@@ -313,6 +329,13 @@ __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
     RowsDot<T, 16, 6, QNIT> qd;
     qd.load([&](int vr) { return a.w_qkv + (int64_t)((vr >> 6) * E + h * HD + (vr & 63)) * a.nb_qkv; }, 3 * HD, 0, 0, E / 64);
     __builtin_amdgcn_sched_barrier(0);
+    stamp(a, 0, 8);
+    if (a.stamps != nullptr) {   // diagnostics: when this wave's first residual row has landed
+        float probe = R0.v[0][0].x;
+        asm volatile("" : "+v"(probe));
+        if (probe == 1.2345e-30f) stamp(a, 0, 10);
+        stamp(a, 0, 9);
+    }
 
     if (tid < 3 * HD) qb_s[tid] = qb;
     for (int i = tid; i < xs_bytes(E) / 4; i += BT) reinterpret_cast<uint32_t *>(lds_o)[i] = 0u;   // c_proj K-split: zeros outside head h
@@ -432,7 +455,7 @@ __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
 // ------------------------------------------------------------------------------------------
 // MLP block: grid (4 n_embd / MLP_SLICE, n_seq)
 // ------------------------------------------------------------------------------------------
-template <int T, int FNIT>
+template <int T, int FNIT, int RR>
 __global__ __launch_bounds__(BT) void mlp_block_kernel(const BlockArgs a) {
     __shared__ __align__(16) uint8_t lds_x[xs_bytes(E_MAX)];       // LN2(y), quantized
     __shared__ __align__(16) uint8_t lds_h[xs_bytes(4 * E_MAX)];   // slice j of gelu(fc), quantized (K = 4E)
@@ -445,14 +468,15 @@ __global__ __launch_bounds__(BT) void mlp_block_kernel(const BlockArgs a) {
     stamp(a, 1, 0);
     stamp_clk(a, 1, 6);
 
-    Resid R0;
+    Resid<RR> R0;
     resid_issue(a, s, 0, R0);
     float4 g[1][2], bb[1][2];
     load_ln(a.ln_g, a.ln_b, E, g, bb);
     const float fb = a.b_fc[j * MLP_SLICE + min(tid, MLP_SLICE - 1)];
-    RowsDot<T, 16, 8, FNIT> fd;
+    RowsDot<T, 16, MLP_SLICE / 32, FNIT> fd;
     fd.load([&](int r) { return a.w_fc + (int64_t)(j * MLP_SLICE + r) * a.nb_fc; }, MLP_SLICE, 0, 0, E / 64);
     __builtin_amdgcn_sched_barrier(0);
+    stamp(a, 1, 8);
 
     if (tid < MLP_SLICE) fb_s[tid] = fb;
     float4 xa[1][1], xb[1][1];
@@ -462,15 +486,22 @@ __global__ __launch_bounds__(BT) void mlp_block_kernel(const BlockArgs a) {
     ln_quantize<T>(a, xa, xb, g, bb, sx, resid_first(a, red));
     stamp(a, 1, 2);
 
+    if (a.stamps != nullptr) {   // diagnostics: this wave's fc weights have landed
+        uint32_t probe = reinterpret_cast<const uint32_t *>(&fd.f[0][MLP_SLICE / 32 - 1])[0];
+        asm volatile("" : "+v"(probe));
+        if (probe == 0x12345u && threadIdx.x == 999) stamp(a, 1, 10);
+        stamp(a, 1, 9);
+    }
     fd.compute(sx, E, MLP_SLICE, [&](int r, float v) { h_s[r] = gelu_ggml(v + fb_s[r]); });
+    stamp(a, 1, 11);
 
-    // mlp proj K-split weights: slots [4j, 4j+4) of every row (the slice's 256 columns)
+    // mlp proj K-split weights: slots [SL j, SL j + SL) of every row (the slice's columns); one
+    // pass covers 8 waves x 32 x 3 = 768 rows
     constexpr int SL = MLP_SLICE / 64;
-    using MD = RowsDot<T, SL, 4, 1>;
-    MD md0, md1;
+    using MD = RowsDot<T, SL, 3, 1>;
+    MD md0;
     auto mrow = [&](int r) { return a.w_mp + (int64_t)r * a.nb_mp; };
     md0.load(mrow, E, 0, SL * j, SL);
-    md1.load(mrow, E, MD::RPP, SL * j, SL);
     stamp(a, 1, 3);
     lds_barrier();
     if (tid < MLP_SLICE / 8) {
@@ -485,8 +516,7 @@ __global__ __launch_bounds__(BT) void mlp_block_kernel(const BlockArgs a) {
     float *po = a.parts_out + ((int64_t)j * a.n_seq + s) * E;
     auto out = [&](int r, float v) { po[r] = v; };
     md0.compute(sh, 4 * E, E, out);
-    md1.compute(sh, 4 * E, E, out);
-    for (int base = 2 * MD::RPP; base < E; base += MD::RPP) {
+    for (int base = MD::RPP; base < E; base += MD::RPP) {
         MD mdn;
         mdn.load(mrow, E, base, SL * j, SL);
         mdn.compute(sh, 4 * E, E, out);
@@ -496,25 +526,32 @@ __global__ __launch_bounds__(BT) void mlp_block_kernel(const BlockArgs a) {
 }
 
 // x_out = base + bias + sum parts (the residual leaving a stage): grid (n_seq)
+template <int RR>
 __global__ __launch_bounds__(BT) void resid_kernel(const BlockArgs a) {
     __shared__ __align__(16) float red[RED_FLOATS];
-    Resid R0;
+    Resid<RR> R0;
     resid_issue(a, blockIdx.x, 0, R0);
     float4 v0, v1;
     resid_finish(a, blockIdx.x, R0, red, v0, v1);
     store_resid(a, blockIdx.x, v0, v1);
 }
 
-template <int T, int NIT>
+// residual rows per thread of one issue round (3 covers GPT-2 117M: 14 rows over 5 row groups)
+int resid_rr(const BlockArgs &a) {
+    const int G = BT / (a.E / 8);
+    return (1 + (a.bias_in != nullptr) + a.n_parts_in + G - 1) / G <= 3 ? 3 : RROWS;   // 117M: 26 rows -> 6
+}
+
+template <int T, int RR>
 hipError_t launch_pair(bool attn, const BlockArgs &a, hipStream_t st) {
-    if (attn) hipLaunchKernelGGL((attn_block_kernel<T, NIT>), dim3(a.n_head, a.n_seq), dim3(BT), 0, st, a);
-    else hipLaunchKernelGGL((mlp_block_kernel<T, NIT>), dim3(4 * a.E / MLP_SLICE, a.n_seq), dim3(BT), 0, st, a);
+    if (attn) hipLaunchKernelGGL((attn_block_kernel<T, 1, RR>), dim3(a.n_head, a.n_seq), dim3(BT), 0, st, a);
+    else hipLaunchKernelGGL((mlp_block_kernel<T, 1, RR>), dim3(4 * a.E / MLP_SLICE, a.n_seq), dim3(BT), 0, st, a);
     return hipGetLastError();
 }
 
 template <int T>
 hipError_t launch_type(bool attn, const BlockArgs &a, hipStream_t st) {
-    return launch_pair<T, 1>(attn, a, st);
+    return resid_rr(a) == 3 ? launch_pair<T, 3>(attn, a, st) : launch_pair<T, RROWS>(attn, a, st);
 }
 
 hipError_t launch_block(int type, bool attn, const BlockArgs &a, hipStream_t st) {
@@ -577,7 +614,8 @@ hipError_t gpt2_resid_launch(const float *base, const float *bias_in, const floa
     BlockArgs a{};
     a.base = base; a.bias_in = bias_in; a.parts_in = parts_in; a.n_parts_in = parts_in ? n_parts_in : 0;
     a.x_out = x_out; a.E = E; a.n_seq = n_seq;
-    hipLaunchKernelGGL(resid_kernel, dim3(n_seq), dim3(BT), 0, st, a);
+    if (resid_rr(a) == 3) hipLaunchKernelGGL(resid_kernel<3>, dim3(n_seq), dim3(BT), 0, st, a);
+    else hipLaunchKernelGGL(resid_kernel<RROWS>, dim3(n_seq), dim3(BT), 0, st, a);
     return hipGetLastError();
 }
 

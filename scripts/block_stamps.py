@@ -29,11 +29,13 @@ L.ggml_mi355x_debug_stamps.argtypes = [C.c_void_p, C.c_size_t]
 NL = hp["n_layer"]
 NWG = [hp["n_head"], 4 * hp["n_embd"] // 256]
 NPH = [7, 6]
-buf = np.zeros(2 * NL * 64 * 8, np.uint64)
+buf = np.zeros(2 * NL * 64 * 16, np.uint64)
 ph = {0: [], 1: []}
 spans = {0: [], 1: []}
 gaps = []
 clk = []
+extra = []
+extra1 = []
 with torch.cuda.stream(s):
     z = torch.full((1,), pos0, dtype=torch.int32, device="cuda")
     c.set_pos(z.data_ptr(), s.cuda_stream)
@@ -44,11 +46,15 @@ with torch.cuda.stream(s):
         if step < 4:
             continue
         L.ggml_mi355x_debug_stamps(buf.ctypes.data, buf.size)
-        t = buf.reshape(NL, 2, 64, 8).astype(np.int64)
+        t = buf.reshape(NL, 2, 64, 16).astype(np.int64)
         prev_end = None
         for layer in range(NL):
             for k in (0, 1):
                 w = t[layer, k, :NWG[k], :NPH[k]]
+                if k == 0:
+                    extra.append((t[layer, 0, :NWG[0], 8:10] - t[layer, 0, :NWG[0], 0:1]) * 10)
+                else:
+                    extra1.append((t[layer, 1, :NWG[1]][:, [8, 9, 11]] - t[layer, 1, :NWG[1], 0:1]) * 10)
                 start = w[:, 0:1]
                 ph[k].append((w - start) * 10)
                 spans[k].append((w[:, NPH[k] - 1].max() - w[:, 0].min()) * 10)
@@ -71,3 +77,7 @@ for k, nm in ((0, "attn block"), (1, "mlp block")):
         print(f"   {n:16s} +{med[i]:7.0f} ns (p90 {p90[i]:7.0f})")
 print(f"kernel gaps (last end -> next first start): median {np.median(gaps):.0f} ns, p90 {np.percentile(gaps, 90):.0f}")
 print(f"in-kernel shader clock (mlp block, s_memtime / s_memrealtime): median {np.median(clk):.0f} MHz")
+ex = np.median(np.concatenate(extra), axis=0)
+print(f"attn block: loads issued +{ex[0]:.0f} ns, wave 0's first residual row landed +{ex[1]:.0f} ns")
+ex = np.median(np.concatenate(extra1), axis=0)
+print(f"mlp block: loads issued +{ex[0]:.0f} ns, wave 0's fc weights landed +{ex[1]:.0f} ns, fc computed (wave 0) +{ex[2]:.0f} ns")

@@ -10,7 +10,11 @@ printable ASCII characters, the rest "<tN>") makes that text parse back into ids
   * CPU: oracle/gpt2_ref (our restatement of the example's graph on the reference ggml, which
     the golden logits come from) teacher-forced with the example's own stream must put its
     argmax on every token the example chose — this pins the restatement to the example.
-  * GPU: the MI355X engine's device-resident greedy loop must generate the example's stream.
+  * GPU: the MI355X engine's device-resident greedy loop must generate the example's stream,
+    up to near-ties: the engine quantizes activations per 32 values (the reference's GPU form),
+    while ggml-cpu uses 256-value Q8_K blocks for K-quant weights, so the two sit ~1e-3 NMSE
+    apart (the bar of test_gpt2.py). Where the streams first differ, the reference's own logits
+    must rank the two candidates within TIE_SIGMA standard errors of that noise.
 """
 import json
 import os
@@ -31,6 +35,8 @@ MANIFEST = json.load(open(os.path.join(ROOT, "tests", "golden", "gpt2_manifest.j
 SMALL = MANIFEST["hparams"]
 PROMPT = "This is an example"   # main-sched.cpp's own default prompt in the README runs
 N_NEW = 24
+NMSE_VS_REF = 1e-3                # engine vs ggml-cpu logits (test_gpt2.py)
+TIE_SIGMA = 3.0
 
 needs_example = pytest.mark.skipif(not (os.path.exists(EXAMPLE) and os.path.exists(REF_BIN)),
                                    reason="oracle/_ref not built (make -f oracle/ref.mk)")
@@ -74,19 +80,40 @@ def test_parse_generated():
     assert parse_generated(out, "ab") == [145, ord("c") - 32, 7]
 
 
-@needs_example
-@pytest.mark.parametrize("name", ["q4_0", "q4_K", "q6_K"])
-def test_gpt2_ref_pinned_to_reference_example(name):
-    path, prompt, gen = model_and_stream(name)
-    seq = prompt + gen
+def reference_logits(path: str, seq: list) -> np.ndarray:
+    """gpt2_ref teacher-forced on seq[:-1]: row i = the logits that predict seq[i + 1]"""
     out = path + ".logits"
     subprocess.run([REF_BIN, path, "--tokens", ",".join(map(str, seq[:-1])), "--out", out, "--threads", "4"], check=True,
                    capture_output=True, timeout=300)
     logits = np.fromfile(out, np.float32).reshape(len(seq) - 1, SMALL["n_vocab"])
     os.remove(out)
+    return logits
+
+
+@needs_example
+@pytest.mark.parametrize("name", ["q4_0", "q4_K", "q6_K"])
+def test_gpt2_ref_pinned_to_reference_example(name):
+    path, prompt, gen = model_and_stream(name)
+    logits = reference_logits(path, prompt + gen)
     # position i predicts token i + 1; the example sampled from the last prompt position on
     got = logits[len(prompt) - 1:].argmax(1).tolist()
     assert got == gen
+
+
+def test_near_tie_rule():
+    """the divergence rule accepts a flip inside the noise bound and nothing else"""
+    lg = np.zeros((1, 8), np.float32)
+    lg[0, :] = np.linspace(-1, 1, 8)
+    lg[0, 3] = 1.0 - 1e-3
+    assert near_tie(lg[0], want=7, got=3)
+    assert not near_tie(lg[0], want=7, got=0)
+
+
+def near_tie(ref_row: np.ndarray, want: int, got: int) -> bool:
+    """the reference ranks `want` over `got` by less than TIE_SIGMA standard errors of the
+    engine's logit noise (per-logit RMS error sqrt(NMSE_VS_REF) x RMS of the row)"""
+    noise = np.sqrt(NMSE_VS_REF * np.mean(ref_row.astype(np.float64) ** 2))
+    return float(ref_row[want] - ref_row[got]) <= TIE_SIGMA * noise
 
 
 @pytest.mark.gpu
@@ -102,4 +129,8 @@ def test_engine_greedy_matches_reference_example(name):
     got = G.greedy_generate(ctx, [prompt], N_NEW)[0]
     ctx.free()
     st.free()
-    assert got == gen
+    if got == gen:
+        return
+    i = next(k for k in range(N_NEW) if got[k] != gen[k])
+    ref = reference_logits(path, prompt + gen)[len(prompt) - 1 + i]
+    assert near_tie(ref, gen[i], got[i]), (i, got, gen, float(ref[gen[i]] - ref[got[i]]))
