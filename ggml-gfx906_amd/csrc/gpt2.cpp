@@ -51,6 +51,9 @@ hipError_t gpt2_mlp_block_launch(int layer, int type, const float *base, const f
                                  float *x_out, const float *ln_g, const float *ln_b, float eps, const uint8_t *w_fc,
                                  int64_t nb_fc, const float *b_fc, const uint8_t *w_mp, int64_t nb_mp, float *parts_out, int E,
                                  int n_head, int n_seq, hipStream_t st);
+bool gpt2_block_repacks(int type);
+hipError_t gpt2_block_repack(int type, int E, const uint8_t *w_o, uint8_t *o_dst, const uint8_t *w_mp, uint8_t *mp_dst,
+                             size_t *o_bytes, size_t *mp_bytes, hipStream_t st);
 hipError_t gpt2_resid_launch(const float *base, const float *bias_in, const float *parts_in, int n_parts_in, float *x_out, int E,
                              int n_seq, hipStream_t st);
 }  // namespace mi355x
@@ -120,6 +123,10 @@ struct ggml_mi355x_gpt2_ctx {
     // and the K-split partial slabs [split][seq][n_embd] of c_proj (per head) and the MLP proj
     bool block = false;
     float *xr = nullptr, *xm = nullptr, *p_attn = nullptr, *p_mlp = nullptr;
+    // 32-block types: per layer, head-major c_proj and slice-major MLP projection copies
+    // (gpt2_block_repack), made from the model's weights when the context is created
+    uint8_t *rep = nullptr;
+    std::vector<const uint8_t *> rep_o, rep_mp;
     std::map<hipStream_t, hipGraphExec_t> graphs;
 };
 
@@ -204,13 +211,16 @@ int run_step(ggml_mi355x_gpt2_ctx *c, hipStream_t st) {
             float *kc = c->kc + (size_t)(l - m->l0) * cache_layer;
             float *vc = c->vc + (size_t)(l - m->l0) * cache_layer;
             auto f = [](const Tensor &t) { return reinterpret_cast<const float *>(t.data); };
+            const bool rp = c->rep != nullptr;
             rc = hip_status(gpt2_attn_block_launch(l - m->l0, m->wtype, base, bias, parts, np, c->xr, f(L.ln1_g), f(L.ln1_b), 1e-5f, L.attn_w.data,
                                                    row_bytes(m->wtype, E), f(L.attn_b), kc, vc, c->pos, kq_scale, hp.n_ctx,
-                                                   L.proj_w.data, row_bytes(m->wtype, E), c->p_attn, E, hp.n_head, c->n_seq, st));
+                                                   rp ? c->rep_o[l - m->l0] : L.proj_w.data, row_bytes(m->wtype, E), c->p_attn, E,
+                                                   hp.n_head, c->n_seq, st));
             if (rc) return rc;
             rc = hip_status(gpt2_mlp_block_launch(l - m->l0, m->wtype, c->xr, f(L.proj_b), c->p_attn, hp.n_head, c->xm, f(L.ln2_g), f(L.ln2_b),
-                                                  1e-5f, L.fc_w.data, row_bytes(m->wtype, E), f(L.fc_b), L.mproj_w.data,
-                                                  row_bytes(m->wtype, 4 * E), c->p_mlp, E, hp.n_head, c->n_seq, st));
+                                                  1e-5f, L.fc_w.data, row_bytes(m->wtype, E), f(L.fc_b),
+                                                  rp ? c->rep_mp[l - m->l0] : L.mproj_w.data, row_bytes(m->wtype, 4 * E), c->p_mlp, E,
+                                                  hp.n_head, c->n_seq, st));
             if (rc) return rc;
             base = c->xm;
             bias = f(L.mproj_b);
@@ -494,6 +504,29 @@ int ggml_mi355x_gpt2_ctx_init(ggml_mi355x_gpt2_model *m, int32_t n_seq, ggml_mi3
         delete c;
         return GGML_MI355X_EHIP;
     }
+    if (block && gpt2_block_repacks(m->wtype)) {
+        size_t ob = 0, mb = 0;
+        (void)gpt2_block_repack(m->wtype, hp.n_embd, nullptr, nullptr, nullptr, nullptr, &ob, &mb, nullptr);
+        if (hipMalloc(&c->rep, (ob + mb) * n_layers) != hipSuccess) {
+            (void)hipFree(c->arena);
+            delete c;
+            return GGML_MI355X_ENOMEM;
+        }
+        for (size_t l = 0; l < n_layers; ++l) {
+            uint8_t *o = c->rep + l * (ob + mb), *mp = o + ob;
+            const Layer &L = m->layers[l];
+            if (gpt2_block_repack(m->wtype, hp.n_embd, L.proj_w.data, o, L.mproj_w.data, mp, nullptr, nullptr, nullptr) != hipSuccess) {
+                ggml_mi355x_gpt2_ctx_free(c);
+                return GGML_MI355X_EHIP;
+            }
+            c->rep_o.push_back(o);
+            c->rep_mp.push_back(mp);
+        }
+        if (hipDeviceSynchronize() != hipSuccess) {
+            ggml_mi355x_gpt2_ctx_free(c);
+            return GGML_MI355X_EHIP;
+        }
+    }
     *out = c;
     return GGML_MI355X_OK;
 }
@@ -535,6 +568,7 @@ void ggml_mi355x_gpt2_ctx_free(ggml_mi355x_gpt2_ctx *c) {
     if (!c) return;
     for (auto &kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
     if (c->arena) (void)hipFree(c->arena);
+    if (c->rep) (void)hipFree(c->rep);
     delete c;
 }
 

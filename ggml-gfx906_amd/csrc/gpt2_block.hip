@@ -44,6 +44,11 @@ constexpr int E_MAX = 1024;                // n_embd bound of these kernels (GPT
 constexpr int MLP_SLICE = 128;             // hidden units per mlp workgroup (two whole slots of every type;
                                            // Q6_K: one 128-half of a super-block)
 
+// 32-block types: the engine repacks c_proj and the MLP projection into head- / slice-major
+// copies whose K-splits are contiguous (gpt2.cpp, gpt2_block_repack); K-quant slots are not
+// contiguous byte ranges (header + chunk), so those read the ggml rows in place
+template <int T> constexpr bool REPACK = T == T_Q4_0 || T == T_Q8_0;
+
 // LDS bytes of one quantized activation vector of K values (XSmem layout, nc = 1)
 constexpr int xs_bytes(int K) { return K + 4 * (K / 32) * 2 + 4 * (K / 16); }
 
@@ -198,15 +203,17 @@ struct RowsDot {
     Frag<T> f[NIT][RPW];
     int r0, s0, ns;
 
+    // s0_: first activation slot; ws0: first slot within the weight row (the same unless the
+    // rows are a repacked slice, which starts at slot 0)
     template <class RowPtr>
-    __device__ __forceinline__ void load(RowPtr rowptr, int nrows, int base, int s0_, int ns_) {
+    __device__ __forceinline__ void load(RowPtr rowptr, int nrows, int base, int s0_, int ns_, int ws0 = -1) {
         const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, sl = lane % LPR;
         s0 = s0_;
         ns = ns_;
         r0 = base + wave * (WAVE / LPR) * RPW + (lane / LPR) * RPW;
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
-            const int s = s0 + min(sl + it * LPR, ns - 1);
+            const int s = (ws0 < 0 ? s0 : ws0) + min(sl + it * LPR, ns - 1);
 #pragma unroll
             for (int r = 0; r < RPW; ++r) f[it][r].template load<false>(rowptr(min(r0 + r, nrows - 1)), s, 0);
         }
@@ -403,11 +410,17 @@ __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
     reinterpret_cast<float4 *>(go[grp])[d4] = o4;
     if (d4 == 0) { gm[grp] = m; gl[grp] = l; }
 
-    // c_proj K-split weights: the slots holding head h's 64 columns (Q6_K: halves of two slots)
+    // c_proj K-split weights: the slots holding head h's 64 columns (Q6_K: halves of two slots).
+    // Q4_0 / Q8_0: the engine's head-major copy [head][row][one slot] (gpt2.cpp), a contiguous
+    // stream; K-quants read the ggml rows in place
     constexpr int OLPR = T == T_Q6_K ? 2 : 1;
     const int os0 = T == T_Q6_K ? 4 * (h >> 2) + 2 * ((h & 3) >> 1) : h;
+    const int ows0 = REPACK<T> ? 0 : -1;
+    auto orow = [&](int r) {
+        return REPACK<T> ? a.w_o + ((int64_t)h * E + r) * (2 * QT<T>::bytes) : a.w_o + (int64_t)r * a.nb_o;
+    };
     RowsDot<T, OLPR, 2, 1> od0;
-    od0.load([&](int r) { return a.w_o + (int64_t)r * a.nb_o; }, E, 0, os0, OLPR);
+    od0.load(orow, E, 0, os0, OLPR, ows0);
     stamp(a, 0, 4);
     lds_barrier();
 
@@ -429,13 +442,13 @@ __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
 #pragma unroll
         for (int w = 0; w < AGROUPS; ++w) O += gw_s[w] * go[w][lane];
         o_s[lane] = O / L;
-    }
-    lds_barrier();
-    if (tid < 8) {
-        const int q0 = (tid >> 2) * 32 + (tid & 3) * 8;
-        const float4 v0 = reinterpret_cast<const float4 *>(o_s + q0)[0];
-        const float4 v1 = reinterpret_cast<const float4 *>(o_s + q0)[1];
-        xblock_store<T>(E, 2 * h + (tid >> 2), v0, v1, so.xq, so.xd, so.xs, so.x16);
+        // quantize o (blocks 2h, 2h+1) in the same wave: its LDS accesses run in order
+        if (lane < 8) {
+            const int q0 = (lane >> 2) * 32 + (lane & 3) * 8;
+            const float4 v0 = reinterpret_cast<const float4 *>(o_s + q0)[0];
+            const float4 v1 = reinterpret_cast<const float4 *>(o_s + q0)[1];
+            xblock_store<T>(E, 2 * h + (lane >> 2), v0, v1, so.xq, so.xd, so.xs, so.x16);
+        }
     }
     lds_barrier();
     stamp(a, 0, 5);
@@ -446,7 +459,7 @@ __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
     od0.compute(so, E, E, out);
     for (int base = RowsDot<T, OLPR, 2, 1>::RPP; base < E; base += RowsDot<T, OLPR, 2, 1>::RPP) {
         RowsDot<T, OLPR, 2, 1> odn;
-        odn.load([&](int r) { return a.w_o + (int64_t)r * a.nb_o; }, E, base, os0, OLPR);
+        odn.load(orow, E, base, os0, OLPR, ows0);
         odn.compute(so, E, E, out);
     }
     stamp(a, 0, 6);
@@ -500,8 +513,12 @@ __global__ __launch_bounds__(BT) void mlp_block_kernel(const BlockArgs a) {
     constexpr int SL = MLP_SLICE / 64;
     using MD = RowsDot<T, SL, 3, 1>;
     MD md0;
-    auto mrow = [&](int r) { return a.w_mp + (int64_t)r * a.nb_mp; };
-    md0.load(mrow, E, 0, SL * j, SL);
+    // Q4_0 / Q8_0: the engine's slice-major copy [slice][row][SL slots] (a contiguous stream)
+    const int mws0 = REPACK<T> ? 0 : -1;
+    auto mrow = [&](int r) {
+        return REPACK<T> ? a.w_mp + ((int64_t)j * E + r) * (SL * 2 * QT<T>::bytes) : a.w_mp + (int64_t)r * a.nb_mp;
+    };
+    md0.load(mrow, E, 0, SL * j, SL, mws0);
     stamp(a, 1, 3);
     lds_barrier();
     if (tid < MLP_SLICE / 8) {
@@ -518,7 +535,7 @@ __global__ __launch_bounds__(BT) void mlp_block_kernel(const BlockArgs a) {
     md0.compute(sh, 4 * E, E, out);
     for (int base = MD::RPP; base < E; base += MD::RPP) {
         MD mdn;
-        mdn.load(mrow, E, base, SL * j, SL);
+        mdn.load(mrow, E, base, SL * j, SL, mws0);
         mdn.compute(sh, 4 * E, E, out);
     }
     stamp(a, 1, 5);
@@ -576,6 +593,30 @@ bool gpt2_block_supported(int n_embd, int n_head) {
 }
 
 int gpt2_block_mlp_slices(int n_embd) { return 4 * n_embd / MLP_SLICE; }
+
+// head-major c_proj ([head][row][2 blocks]) and slice-major MLP projection
+// ([slice][row][MLP_SLICE / 32 blocks]) copies of one layer, for the 32-block types; bytes of
+// each through *_bytes (dst == nullptr: sizes only)
+bool gpt2_block_repacks(int type) { return type == T_Q4_0 || type == T_Q8_0; }
+
+hipError_t gpt2_block_repack(int type, int E, const uint8_t *w_o, uint8_t *o_dst, const uint8_t *w_mp, uint8_t *mp_dst,
+                             size_t *o_bytes, size_t *mp_bytes, hipStream_t st) {
+    const int bs = type == T_Q4_0 ? QT<T_Q4_0>::bytes : QT<T_Q8_0>::bytes;
+    const size_t wo = 2 * (size_t)bs, wm = (MLP_SLICE / 32) * (size_t)bs;     // bytes of one row's K-split
+    const size_t ro = (size_t)E / 32 * bs, rm = (size_t)4 * E / 32 * bs;     // ggml row bytes
+    if (o_bytes) *o_bytes = wo * E * (E / HD);
+    if (mp_bytes) *mp_bytes = wm * E * (4 * E / MLP_SLICE);
+    if (!o_dst) return hipSuccess;
+    for (int h = 0; h < E / HD; ++h) {
+        const hipError_t e = hipMemcpy2DAsync(o_dst + h * wo * E, wo, w_o + h * wo, ro, wo, E, hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return e;
+    }
+    for (int j = 0; j < 4 * E / MLP_SLICE; ++j) {
+        const hipError_t e = hipMemcpy2DAsync(mp_dst + j * wm * E, wm, w_mp + j * wm, rm, wm, E, hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
 
 hipError_t gpt2_attn_block_launch(int layer, int type, const float *base, const float *bias_in, const float *parts_in, int n_parts_in,
                                   float *x_out, const float *ln_g, const float *ln_b, float eps, const uint8_t *w_qkv,
