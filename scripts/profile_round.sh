@@ -25,14 +25,14 @@ squash() {  # squash <dir>
     for t in $(find $d -name '*kernel_trace.csv'); do python scripts/trace_summary.py $t 2 > ${t%.csv}_summary.txt; rm -f $t; done
     find $d -name '*counter_collection.csv' -size +2M -delete
 }
-step bench 600 python bench.py
+[ -s $O/bench.log ] || step bench 600 python bench.py
 step prof_bench 600 $RP -d $O/bench -o run -- python bench.py --no-extra --cpu-seconds 1
 squash $O/bench
-step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_fetch -o pmc -- python bench.py --no-extra --cpu-seconds 1 --steps 5 --warmup 1
+step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_fetch -o pmc -- python bench.py --no-extra --no-gpt2 --cpu-seconds 1 --steps 5 --warmup 1
 python scripts/traffic_from_pmc.py $(find $O/pmc_fetch -name '*counter_collection.csv' | head -1) $O/traffic.json $R > /dev/null
 python scripts/pmc_summary.py $O/pmc_fetch > $O/pmc_fetch_summary.txt
 squash $O/pmc_fetch
-step pmc_write 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_write -o pmc -- python bench.py --no-extra --cpu-seconds 1 --steps 5 --warmup 1
+step pmc_write 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_write -o pmc -- python bench.py --no-extra --no-gpt2 --cpu-seconds 1 --steps 5 --warmup 1
 python scripts/pmc_summary.py $O/pmc_write > $O/pmc_write_summary.txt
 squash $O/pmc_write
 step prof_singles 300 $RP -d $O/singles -o run -- python scripts/prof_singles.py
