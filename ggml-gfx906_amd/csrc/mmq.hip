@@ -233,14 +233,15 @@ struct MoeMap {
 // One single-wave workgroup per row (spread over every CU, no barrier): up to 4096 values are held in registers,
 // so the row is read once (16 x 16-B loads in flight per lane), its |x|max reduced across the
 // wave, and written as f16 with coalesced 8-B stores. Longer rows are re-read per 4096 chunk.
-constexpr int CVT_R = 16;   // float4 per lane held across the reduction
+constexpr int CVT_T = 256;  // threads per token row (4 waves: 4x the loads in flight of one wave)
+constexpr int CVT_R = 4;    // float4 per lane held across the reduction
 // WAVE (mmq_wave_kernel's operand): values stored in order (0,2,1,3) within each 4 k, and each
 // 16-k group's sum of the prescaled values, x 1/16, into xsum[row][window of 256 k][16] at the
 // slot the kernel's correction fragment reads (see mmq_wave_kernel)
 template <bool WAVE>
-__global__ __launch_bounds__(64) void mmq_convert_x(const MmArgs a, _Float16 *x16, float *xinv, int Kpad,
+__global__ __launch_bounds__(CVT_T) void mmq_convert_x(const MmArgs a, _Float16 *x16, float *xinv, int Kpad,
                                                     const int *pos_pair, int n_rows, _Float16 *xsum) {
-    const int tok = blockIdx.x, slice = blockIdx.y, lane = threadIdx.x;
+    const int tok = blockIdx.x, slice = blockIdx.y, lane = threadIdx.x & 63, tid = threadIdx.x;
     if (tok >= n_rows) return;
     const float *src;
     if (pos_pair) {
@@ -257,13 +258,13 @@ __global__ __launch_bounds__(64) void mmq_convert_x(const MmArgs a, _Float16 *x1
     auto ld4f = [&](int k) -> float4 {
         return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, (uint32_t)k * 4u, 0, 0));
     };
-    constexpr int CH = 256 * CVT_R;   // values per chunk
-    const int t4 = lane * 4;
+    constexpr int CH = 4 * CVT_T * CVT_R;   // values per chunk
+    const int t4 = tid * 4;
     float4 v[CVT_R];
     float amax = 0.f;
     for (int k0 = 0; k0 < a.K; k0 += CH) {
 #pragma unroll
-        for (int i = 0; i < CVT_R; ++i) v[i] = ld4f(k0 + 256 * i + t4);
+        for (int i = 0; i < CVT_R; ++i) v[i] = ld4f(k0 + 4 * CVT_T * i + t4);
 #pragma unroll
         for (int i = 0; i < CVT_R; ++i)
             amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v[i].x), fabsf(v[i].y)), fmaxf(fabsf(v[i].z), fabsf(v[i].w))));
@@ -274,6 +275,11 @@ __global__ __launch_bounds__(64) void mmq_convert_x(const MmArgs a, _Float16 *x1
     amax = fmaxf(amax, xchg<8>(amax));
     amax = fmaxf(amax, xchg<16>(amax));
     amax = fmaxf(amax, xchg<32>(amax));
+    __shared__ float wmax[CVT_T / 64];
+    if (lane == 0) wmax[tid >> 6] = amax;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < CVT_T / 64; ++w) amax = fmaxf(amax, wmax[w]);
     const int e = amax > 0.f ? (int)ceilf(log2f(amax)) - 14 : 0;
     const float sc = ldexpf(1.f, -e);
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
@@ -283,11 +289,11 @@ __global__ __launch_bounds__(64) void mmq_convert_x(const MmArgs a, _Float16 *x1
     for (int k0 = 0; k0 < Kpad; k0 += CH) {
         if (Kpad > CH) {   // the registers hold the last chunk only: re-read
 #pragma unroll
-            for (int i = 0; i < CVT_R; ++i) v[i] = ld4f(k0 + 256 * i + t4);
+            for (int i = 0; i < CVT_R; ++i) v[i] = ld4f(k0 + 4 * CVT_T * i + t4);
         }
 #pragma unroll
         for (int i = 0; i < CVT_R; ++i) {
-            const int k = k0 + 256 * i + t4;
+            const int k = k0 + 4 * CVT_T * i + t4;
             const float4 y = make_float4(v[i].x * sc, v[i].y * sc, v[i].z * sc, v[i].w * sc);
             if constexpr (WAVE) {
                 const h4 hv = h4{(_Float16)y.x, (_Float16)y.z, (_Float16)y.y, (_Float16)y.w};
@@ -315,13 +321,13 @@ __global__ __launch_bounds__(64) void mmq_convert_x(const MmArgs a, _Float16 *x1
         }
     }
     if constexpr (WAVE) {   // runs past Kpad (phantom steps of the last records): zero sums
-        for (int g = Kpad / 32 + lane; g < nrec * 8; g += 64) {
+        for (int g = Kpad / 32 + tid; g < nrec * 8; g += CVT_T) {
             const int st = g >> 1;
             _Float16 *o = xsum + row_id * nrec * 16 + ((st >> 3) * 2 + (st & 1)) * 16 + (g & 1) * 8 + ((st & 7) >> 1) * 2;
             o[0] = o[1] = (_Float16)0.f;
         }
     }
-    if (lane == 0) xinv[row_id] = ldexpf(1.f, e);
+    if (tid == 0) xinv[row_id] = ldexpf(1.f, e);
 }
 
 // byte offset of 16-B chunk c of LDS row r (128-B rows, XOR swizzle over row pairs)
@@ -1754,7 +1760,7 @@ hipError_t mmq_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratc
     float *xinv = reinterpret_cast<float *>(buf + x16_bytes + sum_bytes + part_bytes);
     const dim3 cgrid(a.M, slices);
     if (wave) {
-        hipLaunchKernelGGL(mmq_convert_x<true>, cgrid, dim3(64), 0, st, a, x16, xinv, Kpad, (const int *)nullptr, a.M, xsum);
+        hipLaunchKernelGGL(mmq_convert_x<true>, cgrid, dim3(CVT_T), 0, st, a, x16, xinv, Kpad, (const int *)nullptr, a.M, xsum);
         switch (type) {
             case T_Q4_0: launch_wave_tn<T_Q4_0>(tile, a, x16, xsum, xinv, Kpad, slices, n_split, split_np, part, st); break;
             case T_Q8_0: launch_wave_tn<T_Q8_0>(tile, a, x16, xsum, xinv, Kpad, slices, n_split, split_np, part, st); break;
@@ -1770,7 +1776,7 @@ hipError_t mmq_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratc
         }
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(mmq_convert_x<false>, cgrid, dim3(64), 0, st, a, x16, xinv, Kpad, (const int *)nullptr, a.M,
+    hipLaunchKernelGGL(mmq_convert_x<false>, cgrid, dim3(CVT_T), 0, st, a, x16, xinv, Kpad, (const int *)nullptr, a.M,
                        (_Float16 *)nullptr);
     switch (type) {
         case T_Q4_0: launch_type<T_Q4_0>(tile, a, x16, xinv, Kpad, slices, st); break;
@@ -1845,7 +1851,7 @@ hipError_t mmq_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scr
     int *tile_off = offsets + (E + 1);
     int *pos_pair = tile_off + (E + 1);
     hipLaunchKernelGGL(moe_prep, dim3(1), dim3(1024), 0, st, a, offsets, tile_off, pos_pair);
-    hipLaunchKernelGGL(mmq_convert_x<false>, dim3(P, 1), dim3(64), 0, st, a, x16, xinv, Kpad, (const int *)pos_pair, P,
+    hipLaunchKernelGGL(mmq_convert_x<false>, dim3(P, 1), dim3(CVT_T), 0, st, a, x16, xinv, Kpad, (const int *)pos_pair, P,
                        (_Float16 *)nullptr);
     const MoeMap moe{offsets, tile_off, pos_pair, E, a.n_used};
     const dim3 grid((a.N + 127) / 128, (P + MOE_BN - 1) / MOE_BN + E, 1);
