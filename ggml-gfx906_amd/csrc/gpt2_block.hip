@@ -354,6 +354,12 @@ __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
     stamp(a, 0, 2);
 
     // ---- q, k, v of head h (+ bias)
+    if (a.stamps != nullptr) {   // diagnostics: this wave's last q/k/v weight fragment has landed
+        uint32_t probe = reinterpret_cast<const uint32_t *>(&qd.f[0][5])[0];
+        asm volatile("" : "+v"(probe));
+        if (probe == 0x12345u && threadIdx.x == 999) stamp(a, 0, 12);
+        stamp(a, 0, 11);
+    }
     qd.compute(sx, E, 3 * HD, [&](int vr, float v) { qkv_s[vr] = v + qb_s[vr]; });
     lds_barrier();
     stamp(a, 0, 3);

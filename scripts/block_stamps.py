@@ -52,7 +52,7 @@ with torch.cuda.stream(s):
             for k in (0, 1):
                 w = t[layer, k, :NWG[k], :NPH[k]]
                 if k == 0:
-                    extra.append((t[layer, 0, :NWG[0], 8:10] - t[layer, 0, :NWG[0], 0:1]) * 10)
+                    extra.append((t[layer, 0, :NWG[0]][:, [8, 9, 11]] - t[layer, 0, :NWG[0], 0:1]) * 10)
                 else:
                     extra1.append((t[layer, 1, :NWG[1]][:, [8, 9, 11]] - t[layer, 1, :NWG[1], 0:1]) * 10)
                 start = w[:, 0:1]
@@ -78,6 +78,7 @@ for k, nm in ((0, "attn block"), (1, "mlp block")):
 print(f"kernel gaps (last end -> next first start): median {np.median(gaps):.0f} ns, p90 {np.percentile(gaps, 90):.0f}")
 print(f"in-kernel shader clock (mlp block, s_memtime / s_memrealtime): median {np.median(clk):.0f} MHz")
 ex = np.median(np.concatenate(extra), axis=0)
-print(f"attn block: loads issued +{ex[0]:.0f} ns, wave 0's first residual row landed +{ex[1]:.0f} ns")
+print(f"attn block: loads issued +{ex[0]:.0f} ns, wave 0's first residual row landed +{ex[1]:.0f} ns, "
+      f"its last q/k/v weights landed +{ex[2]:.0f} ns")
 ex = np.median(np.concatenate(extra1), axis=0)
 print(f"mlp block: loads issued +{ex[0]:.0f} ns, wave 0's fc weights landed +{ex[1]:.0f} ns, fc computed (wave 0) +{ex[2]:.0f} ns")

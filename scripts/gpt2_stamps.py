@@ -25,8 +25,10 @@ c = G.Context(st, 1)
 s = torch.cuda.Stream()
 L = M.lib()
 L.ggml_mi355x_debug_stamps.argtypes = [C.c_void_p, C.c_size_t]
-N = [2304, 768, 3072, 768][idx % 4] if idx < 48 else 50257
-nwg = min(2048, (N + 31) // 32)
+# GGML_MI355X_GPT2_BLOCK unset (two-launch layers): the only fused mat-vec of a step is lm_head
+block = os.environ.get("GGML_MI355X_GPT2_BLOCK", "1") != "0"
+N = 50257 if block or idx >= 48 else [2304, 768, 3072, 768][idx % 4]
+nwg = 256 if N == 50257 else min(2048, (N + 31) // 32)   # lm_head: resident-size grid (mmvq_fused.hip)
 buf = np.zeros(4 * 65536 + 4 * 8 * nwg, np.uint64)
 res = []
 wres = []
