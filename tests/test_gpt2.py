@@ -260,8 +260,12 @@ def _run_logits(path, tokens, n_seq=1, graph=True, split=None):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("block", ["1", "0"], ids=["two_launch_layer", "five_launch_layer"])
 @pytest.mark.parametrize("name", sorted(MANIFEST["cases"]))
-def test_engine_matches_reference_logits(name):
+def test_engine_matches_reference_logits(name, block, monkeypatch):
+    """both layer forms (csrc/gpt2_block.hip, and the five-launch fallback used above
+    n_embd 1024) against the reference's logits and the exact forward"""
+    monkeypatch.setenv("GGML_MI355X_GPT2_BLOCK", block)
     c = MANIFEST["cases"][name]
     got = _run_logits(small_model(name), c["tokens"])[:, 0]
     assert np.isfinite(got).all()
