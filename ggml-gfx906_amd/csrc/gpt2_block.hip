@@ -12,7 +12,7 @@
 //                                                       stores the new K/V row of head h)
 //     part_out[h] = W_proj[:, cols of head h] . o      (the c_proj product restricted to the
 //                                                       head's 64 columns: a K-split of c_proj)
-//   mlp block, workgroup (slice j of 256 hidden units, sequence s):
+//   mlp block, workgroup (slice j of 128 hidden units, sequence s):
 //     y      = x + b_proj + sum_h part_attn[h]
 //     h_j    = gelu(W_fc[rows of slice j] . LN2(y) + b_fc)
 //     part_out[j] = W_mlp[:, cols of slice j] . h_j     (K-split of the MLP projection)
@@ -25,7 +25,10 @@
 // kept as f32 slabs [split][seq][n_embd] and summed in a fixed order by the next launch's
 // prologue (resid_issue / resid_finish), so results are deterministic and independent of the grid.
 // Workgroup 0 of every block also writes the summed residual ("materialized" x), which the
-// next-but-one block uses as its base.
+// next-but-one block uses as its base. For Q4_0 / Q8_0 the K-split streams of c_proj and the
+// MLP projection come from head- / slice-major copies (gpt2_block_repack), so they are
+// contiguous. Measured choices: 128-unit slices beat 256 (4207 vs 3850
+// tokens/s, GPT-2 117M Q4_0), LDS-only barriers keep weight streams in flight.
 #include <algorithm>
 
 #include "mmvq_impl.h"
