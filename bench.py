@@ -344,6 +344,36 @@ def gpt2_leg(torch, world: int, rank: int, n_seq: int, ticks: int, warm: int) ->
     return out
 
 
+def sched_plugin_gpt2(threads: int, tokens: int = 64) -> dict | None:
+    """the drop-in path: the reference's own ggml_backend_sched GPT-2 graph (oracle/_ref/gpt2_ref,
+    restating examples/gpt-2/main-sched.cpp) with our plugin loaded as its GPU backend, on the same
+    synthetic 117M Q4_0 checkpoint; decode ms/token over `tokens` positions (1 GPU)"""
+    exe = os.path.join(ROOT, "oracle", "_ref", "gpt2_ref")
+    if not os.path.exists(exe):
+        return None
+    sys.path[:0] = [os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+    import tempfile
+
+    import gpt2_synth
+    import qref
+    path = os.path.join(tempfile.gettempdir(), f"bench_gpt2_sched_{os.getpid()}.bin")
+    gpt2_synth.write_model(path, gpt2_synth.GPT2_117M, qref.Q4_0, 1234)
+    try:
+        r = subprocess.run([exe, path, "--tokens", "40", "--threads", str(threads), "--plugin", M.LIB_PATH, "--devices", "1",
+                            "--time-tokens", str(tokens)], capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            return None
+        j = json.loads(r.stdout.strip().splitlines()[-1])
+    except (subprocess.TimeoutExpired, ValueError, IndexError):
+        return None
+    finally:
+        os.remove(path)
+    return {"value": round(j["tokens_per_s"], 2), "unit": "tokens/s", "ms_per_token": round(j["ms_per_token"], 3),
+            "path": "reference ggml_backend_sched + libggml-hip-mi355x.so (weights, KV and supported ops on MI355X, "
+                    f"the rest on ggml-cpu with {threads} threads)",
+            "sample": f"GPT-2 117M Q4_0 (synthetic), 1 sequence, {tokens} decode positions after a 40-token prompt"}
+
+
 def cpu_gpt2_baseline(threads: int, tokens: int = 128) -> dict | None:
     """the reference's ggml-cpu GPT-2 graph (oracle/_ref/gpt2_ref) on a synthetic 117M Q4_0
     checkpoint written by tests/gpt2_synth.py: decode ms/token over `tokens` positions"""
@@ -570,6 +600,7 @@ def main() -> None:
             gpt2["single_stream_tokens_per_s"] = round(1e3 / r1["latency_ms_per_token"], 1)
         if cpu is not None:
             cpu["gpt2"] = cpu_gpt2_example_baseline(cpu["cores"]) or cpu_gpt2_baseline(cpu["cores"])
+            gpt2["reference_scheduler_with_plugin"] = sched_plugin_gpt2(cpu["cores"])
 
     if rank == 0:
         line = {
