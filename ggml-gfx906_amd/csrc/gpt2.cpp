@@ -46,7 +46,9 @@ hipError_t gpt2_attn_block_launch(int layer, int type, const float *base, const 
                                   float *x_out, const float *ln_g, const float *ln_b, float eps, const uint8_t *w_qkv,
                                   int64_t nb_qkv, const float *b_qkv, float *kc, float *vc, const int32_t *pos, float scale,
                                   int n_ctx, const uint8_t *w_o, int64_t nb_o, float *parts_out, int E, int n_head, int n_seq,
+                                  const uint8_t *wte, int64_t wte_nb, const float *wpe, const int32_t *tokens, int n_vocab,
                                   hipStream_t st);
+bool gpt2_block_embeds(int type);
 hipError_t gpt2_mlp_block_launch(int layer, int type, const float *base, const float *bias_in, const float *parts_in, int n_parts_in,
                                  float *x_out, const float *ln_g, const float *ln_b, float eps, const uint8_t *w_fc,
                                  int64_t nb_fc, const float *b_fc, const uint8_t *w_mp, int64_t nb_mp, float *parts_out, int E,
@@ -192,7 +194,9 @@ int run_step(ggml_mi355x_gpt2_ctx *c, hipStream_t st) {
     const auto &hp = m->hp;
     const int E = hp.n_embd;
     int rc;
-    if (m->first) {
+    // the two-launch layer takes the embedding in layer 0's prologue (32-block types)
+    const bool emb_fused = c->block && m->first && gpt2_block_embeds(m->wtype) && !getenv("GGML_MI355X_GPT2_EMBED_KERNEL");
+    if (m->first && !emb_fused) {
         rc = hip_status(gpt2_embed_launch(m->wte.type, m->wte.data, row_bytes(m->wte.type, E), reinterpret_cast<const float *>(m->wpe.data),
                                           c->tokens, c->pos, c->x, c->n_seq, E, hp.n_vocab, hp.n_ctx, st));
         if (rc) return rc;
@@ -215,7 +219,9 @@ int run_step(ggml_mi355x_gpt2_ctx *c, hipStream_t st) {
             rc = hip_status(gpt2_attn_block_launch(l - m->l0, m->wtype, base, bias, parts, np, c->xr, f(L.ln1_g), f(L.ln1_b), 1e-5f, L.attn_w.data,
                                                    row_bytes(m->wtype, E), f(L.attn_b), kc, vc, c->pos, kq_scale, hp.n_ctx,
                                                    rp ? c->rep_o[l - m->l0] : L.proj_w.data, row_bytes(m->wtype, E), c->p_attn, E,
-                                                   hp.n_head, c->n_seq, st));
+                                                   hp.n_head, c->n_seq, emb_fused && l == 0 ? m->wte.data : nullptr,
+                                                   row_bytes(m->wtype, E), reinterpret_cast<const float *>(m->wpe.data), c->tokens,
+                                                   hp.n_vocab, st));
             if (rc) return rc;
             rc = hip_status(gpt2_mlp_block_launch(l - m->l0, m->wtype, c->xr, f(L.proj_b), c->p_attn, hp.n_head, c->xm, f(L.ln2_g), f(L.ln2_b),
                                                   1e-5f, L.fc_w.data, row_bytes(m->wtype, E), f(L.fc_b),

@@ -51,6 +51,7 @@ constexpr int MLP_SLICE = 128;             // hidden units per mlp workgroup (tw
 // copies whose K-splits are contiguous (gpt2.cpp, gpt2_block_repack); K-quant slots are not
 // contiguous byte ranges (header + chunk), so those read the ggml rows in place
 template <int T> constexpr bool REPACK = T == T_Q4_0 || T == T_Q8_0;
+constexpr bool REPACK_TYPE(int t) { return t == T_Q4_0 || t == T_Q8_0; }
 
 // LDS bytes of one quantized activation vector of K values (XSmem layout, nc = 1)
 constexpr int xs_bytes(int K) { return K + 4 * (K / 32) * 2 + 4 * (K / 16); }
@@ -84,6 +85,13 @@ struct BlockArgs {
     // slot ((2 * layer + kind) * 64 + x) * 16 + phase; nullptr when off
     unsigned long long *stamps;
     int layer;
+    // layer 0 of a first stage, Q4_0 / Q8_0 (EMB kernels): the residual is the token embedding
+    // wte[tokens[s]] + wpe[pos[s]] (main-sched.cpp:589-595), dequantized in the prologue
+    const uint8_t *wte;
+    int64_t wte_nb;
+    const float *wpe;
+    const int32_t *tokens;
+    int n_vocab;
 };
 
 __device__ __forceinline__ void stamp(const BlockArgs &a, int kind, int phase) {
@@ -283,6 +291,46 @@ struct RowsDot {
     }
 };
 
+// token embedding of sequence s for this thread's 8-value chunk (thread t < E/8: values
+// 8t .. 8t+7; the others repeat a valid chunk): the block's raw scale and 8 code bytes and the
+// wpe row are issued here; token and position are uniform per workgroup (scalar loads), so the
+// vector loads wait on nothing in flight. embed_finish decodes exactly as dequantize_row_q4_0 /
+// _q8_0 (src/ggml-quants.c:307-323, 401-415) and adds wpe (the ggml_add of :589-595).
+struct Emb {
+    uint32_t d;
+    uint32_t q[2];
+    float4 w[2];
+};
+
+template <int T>
+__device__ __forceinline__ void embed_issue(const BlockArgs &a, int s, Emb &e) {
+    const int nch = a.E / 8, k = 8 * ((int)threadIdx.x % nch);
+    const int tok = min(max(a.tokens[s], 0), a.n_vocab - 1);
+    const int p = min(max(a.pos[s], 0), a.n_ctx - 1);
+    const uint8_t *blk = a.wte + (int64_t)tok * a.wte_nb + (int64_t)(k >> 5) * QT<T>::bytes;
+    e.d = ld2(blk);
+    ld8(blk + 2 + (T == T_Q4_0 ? (k & 15) : (k & 31)), e.q);
+    const float *wp = a.wpe + (int64_t)p * a.E + k;
+    e.w[0] = reinterpret_cast<const float4 *>(wp)[0];
+    e.w[1] = reinterpret_cast<const float4 *>(wp)[1];
+}
+
+template <int T>
+__device__ __forceinline__ void embed_finish(const BlockArgs &a, const Emb &e, float4 &x0, float4 &x1) {
+    const int k = 8 * ((int)threadIdx.x % (a.E / 8));
+    const float d = h2f((uint16_t)e.d);
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t byte = (e.q[i >> 2] >> (8 * (i & 3))) & 0xffu;
+        const int q = T == T_Q4_0 ? (int)((k & 31) >= 16 ? byte >> 4 : byte & 0x0fu) - 8 : (int)(int8_t)byte;
+        v[i] = __fmul_rn((float)q, d);
+    }
+    x0 = make_float4(v[0] + e.w[0].x, v[1] + e.w[0].y, v[2] + e.w[0].z, v[3] + e.w[0].w);
+    x1 = make_float4(v[4] + e.w[1].x, v[5] + e.w[1].y, v[6] + e.w[1].z, v[7] + e.w[1].w);
+    if (!resid_in(a)) x0 = x1 = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 // LN of the register-resident residual (layer_norm_cols, shift = x[0] of the sequence) and its
 // int8 quantization into `sm` (K = E). Ends with a workgroup barrier.
 template <int T>
@@ -313,7 +361,7 @@ __device__ __forceinline__ void load_ln(const float *gp, const float *bp, int E,
 constexpr int AGROUPS = NW * 4;            // 16-lane key groups per workgroup
 constexpr int AU = 8;                      // keys per group in flight per round
 
-template <int T, int QNIT, int RR>
+template <int T, int QNIT, int RR, bool EMB = false>
 __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
     __shared__ __align__(16) uint8_t lds_x[xs_bytes(E_MAX)];   // LN1(x), quantized
     __shared__ __align__(16) uint8_t lds_o[xs_bytes(E_MAX)];   // head h's attention output, quantized
@@ -328,9 +376,12 @@ __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
     const XSmem sx = xsmem(lds_x, E, 1), so = xsmem(lds_o, E, 1);
     stamp(a, 0, 0);
 
-    // ---- issue: residual rows, LN params, q/k/v bias, position; then the qkv weight stream
-    Resid<RR> R0;
-    resid_issue(a, s, 0, R0);
+    // ---- issue: residual rows (layer 0 of a first stage: the token embedding), LN params, q/k/v
+    // bias, position; then the qkv weight stream
+    [[maybe_unused]] Resid<RR> R0;
+    [[maybe_unused]] Emb em;
+    if constexpr (EMB) embed_issue<T>(a, s, em);
+    else resid_issue(a, s, 0, R0);
     float4 g[1][2], bb[1][2];
     load_ln(a.ln_g, a.ln_b, E, g, bb);
     const int vr_b = min(tid, 3 * HD - 1);
@@ -350,10 +401,19 @@ __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
     if (tid < 3 * HD) qb_s[tid] = qb;
     for (int i = tid; i < xs_bytes(E) / 4; i += BT) reinterpret_cast<uint32_t *>(lds_o)[i] = 0u;   // c_proj K-split: zeros outside head h
     float4 xa[1][1], xb[1][1];
-    resid_finish(a, s, R0, red, xa[0][0], xb[0][0]);
+    float shift0;
+    if constexpr (EMB) {
+        embed_finish<T>(a, em, xa[0][0], xb[0][0]);
+        if (tid == 0) red[0] = xa[0][0].x;
+        lds_barrier();
+        shift0 = red[0];
+    } else {
+        resid_finish(a, s, R0, red, xa[0][0], xb[0][0]);
+        shift0 = resid_first(a, red);
+    }
     stamp(a, 0, 1);
     if (h == 0) store_resid(a, s, xa[0][0], xb[0][0]);
-    ln_quantize<T>(a, xa, xb, g, bb, sx, resid_first(a, red));
+    ln_quantize<T>(a, xa, xb, g, bb, sx, shift0);
     stamp(a, 0, 2);
 
     // ---- q, k, v of head h (+ bias)
@@ -570,7 +630,10 @@ int resid_rr(const BlockArgs &a) {
 
 template <int T, int RR>
 hipError_t launch_pair(bool attn, const BlockArgs &a, hipStream_t st) {
-    if (attn) hipLaunchKernelGGL((attn_block_kernel<T, 1, RR>), dim3(a.n_head, a.n_seq), dim3(BT), 0, st, a);
+    if (attn && a.wte != nullptr) {
+        if constexpr (REPACK<T>) hipLaunchKernelGGL((attn_block_kernel<T, 1, 3, true>), dim3(a.n_head, a.n_seq), dim3(BT), 0, st, a);
+        else return hipErrorInvalidValue;
+    } else if (attn) hipLaunchKernelGGL((attn_block_kernel<T, 1, RR>), dim3(a.n_head, a.n_seq), dim3(BT), 0, st, a);
     else hipLaunchKernelGGL((mlp_block_kernel<T, 1, RR>), dim3(4 * a.E / MLP_SLICE, a.n_seq), dim3(BT), 0, st, a);
     return hipGetLastError();
 }
@@ -603,6 +666,9 @@ bool gpt2_block_supported(int n_embd, int n_head) {
 
 int gpt2_block_mlp_slices(int n_embd) { return 4 * n_embd / MLP_SLICE; }
 
+// layer 0 of a first stage can take the token embedding in its prologue (32-block types)
+bool gpt2_block_embeds(int type) { return REPACK_TYPE(type); }
+
 // head-major c_proj ([head][row][2 blocks]) and slice-major MLP projection
 // ([slice][row][MLP_SLICE / 32 blocks]) copies of one layer, for the 32-block types; bytes of
 // each through *_bytes (dst == nullptr: sizes only)
@@ -631,6 +697,7 @@ hipError_t gpt2_attn_block_launch(int layer, int type, const float *base, const 
                                   float *x_out, const float *ln_g, const float *ln_b, float eps, const uint8_t *w_qkv,
                                   int64_t nb_qkv, const float *b_qkv, float *kc, float *vc, const int32_t *pos, float scale,
                                   int n_ctx, const uint8_t *w_o, int64_t nb_o, float *parts_out, int E, int n_head, int n_seq,
+                                  const uint8_t *wte, int64_t wte_nb, const float *wpe, const int32_t *tokens, int n_vocab,
                                   hipStream_t st) {
     if (!gpt2_block_supported(E, n_head)) return hipErrorInvalidValue;
     BlockArgs a{};
@@ -640,6 +707,7 @@ hipError_t gpt2_attn_block_launch(int layer, int type, const float *base, const 
     a.w_o = w_o; a.nb_o = nb_o; a.parts_out = parts_out;
     a.E = E; a.n_head = n_head; a.n_seq = n_seq;
     a.layer = layer; a.stamps = stamps_buffer();
+    a.wte = wte; a.wte_nb = wte_nb; a.wpe = wpe; a.tokens = tokens; a.n_vocab = n_vocab;
     return launch_block(type, true, a, st);
 }
 
