@@ -171,11 +171,19 @@ __global__ __launch_bounds__(256) void argmax_final_kernel(const float *__restri
     const int s = blockIdx.x;
     float v = -INFINITY;
     int idx = 0x7fffffff;
-    for (int k = threadIdx.x; k < ARGMAX_SLOTS; k += 256) {
-        const float x = pv[(int64_t)s * ARGMAX_SLOTS + k];
-        const int i = pi[(int64_t)s * ARGMAX_SLOTS + k];
-        if (x > v || (x == v && i < idx)) { v = x; idx = i; }
+    // every slot pair of this thread is loaded before any is compared (one memory round trip,
+    // not ARGMAX_SLOTS / 256 dependent ones)
+    constexpr int PER = ARGMAX_SLOTS / 256;
+    float xs[PER];
+    int is[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        xs[u] = pv[(int64_t)s * ARGMAX_SLOTS + threadIdx.x + 256 * u];
+        is[u] = pi[(int64_t)s * ARGMAX_SLOTS + threadIdx.x + 256 * u];
     }
+#pragma unroll
+    for (int u = 0; u < PER; ++u)
+        if (xs[u] > v || (xs[u] == v && is[u] < idx)) { v = xs[u]; idx = is[u]; }
     for (int d = 1; d < 64; d <<= 1) {
         const float ov = __shfl_xor(v, d);
         const int oi = __shfl_xor(idx, d);
