@@ -41,6 +41,7 @@ step prof_mmq 300 $RP -d $O/mmq -o run -- python scripts/mmq_bench.py q8_0:4096:
 squash $O/mmq
 step prof_gpt2 300 $RP -d $O/gpt2 -o run -- python scripts/gpt2_bench.py 1 256 1
 squash $O/gpt2
+step block_stamps 200 bash -c 'python scripts/block_stamps.py 24 64 && python scripts/block_stamps.py 24 600'
 step hbm_floor 120 scripts/hbm_probe
 du -sh $O
 echo "=== done"
