@@ -48,14 +48,17 @@ hipError_t mmq_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scr
 bool mmq8_supported(int type, const MmArgs &a);
 hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
 
-// mat-mat kernel family: GGML_MI355X_MMQ = i8 (the int8 MFMA path wherever it applies) | f16
-// (the f16 MFMA kernels only); unset: the measured default rule of use_mmq8
+// mat-mat kernel family: the int8 MFMA tile (csrc/mmq8.hip) wherever it applies (K a multiple
+// of 256, aligned rows): it is exact in the block scales (no f16 range to overflow) and measured
+// as fast or faster than the f16 tiles for Q4_0 / Q8_0 / Q4_K / Q5_K from 9 to 2048 tokens
+// (scripts/mmq8_sweep.sh, profiles/r03_mmq_sweep.txt); Q6_K costs two MFMAs per 32-k block there
+// and runs ~1.4x slower than its f16 tile but stays on the exact path. GGML_MI355X_MMQ = f16
+// selects the f16 kernels (csrc/mmq.hip) for A/B measurements.
 static bool use_mmq8(int type, const MmArgs &m) {
-    const char *env = getenv("GGML_MI355X_MMQ");
     if (!mmq8_supported(type, m)) return false;
-    if (env && !strcmp(env, "i8")) return true;
+    const char *env = getenv("GGML_MI355X_MMQ");
     if (env && !strcmp(env, "f16")) return false;
-    return false;
+    return true;
 }
 
 static constexpr size_t LDS_LIMIT = 160 * 1024;
@@ -169,6 +172,7 @@ int mul_mat(const TensorView &a, const TensorView &b, const TensorView &d, hipSt
     if (rc != GGML_MI355X_OK) return rc;
     if (a.ne[1] == 0 || b.ne[1] == 0 || b.ne[2] == 0 || b.ne[3] == 0) return GGML_MI355X_OK;
     MmArgs m = base_args(a, b, d);
+    std::lock_guard<std::mutex> hold(scratch.mu);   // until the scratch users are queued
     hipError_t e;
     if (m.M > 8 && use_mmq8(a.type, m)) e = mmq8_launch(a.type, m, st, scratch);
     else if (m.M > 8 && mmq_supported(a.type, m)) e = mmq_launch(a.type, m, st, scratch);
@@ -217,6 +221,7 @@ int mul_mat_id(const TensorView &as, const TensorView &b, const TensorView &ids,
     m.x_aligned16 = aligned16(b.data, m.nb11, m.nb12, m.nb13);
     static const int min_pairs = getenv("GGML_MI355X_MMQ_ID_MIN") ? atoi(getenv("GGML_MI355X_MMQ_ID_MIN")) : MMQ_ID_MIN_PAIRS;
     const bool grouped = m.n_used * m.n_tok >= min_pairs && mmq_id_supported(as.type, m);
+    std::lock_guard<std::mutex> hold(scratch.mu);
     const hipError_t e = grouped ? mmq_id_launch(as.type, m, st, scratch) : mmvq_id_launch(as.type, m, 1, st);
     if (e == hipErrorOutOfMemory) return GGML_MI355X_ENOMEM;
     return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;

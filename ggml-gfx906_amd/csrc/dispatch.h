@@ -6,6 +6,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "qmm_args.h"
 
 namespace mi355x {
@@ -22,7 +24,13 @@ struct TensorView {
 // stream. Growing is refused (nullptr, the launch then fails with GGML_MI355X_ENOMEM) while the
 // stream is being captured into a hipGraph: hipFree / hipMalloc are not capturable, so a
 // captured launch must have been run once eagerly on the same stream first.
+//
+// Several host threads may share one stream (torch's default stream is handle 0 on every
+// thread, and ctypes releases the GIL during a call), so mul_mat / mul_mat_id hold `mu` from
+// get() until every kernel that uses the buffer is queued: a second thread that must grow the
+// buffer then synchronizes the stream behind those kernels before it frees the old one.
 struct Scratch {
+    std::mutex mu;
     void *ptr = nullptr;
     size_t cap = 0;
     int device = -1;

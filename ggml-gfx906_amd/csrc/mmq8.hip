@@ -1,29 +1,39 @@
-// mmq8.hip — quantized mat-mat (prefill, ne11 > 8) on the int8 matrix cores.
+// mmq8.hip — quantized mat-mat (prefill, ne11 > 8) on the int8 matrix cores, all five types.
 //
-// The integer form of the reference's MMQ (src/ggml-cuda/mmq.cuh:3134 mul_mat_q, mma.cuh:515-569
-// int8 tiles; the arithmetic of ggml-cpu's block dot products, src/ggml-cpu/quants.c
-// ggml_vec_dot_q4_K_q8_K / _q8_0_q8_0), built for gfx950:
+// The integer form of the reference's MMQ (src/ggml-cuda/mmq.cuh:3134 mul_mat_q; int8 tiles
+// mma.cuh:515-569; the per-type tile loaders load_tiles_q4_0 / _q8_0 / _q4_K / _q5_K / _q6_K,
+// mmq.cuh:2027 for Q6_K) with the arithmetic of ggml-cpu's block dots
+// (src/ggml-cpu/quants.c ggml_vec_dot_q4_K_q8_K / _q6_K_q8_K / _q8_0_q8_0), built for gfx950:
 //
 //   1. mmq8_quant_x: activations -> int8 blocks of 256 exactly as quantize_row_q8_K_ref
-//      (src/ggml-quants.c:2555-2591: d = max/-127 of the signed largest-|x| value, q =
-//      nearest_int(x * -127/max) clamped to 127) plus the 16-element block sums, one wave per
-//      (token, 256-k block). Layout x8[slice][Mpad][K], xd[slice][Mpad][K/256],
-//      xbs[slice][Mpad][K/256][16] (f16: sums of 16 int8 are exact in f16).
-//   2. mmq8_kernel: 64 weight rows x 64 tokens per workgroup, 4 waves of one 32x32 tile each,
-//      KG K-groups (split-K inside the workgroup, reduced through LDS). Per 256-k block the
-//      workgroup stages the raw weight bytes and the int8 activations through LDS (coalesced
-//      16-B global loads into registers, realigned and written as 32-B rows with a 16-B XOR
-//      swizzle that makes every ds_read_b128 fragment read conflict-free), then each wave runs
-//      v_mfma_i32_32x32x32_i8 per 32-k block: the B operand is one weight row per lane (so the
-//      row's block scale is a per-lane scalar), the A operand 32 tokens.
-//        Q8_0 / Q4_0: R_b (int32, exact) -> p += d_b * R_b  (Q4_0 codes decoded to q-8)
+//      (src/ggml-quants.c:2555-2591: d = max/-127 of the signed largest-|x| value,
+//      q = nearest_int(x * -127/max) clamped to 127, 16-element block sums). The output is not
+//      a row-major array but, per (token tile of 64, super-block of 256 k), the exact LDS image
+//      the tile kernel consumes, so the kernel copies it with LDS-DMA (buffer_load ... lds, no
+//      VGPR round trip, no ds_write) in whole 1-KiB pieces.
+//   2. mmq8_kernel<T>: 128 weight rows x 64 tokens per workgroup, 8 waves = 2 K-groups x
+//      (2 row halves x 2 token halves); a wave owns 64 rows x 32 tokens, i.e. two 32x32 MFMA
+//      tiles that share the token (A) fragment. Per super-block the weight rows are loaded with
+//      16-B buffer loads into registers one stage ahead, decoded to int8 codes (Q4_0: q-8,
+//      Q4_K: q, Q5_K: q | qh<<4, Q6_K: q-32, Q8_0 as is) and written to LDS in MFMA-fragment
+//      order with an XOR swizzle that keeps both the staging writes and the fragment reads free
+//      of bank conflicts. K-group g takes blocks 4g..4g+3 of every super-block.
+//        Q8_0 / Q4_0: v_mfma_i32_32x32x32_i8 per 32-k block with C = 0x4B400000: the int32
+//          result R + 0x4B400000 IS the f32 bit pattern of 12582912 + R (|R| < 2^22), so one
+//          fma per output and block applies the weight scale: p += (12582912 + R) * d_w; the
+//          constant 12582912 * sum(d_w) leaves once per super-block.
 //        Q4_K / Q5_K: p_i += sc_j * R_j in int32 (v_mad_i32_i24: the 6-bit sub-block scales
-//                     are integers, as ggml_vec_dot_q4_K_q8_K sums them), and the min term
-//                     sum_j m_j * bsum_j as one f16 MFMA per block on exact integers;
-//                     per block p = d * p_i - dmin * mins.
-//      and acc += d8[token] * p once per 256-k block.
-//   The integer dot products are those of the CPU backend bit for bit; only the fp32 order of
-//   the per-block scale accumulation differs (K-quants: identical activation blocks too).
+//          are integers, as ggml_vec_dot_q4_K_q8_K sums them); the min term sum_j m_j * bsum_j
+//          as one f16 MFMA on exact integers; p = d * p_i - dmin * mins.
+//        Q6_K: scales are per 16 weights, so one v_mfma_i32_32x32x16_i8 per scale group and
+//          p_i += sc_g * R_g (signed); p = d * p_i.
+//      and acc += d_x[token] * p once per super-block (the activation scale is per 256).
+//   Split-K over workgroups (fixed-order reduce kernel) when the tile grid alone cannot fill
+//   the chip; the workgroup -> tile map keeps the token tiles of one row tile on one XCD so
+//   that XCD's L2 serves the weight rows to all of them.
+//   The integer dot products are those of the CPU backend bit for bit (Q8_K activation blocks,
+//   i.e. the CPU's own for the K-quants); only the fp32 order of the scale accumulation differs.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -37,99 +47,43 @@ typedef int i32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void *lds_ptr_t;
 
 constexpr uint32_t Q8_RSRC_W3 = 0x00020000u;   // raw buffer, dword3 for gfx9-class descriptors
-constexpr int Q8_QK = 256;                     // activation block (Q8_K super-block)
-constexpr int Q8_TILE = 64;                    // weight rows = tokens per workgroup
+constexpr int Q8_QK = 256;                     // activation block = one super-block of k
+constexpr int Q8_TOK = 64;                     // tokens per activation image
+// TR = weight rows per workgroup (128, or 64 for two workgroups per CU), 4 TR threads
+constexpr uint32_t Q8_MAGIC_I = 0x4B400000u;   // f32 bits of 12582912 = 1.5 * 2^23
+constexpr float Q8_MAGIC_F = 12582912.0f;
 
-// ------------------------------------------------------------------------------------------
-// activations -> Q8_K-style int8 blocks (restates quantize_row_q8_K_ref, src/ggml-quants.c:2555)
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void mmq8_quant_x(const MmArgs a, int8_t *__restrict__ x8, float *__restrict__ xd,
-                                                    _Float16 *__restrict__ xbs, int Mpad, int n_sb) {
-    const int lane = threadIdx.x & 63;
-    const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (item >= (int64_t)Mpad * n_sb) return;   // whole wave
-    const int tok = (int)(item / n_sb), sb = (int)(item % n_sb);
-    const int slice = blockIdx.y;
-    const int i12 = slice % a.ne12, i13 = slice / a.ne12;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (tok < a.M) {
-        const float *src = reinterpret_cast<const float *>(a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13 +
-                                                           (int64_t)tok * a.nb11) +
-                           sb * Q8_QK + lane * 4;
-        if (a.x_aligned16) {
-            const float4 f = *reinterpret_cast<const float4 *>(src);
-            v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
-        } else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = src[i];
-        }
-    }
-    // largest |x| and the first k reaching it (the reference's strict '>' keeps the first)
-    float am = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
-#pragma unroll
-    for (int o = 32; o; o >>= 1) am = fmaxf(am, __shfl_xor(am, o));
-    int idx = 1 << 30;
-#pragma unroll
-    for (int i = 3; i >= 0; --i)
-        if (fabsf(v[i]) == am) idx = lane * 4 + i;
-#pragma unroll
-    for (int o = 32; o; o >>= 1) idx = min(idx, __shfl_xor(idx, o));
-    const int sel = idx & 3;
-    const float mine = sel == 0 ? v[0] : sel == 1 ? v[1] : sel == 2 ? v[2] : v[3];
-    const float mx = __shfl(mine, (idx >> 2) & 63);
-    int q[4] = {0, 0, 0, 0};
-    float d = 0.f;
-    if (am != 0.f) {
-        const float iscale = -127.f / mx;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) q[i] = min(127, (int)__builtin_rintf(iscale * v[i]));
-        d = 1.f / iscale;
-    }
-    const int64_t rowi = (int64_t)slice * Mpad + tok;
-    const uint32_t packed = (uint32_t)(q[0] & 0xff) | (uint32_t)(q[1] & 0xff) << 8 | (uint32_t)(q[2] & 0xff) << 16 |
-                            (uint32_t)(q[3] & 0xff) << 24;
-    reinterpret_cast<uint32_t *>(x8 + rowi * ((int64_t)n_sb * Q8_QK) + sb * Q8_QK)[lane] = packed;
-    int s = q[0] + q[1] + q[2] + q[3];
-    s += __shfl_xor(s, 1);
-    s += __shfl_xor(s, 2);
-    if ((lane & 3) == 0) xbs[(rowi * n_sb + sb) * 16 + (lane >> 2)] = (_Float16)s;
-    if (lane == 0) xd[rowi * n_sb + sb] = d;
+// ---- activation image of one (token tile, super-block): the LDS bytes, 1-KiB pieces ----
+//   codes  [blk 8][h 2][tok 64][16 B]            (Q6_K: [blk 8][h 2][hl 2][tok 64][8 B])
+//   dx     [tok 64] f32                          at XI_DX
+//   bsums  [hl 2][tok 64][8 f16], k16-sums 8hl.. at XI_BS (Q4_K / Q5_K)
+constexpr int XI_DX = 16384, XI_BS = 16640;
+template <int T> constexpr bool q8_has_min() { return T == T_Q4_K || T == T_Q5_K; }
+template <int T> constexpr int ximg_bytes() { return q8_has_min<T>() ? 19456 : 17408; }
+// ---- weight image: codes [blk 8][h 2][row TR][16 B] (Q6_K [blk][h][hl][row][8 B]) + meta [kg][row][16 B]
+template <int TR> constexpr int wi_meta() { return 256 * TR; }
+template <int TR> constexpr int wi_bytes() { return 288 * TR; }
+
+// 16-B code piece (blk, h) of weight row `row`. The XOR permutes rows inside a group of 16, so a
+// fragment read (16 lanes = 16 consecutive rows of one piece) still touches every LDS bank once;
+// the XOR pattern is chosen per staging map so that the 16 lanes of a staging write, which hold
+// different pieces of few rows, land on 16 distinct 16-B slots as well.
+template <int T> __device__ __forceinline__ int swz16(int blk, int h) {
+    return q8_has_min<T>() ? (4 * h + 8 * ((blk >> 1) & 1)) : ((2 * blk + h) & 15);
 }
-
-// ------------------------------------------------------------------------------------------
-// LDS image of one 256-k block (per K-group):
-//   XQ  8 planes x 64 tokens x 32 B  int8 activations, plane b = k 32b..32b+31
-//   XD  64 f32                        activation block scales
-//   XB  64 tokens x 32 B              16 f16 block sums (K-quants)
-//   W   per type (below)
-// A 32-B plane row holds two 16-B halves (k 0..15, 16..31); half h of row r sits at
-// 16 * (h ^ (r >> 4 & 1)), which spreads every 16-lane ds_read_b128 group over all 64 banks.
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t pl_off(int r, int h) { return (uint32_t)(r * 32 + 16 * (h ^ ((r >> 4) & 1))); }
-
-constexpr int L_XQ = 0, L_XD = 8 * 2048, L_XB = L_XD + 256, L_W = L_XB + 2048;
-
-template <int T> struct W8;
-// Q8_0: WQ 8 planes x 64 rows x 32 B (int8 codes), WD 64 rows x 8 f32 (block scales)
-template <> struct W8<T_Q8_0> {
-    static constexpr int SBB = 272, WQ = 0, WD = 8 * 2048, BYTES = WD + 2048, NREG = 2 * 9;
-};
-// Q4_0: WQ 8 planes x 64 rows x 16 B (nibbles), WD as Q8_0
-template <> struct W8<T_Q4_0> {
-    static constexpr int SBB = 144, WQ = 0, WD = 8 * 1024, BYTES = WD + 2048, NREG = 2 * 5;
-};
-// Q4_K: WQ 4 planes x 64 rows x 32 B (nibble pairs), WH 64 rows x 16 B header (d, dmin, scales)
-template <> struct W8<T_Q4_K> {
-    static constexpr int SBB = 144, WQ = 0, WH = 4 * 2048, BYTES = WH + 1024, NREG = 3 * 4, NCH = 9;
-};
-// Q5_K: as Q4_K plus QH 64 rows x 32 B high bits
-template <> struct W8<T_Q5_K> {
-    static constexpr int SBB = 176, WQ = 0, WH = 4 * 2048, QH = WH + 1024, BYTES = QH + 2048, NREG = 3 * 4, NCH = 11;
-};
-
-template <int T> constexpr int stage_bytes() { return (L_W + W8<T>::BYTES + 15) / 16 * 16; }
+template <int T, int TR> __device__ __forceinline__ uint32_t wslot16(int blk, int h, int row) {
+    return (uint32_t)(blk * 32 * TR + h * 16 * TR + ((row ^ swz16<T>(blk, h)) << 4));
+}
+// Q6_K: 8-B piece (blk, h, hl) (one 16-weight scale group per 32x32x16 MFMA); rows permuted
+// inside groups of 32 (a 32-lane ds_read_b64 reads 32 consecutive rows)
+__device__ __forceinline__ int swz8(int blk, int h) { return 8 * (2 * (blk >> 2) + h); }
+template <int TR> __device__ __forceinline__ uint32_t wslot8(int blk, int h, int hl, int row) {
+    return (uint32_t)(blk * 32 * TR + h * 16 * TR + hl * 8 * TR + ((row ^ swz8(blk, h)) << 3));
+}
 
 __device__ __forceinline__ u32x4v bl128(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
@@ -137,364 +91,708 @@ __device__ __forceinline__ u32x4v bl128(__amdgpu_buffer_rsrc_t r, uint32_t off) 
 __device__ __forceinline__ uint32_t bl32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
 }
-__device__ __forceinline__ void lds_st128(uint8_t *p, u32x4v v) { *reinterpret_cast<u32x4v *>(p) = v; }
-__device__ __forceinline__ u32x4v lds_ld128(const uint8_t *p) { return *reinterpret_cast<const u32x4v *>(p); }
-
-// ---- weight staging: global -> registers (issued early) -> LDS (after the block's compute) ----
-// j: thread index in the K-group (0..255); wbase: byte offset of this tile's first row + the
-// 256-k block within the row
-template <int T> struct WStage;
-
-template <> struct WStage<T_Q8_0> {   // task (row, block): 9 dwords covering the 34-B block
-    uint32_t w[2][9];
-    __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, uint32_t wbase, uint32_t nb01, int j) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int task = j + 256 * t, row = task >> 3, blk = task & 7;
-            const uint32_t off = wbase + (uint32_t)row * nb01 + 34u * blk;
-            const uint32_t o4 = off & ~3u;
-            const u32x4v a0 = bl128(rs, o4), a1 = bl128(rs, o4 + 16);
-            w[t][0] = a0[0]; w[t][1] = a0[1]; w[t][2] = a0[2]; w[t][3] = a0[3];
-            w[t][4] = a1[0]; w[t][5] = a1[1]; w[t][6] = a1[2]; w[t][7] = a1[3];
-            w[t][8] = bl32(rs, o4 + 32);
-        }
-    }
-    __device__ __forceinline__ void zero() {
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int i = 0; i < 9; ++i) w[t][i] = 0;
-    }
-    __device__ __forceinline__ void store(uint8_t *W, uint32_t wbase, uint32_t nb01, int j) const {
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int task = j + 256 * t, row = task >> 3, blk = task & 7;
-            const bool odd = ((wbase + (uint32_t)row * nb01 + 34u * blk) & 2u) != 0;   // block at +2 in w[0]
-            // odd: d = hi16(w0), codes = w1..w8; even: d = lo16(w0), codes = bytes 2..33
-            const uint32_t dbits = odd ? (w[t][0] >> 16) : (w[t][0] & 0xffffu);
-            uint32_t q[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) q[i] = odd ? w[t][i + 1] : __builtin_amdgcn_alignbyte(w[t][i + 1], w[t][i], 2);
-            uint8_t *WQ = W + W8<T_Q8_0>::WQ + blk * 2048;
-            lds_st128(WQ + pl_off(row, 0), u32x4v{q[0], q[1], q[2], q[3]});
-            lds_st128(WQ + pl_off(row, 1), u32x4v{q[4], q[5], q[6], q[7]});
-            *reinterpret_cast<float *>(W + W8<T_Q8_0>::WD + pl_off(row, blk >> 2) + 4 * (blk & 3)) = h2f((uint16_t)dbits);
-        }
-    }
-};
-
-template <> struct WStage<T_Q4_0> {   // task (row, block): 5 dwords covering the 18-B block
-    uint32_t w[2][5];
-    __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, uint32_t wbase, uint32_t nb01, int j) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int task = j + 256 * t, row = task >> 3, blk = task & 7;
-            const uint32_t off = wbase + (uint32_t)row * nb01 + 18u * blk;
-            const uint32_t o4 = off & ~3u;
-            const u32x4v a0 = bl128(rs, o4);
-            w[t][0] = a0[0]; w[t][1] = a0[1]; w[t][2] = a0[2]; w[t][3] = a0[3];
-            w[t][4] = bl32(rs, o4 + 16);
-        }
-    }
-    __device__ __forceinline__ void zero() {
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int i = 0; i < 5; ++i) w[t][i] = 0;
-    }
-    __device__ __forceinline__ void store(uint8_t *W, uint32_t wbase, uint32_t nb01, int j) const {
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int task = j + 256 * t, row = task >> 3, blk = task & 7;
-            const bool odd = ((wbase + (uint32_t)row * nb01 + 18u * blk) & 2u) != 0;
-            const uint32_t dbits = odd ? (w[t][0] >> 16) : (w[t][0] & 0xffffu);
-            uint32_t q[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) q[i] = odd ? w[t][i + 1] : __builtin_amdgcn_alignbyte(w[t][i + 1], w[t][i], 2);
-            lds_st128(W + W8<T_Q4_0>::WQ + blk * 1024 + row * 16, u32x4v{q[0], q[1], q[2], q[3]});
-            *reinterpret_cast<float *>(W + W8<T_Q4_0>::WD + pl_off(row, blk >> 2) + 4 * (blk & 3)) = h2f((uint16_t)dbits);
-        }
-    }
-};
-
-// K-quants: the row's 256-k block is 16-B aligned; task (row, 16-B chunk)
-template <int T> struct WStageK {
-    static constexpr int NCH = W8<T>::NCH, NT = 64 * NCH;
-    u32x4v w[3];
-    __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, uint32_t wbase, uint32_t nb01, int j) {
-#pragma unroll
-        for (int t = 0; t < 3; ++t) {
-            const int task = j + 256 * t;
-            const int row = task / NCH, ch = task % NCH;
-            // tasks past the block (t = 2 for some threads) read an in-range dummy, never stored
-            w[t] = bl128(rs, wbase + (uint32_t)min(row, 63) * nb01 + 16u * ch);
-        }
-    }
-    __device__ __forceinline__ void zero() {
-#pragma unroll
-        for (int t = 0; t < 3; ++t) w[t] = u32x4v{0, 0, 0, 0};
-    }
-    __device__ __forceinline__ void store(uint8_t *W, uint32_t, uint32_t, int j) const {
-#pragma unroll
-        for (int t = 0; t < 3; ++t) {
-            const int task = j + 256 * t;
-            if (task >= NT) break;
-            const int row = task / NCH, ch = task % NCH;
-            uint8_t *dst;
-            if (ch == 0) {
-                dst = W + W8<T>::WH + row * 16;
-            } else if (T == T_Q5_K && ch <= 2) {
-                dst = W + W8<T_Q5_K>::QH + pl_off(row, ch - 1);
-            } else {
-                const int c16 = ch - (T == T_Q5_K ? 3 : 1);
-                dst = W + W8<T>::WQ + (c16 >> 1) * 2048 + pl_off(row, c16 & 1);
-            }
-            lds_st128(dst, w[t]);
-        }
-    }
-};
-template <> struct WStage<T_Q4_K> : WStageK<T_Q4_K> {};
-template <> struct WStage<T_Q5_K> : WStageK<T_Q5_K> {};
-
-// ---- activation staging: 64 tokens x 256 B + scales (+ block sums) ----
-struct XStage {
-    u32x4v q[4];
-    float d;
-    u32x4v bs;
-    __device__ __forceinline__ void load(const int8_t *x8, const float *xd, const _Float16 *xbs, int64_t row0, int K,
-                                         int n_sb, int sb, int j, bool ksum) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int task = j + 256 * i, tok = task >> 4, c16 = task & 15;
-            q[i] = *reinterpret_cast<const u32x4v *>(x8 + (row0 + tok) * K + sb * Q8_QK + 16 * c16);
-        }
-        d = j < 64 ? xd[(row0 + j) * n_sb + sb] : 0.f;
-        if (ksum && j < 128)
-            bs = *reinterpret_cast<const u32x4v *>(xbs + ((row0 + (j >> 1)) * n_sb + sb) * 16 + 8 * (j & 1));
-    }
-    __device__ __forceinline__ void store(uint8_t *S, int j, bool ksum) const {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int task = j + 256 * i, tok = task >> 4, c16 = task & 15;
-            lds_st128(S + L_XQ + (c16 >> 1) * 2048 + pl_off(tok, c16 & 1), q[i]);
-        }
-        if (j < 64) reinterpret_cast<float *>(S + L_XD)[j] = d;
-        if (ksum && j < 128) lds_st128(S + L_XB + pl_off(j >> 1, j & 1), bs);
-    }
-};
-
+__device__ __forceinline__ void st128(uint8_t *p, u32x4v v) { *reinterpret_cast<u32x4v *>(p) = v; }
+__device__ __forceinline__ void st64(uint8_t *p, u32x2v v) { *reinterpret_cast<u32x2v *>(p) = v; }
+__device__ __forceinline__ u32x4v ld128(const uint8_t *p) { return *reinterpret_cast<const u32x4v *>(p); }
+__device__ __forceinline__ u32x2v ld64(const uint8_t *p) { return *reinterpret_cast<const u32x2v *>(p); }
+__device__ __forceinline__ float uf(uint32_t u) { return __builtin_bit_cast(float, u); }
+__device__ __forceinline__ uint32_t fu(float f) { return __builtin_bit_cast(uint32_t, f); }
 __device__ __forceinline__ i32x4 as_i4(u32x4v v) { return __builtin_bit_cast(i32x4, v); }
+__device__ __forceinline__ long as_l(u32x2v v) { return __builtin_bit_cast(long, v); }
 
-// ---- compute of one 256-k block by one wave: 32 tokens (A) x 32 weight rows (B) ----
-// acc[i]: token 32*tg + (i & 3) + 8 * (i >> 2) + 4 * h, weight row 32*rg + (lane & 31)
+// 16 B per lane from the buffer straight into LDS at lds_dst + 16 * lane (lds_dst wave-uniform)
+__device__ __forceinline__ void q8_dma16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_dst, uint32_t voff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds_dst, 16, voff, 0, 0, 0);
+}
+
+// ------------------------------------------------------------------------------------------
+// activations -> Q8_K blocks, written as stage images (restates quantize_row_q8_K_ref,
+// src/ggml-quants.c:2555-2591). A workgroup takes 16 tokens of one super-block; thread
+// (token t, piece p) holds k = 16p..16p+15 (64 B read per lane, a token's 1 KB by 16 lanes),
+// i.e. exactly one 16-B code piece of the image and one 16-element block sum.
+// ------------------------------------------------------------------------------------------
 template <int T>
-__device__ __forceinline__ void block_compute(const uint8_t *S, int rg, int tg, int lane, f32x16 &acc) {
-    const int r = lane & 31, h = lane >> 5;
-    const int wrow = 32 * rg + r, atok = 32 * tg + r;
-    const uint8_t *W = S + L_W;
-    const i32x16 zero16 = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    f32x16 p;
-    if constexpr (T == T_Q8_0 || T == T_Q4_0) {
-        const float4 d0 = *reinterpret_cast<const float4 *>(W + W8<T>::WD + pl_off(wrow, 0));
-        const float4 d1 = *reinterpret_cast<const float4 *>(W + W8<T>::WD + pl_off(wrow, 1));
-        const float dw[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+__global__ __launch_bounds__(256) void mmq8_quant_x(const MmArgs a, uint8_t *__restrict__ ximg, int n_tt, int n_sb) {
+    constexpr int XB = ximg_bytes<T>();
+    const int tid = threadIdx.x, p = tid & 15;
+    const int tok = (blockIdx.x / n_sb) * 16 + (tid >> 4), sb = blockIdx.x % n_sb;
+    const int slice = blockIdx.y;
+    const int i12 = slice % a.ne12, i13 = slice / a.ne12;
+    float v[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) p[i] = 0.f;
+    for (int i = 0; i < 16; ++i) v[i] = 0.f;
+    if (tok < a.M) {
+        const float *src = reinterpret_cast<const float *>(a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13 +
+                                                           (int64_t)tok * a.nb11) +
+                           sb * Q8_QK + p * 16;
+        if (a.x_aligned16) {
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            u32x4v bq;
-            if constexpr (T == T_Q8_0) {
-                bq = lds_ld128(W + W8<T>::WQ + b * 2048 + pl_off(wrow, h));
-            } else {   // Q4_0: k 0..15 low nibbles, 16..31 high nibbles, codes q - 8
-                const u32x4v raw = lds_ld128(W + W8<T>::WQ + b * 1024 + wrow * 16);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) bq[i] = sub8_bytes((raw[i] >> (4 * h)) & 0x0F0F0F0Fu);
+            for (int j = 0; j < 4; ++j) {
+                const float4 f = reinterpret_cast<const float4 *>(src)[j];
+                v[4 * j] = f.x; v[4 * j + 1] = f.y; v[4 * j + 2] = f.z; v[4 * j + 3] = f.w;
             }
-            const u32x4v aq = lds_ld128(S + L_XQ + b * 2048 + pl_off(atok, h));
-            const i32x16 R = __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i4(aq), as_i4(bq), zero16, 0, 0, 0);
+        } else {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) p[i] = __builtin_fmaf((float)R[i], dw[b], p[i]);
+            for (int i = 0; i < 16; ++i) v[i] = src[i];
         }
-    } else {   // Q4_K / Q5_K
-        const u32x4v hd = lds_ld128(W + W8<T>::WH + wrow * 16);
-        const uint32_t S3[3] = {hd[1], hd[2], hd[3]};
-        uint32_t sc[8], mn[8];
+    }
+    // the signed value of largest |x|, first k on ties (the reference's strict '>'), over the
+    // token's 16 lanes: (|x|, k, x) reduced with max |x|, then min k
+    float am = fabsf(v[0]), mx = v[0];
+    int idx = 16 * p;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) k4_scale_min_pair(S3, c, sc[2 * c], sc[2 * c + 1], mn[2 * c], mn[2 * c + 1]);
-        u32x4v qh = {0, 0, 0, 0};
-        if constexpr (T == T_Q5_K) qh = lds_ld128(W + W8<T_Q5_K>::QH + pl_off(wrow, h));
-        i32x16 pi = zero16;
+    for (int i = 1; i < 16; ++i)
+        if (fabsf(v[i]) > am) { am = fabsf(v[i]); mx = v[i]; idx = 16 * p + i; }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+        const float am2 = __shfl_xor(am, o), mx2 = __shfl_xor(mx, o);
+        const int idx2 = __shfl_xor(idx, o);
+        if (am2 > am || (am2 == am && idx2 < idx)) { am = am2; mx = mx2; idx = idx2; }
+    }
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    int s = 0;
+    float d = 0.f;
+    if (am != 0.f) {
+        const float iscale = -127.f / mx;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int q = min(127, (int)__builtin_rintf(iscale * v[i]));
+            s += q;
+            w[i >> 2] |= (uint32_t)(q & 0xff) << (8 * (i & 3));
+        }
+        d = 1.f / iscale;
+    }
+    uint8_t *img = ximg + (((int64_t)slice * n_tt + (tok >> 6)) * n_sb + sb) * XB;
+    const int tl = tok & 63, blk = p >> 1, h = p & 1;
+    if constexpr (T == T_Q6_K) {
+        *reinterpret_cast<u32x2v *>(img + blk * 2048 + h * 1024 + tl * 8) = u32x2v{w[0], w[1]};
+        *reinterpret_cast<u32x2v *>(img + blk * 2048 + h * 1024 + 512 + tl * 8) = u32x2v{w[2], w[3]};
+    } else {
+        *reinterpret_cast<u32x4v *>(img + blk * 2048 + h * 1024 + tl * 16) = u32x4v{w[0], w[1], w[2], w[3]};
+    }
+    if constexpr (q8_has_min<T>())
+        *reinterpret_cast<_Float16 *>(img + XI_BS + (p >> 3) * 1024 + tl * 16 + 2 * (p & 7)) = (_Float16)s;
+    if (p == 0) *reinterpret_cast<float *>(img + XI_DX + tl * 4) = d;
+}
+
+// ------------------------------------------------------------------------------------------
+// weight staging. Every thread loads its tasks of the row tile's super-block into registers one
+// stage ahead and, after the stage's MFMAs, decodes them into the LDS image. Tasks run along the
+// rows (consecutive lanes = consecutive blocks / chunks of one row), so a wave's 16-B loads
+// cover a few whole rows (coalesced) instead of one window of many rows.
+// ------------------------------------------------------------------------------------------
+struct RowTile {   // first row of the tile, rows of the matrix, row pitch, super-block offset
+    int row0, N;
+    uint32_t nb01, sboff;
+    __device__ __forceinline__ uint32_t rb(int row) const {
+        return (uint32_t)min(row0 + row, N - 1) * nb01 + sboff;
+    }
+};
+
+template <int T> struct WStage8;
+
+// Q8_0: task (row, block) = (t >> 3, t & 7), t = tid + 512 e. Rows and super-blocks are
+// dword-aligned (host check), so even blocks start dword-aligned (codes at +2) and odd blocks at
+// +2 (codes dword-aligned): one v_perm per dword realigns either.
+template <> struct WStage8<T_Q8_0> {
+    static constexpr int VMEM = 6;   // vector-memory instructions of one load()
+    uint32_t w[2][9];
+    template <int TR> __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, const RowTile &R, int tid) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int t = tid + 4 * TR * e;
+            const uint32_t o4 = (R.rb(t >> 3) + 34u * (t & 7)) & ~3u;
+            const u32x4v a0 = bl128(rs, o4), a1 = bl128(rs, o4 + 16);
+            w[e][0] = a0[0]; w[e][1] = a0[1]; w[e][2] = a0[2]; w[e][3] = a0[3];
+            w[e][4] = a1[0]; w[e][5] = a1[1]; w[e][6] = a1[2]; w[e][7] = a1[3];
+            w[e][8] = bl32(rs, o4 + 32);
+        }
+    }
+    template <int TR> __device__ __forceinline__ void store(uint8_t *W, const RowTile &, int tid) const {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int t = tid + 4 * TR * e, row = t >> 3, blk = t & 7, odd = blk & 1;
+            const uint32_t sel = odd ? 0x07060504u : 0x05040302u;
+            uint32_t c[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) c[i] = __builtin_amdgcn_perm(w[e][i + 1], w[e][i], sel);
+            const float d = h2f((uint16_t)(odd ? w[e][0] >> 16 : w[e][0] & 0xffffu));
+            st128(W + wslot16<T_Q8_0, TR>(blk, 0, row), u32x4v{c[0], c[1], c[2], c[3]});
+            st128(W + wslot16<T_Q8_0, TR>(blk, 1, row), u32x4v{c[4], c[5], c[6], c[7]});
+            *reinterpret_cast<float *>(W + wi_meta<TR>() + (blk >> 2) * 16 * TR + row * 16 + 4 * (blk & 3)) = d;
+        }
+    }
+};
+
+// Q4_0: as Q8_0 with 18-B blocks; codes decoded to q - 8
+template <> struct WStage8<T_Q4_0> {
+    static constexpr int VMEM = 4;
+    uint32_t w[2][5];
+    template <int TR> __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, const RowTile &R, int tid) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int t = tid + 4 * TR * e;
+            const uint32_t o4 = (R.rb(t >> 3) + 18u * (t & 7)) & ~3u;
+            const u32x4v a0 = bl128(rs, o4);
+            w[e][0] = a0[0]; w[e][1] = a0[1]; w[e][2] = a0[2]; w[e][3] = a0[3];
+            w[e][4] = bl32(rs, o4 + 16);
+        }
+    }
+    template <int TR> __device__ __forceinline__ void store(uint8_t *W, const RowTile &, int tid) const {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int t = tid + 4 * TR * e, row = t >> 3, blk = t & 7, odd = blk & 1;
+            const uint32_t sel = odd ? 0x07060504u : 0x05040302u;
+            uint32_t lo[4], hi[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t n = __builtin_amdgcn_perm(w[e][i + 1], w[e][i], sel);
+                lo[i] = sub8_bytes(n & 0x0F0F0F0Fu);          // k 0..15
+                hi[i] = sub8_bytes((n >> 4) & 0x0F0F0F0Fu);   // k 16..31
+            }
+            const float d = h2f((uint16_t)(odd ? w[e][0] >> 16 : w[e][0] & 0xffffu));
+            st128(W + wslot16<T_Q4_0, TR>(blk, 0, row), u32x4v{lo[0], lo[1], lo[2], lo[3]});
+            st128(W + wslot16<T_Q4_0, TR>(blk, 1, row), u32x4v{hi[0], hi[1], hi[2], hi[3]});
+            *reinterpret_cast<float *>(W + wi_meta<TR>() + (blk >> 2) * 16 * TR + row * 16 + 4 * (blk & 3)) = d;
+        }
+    }
+};
+
+// Q4_K / Q5_K (16-B aligned super-blocks): task (row, q) = (tid >> 2, tid & 3): qs chunks q and
+// q+4 (64-weight chunk c = q>>1 (+2), half h = q&1: low nibbles -> block 2c, high -> 2c+1);
+// Q5_K adds qh chunk h; q == 0 the header. meta [kg][row] = {d, dmin, sc (4 B), m (4 B)} of
+// sub-blocks 4kg..4kg+3
+template <int T> struct WStageK8 {
+    static constexpr bool Q5 = T == T_Q5_K;
+    static constexpr uint32_t QS = Q5 ? 48 : 16;
+    static constexpr int VMEM = Q5 ? 4 : 3;   // the header load runs on one lane in four, in every wave
+    u32x4v c[2], qh, hd;
+    template <int TR> __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, const RowTile &R, int tid) {
+        const int q = tid & 3;
+        const uint32_t rb = R.rb(tid >> 2);
+        c[0] = bl128(rs, rb + QS + 16u * q);
+        c[1] = bl128(rs, rb + QS + 16u * (q + 4));
+        if constexpr (Q5) qh = bl128(rs, rb + 16 + 16u * (q & 1));
+        if (q == 0) hd = bl128(rs, rb);
+    }
+    template <int TR> __device__ __forceinline__ void store(uint8_t *W, const RowTile &, int tid) const {
+        const int q = tid & 3, row = tid >> 2, h = q & 1;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int cc = (q >> 1) + 2 * e;   // 64-weight chunk
+            u32x4v lo, hi;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                lo[i] = c[e][i] & 0x0F0F0F0Fu;
+                hi[i] = (c[e][i] >> 4) & 0x0F0F0F0Fu;
+                if constexpr (Q5) {
+                    lo[i] |= ((qh[i] >> (2 * cc)) & 0x01010101u) << 4;
+                    hi[i] |= ((qh[i] >> (2 * cc + 1)) & 0x01010101u) << 4;
+                }
+            }
+            st128(W + wslot16<T, TR>(2 * cc, h, row), lo);
+            st128(W + wslot16<T, TR>(2 * cc + 1, h, row), hi);
+        }
+        if (q == 0) {   // get_scale_min_k4 (src/ggml-quants.c:703-710) in the packed form of quants.c:580-585
+            const uint32_t S0 = hd[1], S1 = hd[2], S2 = hd[3];
+            const uint32_t sc_lo = S0 & 0x3f3f3f3fu;
+            const uint32_t sc_hi = (S2 & 0x0f0f0f0fu) | (((S0 >> 6) & 0x03030303u) << 4);
+            const uint32_t mn_lo = S1 & 0x3f3f3f3fu;
+            const uint32_t mn_hi = ((S2 >> 4) & 0x0f0f0f0fu) | (((S1 >> 6) & 0x03030303u) << 4);
+            const uint32_t d = fu(h2f((uint16_t)(hd[0] & 0xffffu))), dmin = fu(h2f((uint16_t)(hd[0] >> 16)));
+            st128(W + wi_meta<TR>() + row * 16, u32x4v{d, dmin, sc_lo, mn_lo});
+            st128(W + wi_meta<TR>() + 16 * TR + row * 16, u32x4v{d, dmin, sc_hi, mn_hi});
+        }
+    }
+};
+template <> struct WStage8<T_Q4_K> : WStageK8<T_Q4_K> {};
+template <> struct WStage8<T_Q5_K> : WStageK8<T_Q5_K> {};
+
+// Q6_K (210-B super-blocks, 2-byte aligned): task (row, q) = (tid >> 2, tid & 3), half hf = q>>1,
+// k-half h = q&1 of each of the four 32-blocks 4hf..4hf+3: ql[64hf+16h..], ql[64hf+32+16h..],
+// qh[32hf+16h..] (16 B each), decoded as dequantize_row_q6_K (src/ggml-quants.c:1762-1791) to
+// q - 32; q == 0 also the scales and d. meta [kg = hf][row] = {d, sc[8kg .. 8kg+7] (int8), 0}
+template <> struct WStage8<T_Q6_K> {
+    static constexpr int VMEM = 8;
+    uint32_t w[3][5], s[5];
+    template <int TR> __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, const RowTile &R, int tid) {
+        const int q = tid & 3;
+        const uint32_t rb = R.rb(tid >> 2), hf = q >> 1, h = q & 1;
+        const uint32_t po[3] = {64 * hf + 16 * h, 64 * hf + 32 + 16 * h, 128 + 32 * hf + 16 * h};
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const uint32_t o4 = (rb + po[p]) & ~3u;
+            const u32x4v a0 = bl128(rs, o4);
+            w[p][0] = a0[0]; w[p][1] = a0[1]; w[p][2] = a0[2]; w[p][3] = a0[3];
+            w[p][4] = bl32(rs, o4 + 16);
+        }
+        if (q == 0) {
+            const uint32_t o4 = (rb + 192) & ~3u;
+            const u32x4v a0 = bl128(rs, o4);
+            s[0] = a0[0]; s[1] = a0[1]; s[2] = a0[2]; s[3] = a0[3];
+            s[4] = bl32(rs, o4 + 16);
+        }
+    }
+    template <int TR> __device__ __forceinline__ void store(uint8_t *W, const RowTile &R, int tid) const {
+        const int q = tid & 3, row = tid >> 2, hf = q >> 1, h = q & 1;
+        const uint32_t sel = (R.rb(row) & 2) ? 0x05040302u : 0x03020100u;   // realign by 0 or 2 bytes
+        uint32_t la[4], lb[4], qh[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            la[i] = __builtin_amdgcn_perm(w[0][i + 1], w[0][i], sel);
+            lb[i] = __builtin_amdgcn_perm(w[1][i + 1], w[1][i], sel);
+            qh[i] = __builtin_amdgcn_perm(w[2][i + 1], w[2][i], sel);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            uint32_t v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                uint32_t x;
+                if (t == 0) x = (la[i] & 0x0F0F0F0Fu) | ((qh[i] << 4) & 0x30303030u);
+                else if (t == 1) x = (lb[i] & 0x0F0F0F0Fu) | ((qh[i] << 2) & 0x30303030u);
+                else if (t == 2) x = ((la[i] >> 4) & 0x0F0F0F0Fu) | (qh[i] & 0x30303030u);
+                else x = ((lb[i] >> 4) & 0x0F0F0F0Fu) | ((qh[i] >> 2) & 0x30303030u);
+                v[i] = sub32_bytes(x);
+            }
+            const int blk = 4 * hf + t;
+            st64(W + wslot8<TR>(blk, h, 0, row), u32x2v{v[0], v[1]});
+            st64(W + wslot8<TR>(blk, h, 1, row), u32x2v{v[2], v[3]});
+        }
+        if (q == 0) {
+            uint32_t sc[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sc[i] = __builtin_amdgcn_perm(s[i + 1], s[i], sel);
+            const uint32_t dd = __builtin_amdgcn_perm(s[4], s[4], sel) & 0xffffu;
+            const uint32_t d = fu(h2f((uint16_t)dd));
+            st128(W + wi_meta<TR>() + row * 16, u32x4v{d, sc[0], sc[1], 0u});
+            st128(W + wi_meta<TR>() + 16 * TR + row * 16, u32x4v{d, sc[2], sc[3], 0u});
+        }
+    }
+};
+
+// ------------------------------------------------------------------------------------------
+// one super-block of one wave: NG K-groups of 4 blocks starting at group g0 (NG = 1: the
+// workgroup splits the super-block between two K-groups of waves; NG = 2: the wave takes all 8
+// blocks), tokens 32tg.. of the activation image X x rows 64rg.. (two 32x32 tiles).
+// acc[ti][i]: token 32tg + 8(i>>2) + 4hl + (i&3), weight row 64rg + 32ti + (lane & 31)
+// Software pipeline of depth one: the MFMAs of step s are issued before the results of step s-1
+// are consumed, and a scheduling barrier per step keeps the compiler from hoisting every step's
+// MFMAs (their int32 results would not fit the register budget of 2 waves / SIMD).
+// ------------------------------------------------------------------------------------------
+template <int T, int NG, int TR>
+__device__ __forceinline__ void q8_sb_compute(const uint8_t *W, const uint8_t *X, int g0, int rg, int tg, int lane,
+                                              f32x16 &acc0, f32x16 &acc1) {
+    const int r = lane & 31, hl = lane >> 5;
+    const int row0 = 64 * rg + r, row1 = row0 + 32, tok = 32 * tg + r;
+    f32x16 p0, p1;
+    i32x16 zero;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { p0[i] = 0.f; p1[i] = 0.f; zero[i] = 0; }
+    if constexpr (T == T_Q8_0 || T == T_Q4_0) {
+        i32x16 magic;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) magic[i] = (int)Q8_MAGIC_I;
+        float dsum0 = 0.f, dsum1 = 0.f;
+#pragma unroll
+        for (int g = g0; g < g0 + NG; ++g) {
+            const u32x4v m0 = ld128(W + wi_meta<TR>() + g * 16 * TR + row0 * 16);
+            const u32x4v m1 = ld128(W + wi_meta<TR>() + g * 16 * TR + row1 * 16);
+            auto issue = [&](int bi, i32x16 &R0, i32x16 &R1) {
+                const int blk = 4 * g + bi;
+                const u32x4v A = ld128(X + blk * 2048 + hl * 1024 + tok * 16);
+                const u32x4v B0 = ld128(W + wslot16<T, TR>(blk, hl, row0));
+                const u32x4v B1 = ld128(W + wslot16<T, TR>(blk, hl, row1));
+                R0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i4(A), as_i4(B0), magic, 0, 0, 0);
+                R1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i4(A), as_i4(B1), magic, 0, 0, 0);
+            };
+            auto consume = [&](int bi, const i32x16 &R0, const i32x16 &R1) {
+                const float d0 = uf(m0[bi]), d1 = uf(m1[bi]);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    p0[i] = __builtin_fmaf(uf((uint32_t)R0[i]), d0, p0[i]);
+                    p1[i] = __builtin_fmaf(uf((uint32_t)R1[i]), d1, p1[i]);
+                }
+                asm volatile("" : "+v"(p0), "+v"(p1));
+            };
+            i32x16 Ra0, Ra1, Rb0, Rb1;
+            issue(0, Ra0, Ra1);
+            issue(1, Rb0, Rb1);
+            consume(0, Ra0, Ra1);
+            __builtin_amdgcn_sched_barrier(0);
+            issue(2, Ra0, Ra1);
+            consume(1, Rb0, Rb1);
+            __builtin_amdgcn_sched_barrier(0);
+            issue(3, Rb0, Rb1);
+            consume(2, Ra0, Ra1);
+            __builtin_amdgcn_sched_barrier(0);
+            consume(3, Rb0, Rb1);
+            dsum0 += (uf(m0[0]) + uf(m0[1])) + (uf(m0[2]) + uf(m0[3]));
+            dsum1 += (uf(m1[0]) + uf(m1[1])) + (uf(m1[2]) + uf(m1[3]));
+        }
+        const float c0 = Q8_MAGIC_F * dsum0, c1 = Q8_MAGIC_F * dsum1;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { p0[i] -= c0; p1[i] -= c1; }
+    } else {   // K-quants: integer sub-block (or 16-group) scales, exact int32 sums
+        i32x16 pi0, pi1;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { pi0[i] = 0; pi1[i] = 0; }
+        auto consume = [&](int s0, int s1, const i32x16 &R0, const i32x16 &R1) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                pi0[i] += __mul24(R0[i], s0);
+                pi1[i] += __mul24(R1[i], s1);
+            }
+            // integer adds may be reassociated: without this the compiler multiplies every step's
+            // results first and keeps all of them live (spills); pin the accumulators per step
+            asm volatile("" : "+v"(pi0), "+v"(pi1));
+        };
+        float dd0 = 0.f, dd1 = 0.f, dm0 = 0.f, dm1 = 0.f;
+#pragma unroll
+        for (int g = g0; g < g0 + NG; ++g) {
+            const u32x4v m0 = ld128(W + wi_meta<TR>() + g * 16 * TR + row0 * 16);
+            const u32x4v m1 = ld128(W + wi_meta<TR>() + g * 16 * TR + row1 * 16);
+            dd0 = uf(m0[0]); dd1 = uf(m1[0]); dm0 = uf(m0[1]); dm1 = uf(m1[1]);
+            if constexpr (T == T_Q4_K || T == T_Q5_K) {
+                auto issue = [&](int bi, i32x16 &R0, i32x16 &R1) {
+                    const int blk = 4 * g + bi;
+                    const u32x4v A = ld128(X + blk * 2048 + hl * 1024 + tok * 16);
+                    const u32x4v B0 = ld128(W + wslot16<T, TR>(blk, hl, row0));
+                    const u32x4v B1 = ld128(W + wslot16<T, TR>(blk, hl, row1));
+                    R0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i4(A), as_i4(B0), zero, 0, 0, 0);
+                    R1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i4(A), as_i4(B1), zero, 0, 0, 0);
+                };
+                auto sc = [&](const u32x4v &m, int bi) { return (int)((m[2] >> (8 * bi)) & 0xffu); };
+                i32x16 Ra0, Ra1, Rb0, Rb1;
+                issue(0, Ra0, Ra1);
+                issue(1, Rb0, Rb1);
+                consume(sc(m0, 0), sc(m1, 0), Ra0, Ra1);
+                __builtin_amdgcn_sched_barrier(0);
+                issue(2, Ra0, Ra1);
+                consume(sc(m0, 1), sc(m1, 1), Rb0, Rb1);
+                __builtin_amdgcn_sched_barrier(0);
+                issue(3, Rb0, Rb1);
+                consume(sc(m0, 2), sc(m1, 2), Ra0, Ra1);
+                __builtin_amdgcn_sched_barrier(0);
+                consume(sc(m0, 3), sc(m1, 3), Rb0, Rb1);
+            } else {   // Q6_K: 8 scale groups q = 2 bi + h per K-group, one 32x32x16 MFMA each
+                auto issue = [&](int q, i32x16 &R0, i32x16 &R1) {
+                    const int blk = 4 * g + (q >> 1), h = q & 1;
+                    const u32x2v A = ld64(X + blk * 2048 + h * 1024 + hl * 512 + tok * 8);
+                    const u32x2v B0 = ld64(W + wslot8<TR>(blk, h, hl, row0));
+                    const u32x2v B1 = ld64(W + wslot8<TR>(blk, h, hl, row1));
+                    R0 = __builtin_amdgcn_mfma_i32_32x32x16_i8(as_l(A), as_l(B0), zero, 0, 0, 0);
+                    R1 = __builtin_amdgcn_mfma_i32_32x32x16_i8(as_l(A), as_l(B1), zero, 0, 0, 0);
+                };
+                auto sc = [&](const u32x4v &m, int q) {
+                    return (int)(int8_t)(uint8_t)((q < 4 ? m[1] : m[2]) >> (8 * (q & 3)));
+                };
+                i32x16 Ra0, Ra1, Rb0, Rb1;
+                issue(0, Ra0, Ra1);
+#pragma unroll
+                for (int q = 1; q < 8; ++q) {
+                    if (q & 1) issue(q, Rb0, Rb1);
+                    else issue(q, Ra0, Ra1);
+                    if (q & 1) consume(sc(m0, q - 1), sc(m1, q - 1), Ra0, Ra1);
+                    else consume(sc(m0, q - 1), sc(m1, q - 1), Rb0, Rb1);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                consume(sc(m0, 7), sc(m1, 7), Rb0, Rb1);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { p0[i] = dd0 * (float)pi0[i]; p1[i] = dd1 * (float)pi1[i]; }
+        if constexpr (T == T_Q4_K || T == T_Q5_K) {
+            if (g0 == 0) {   // sum_j m_j * bsum_j over all 8 sub-blocks: k16-sum e pairs with m_(e>>1)
+                const f16x8 As = __builtin_bit_cast(f16x8, ld128(X + XI_BS + hl * 1024 + tok * 16));
+                const uint32_t mw0 = *reinterpret_cast<const uint32_t *>(W + wi_meta<TR>() + hl * 16 * TR + row0 * 16 + 12);
+                const uint32_t mw1 = *reinterpret_cast<const uint32_t *>(W + wi_meta<TR>() + hl * 16 * TR + row1 * 16 + 12);
+                f16x8 Bm0, Bm1;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    Bm0[e] = (_Float16)(float)((mw0 >> (8 * (e >> 1))) & 0xffu);
+                    Bm1[e] = (_Float16)(float)((mw1 >> (8 * (e >> 1))) & 0xffu);
+                }
+                f32x16 zf;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) zf[i] = 0.f;
+                const f32x16 mins0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(As, Bm0, zf, 0, 0, 0);
+                const f32x16 mins1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(As, Bm1, zf, 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    p0[i] = __builtin_fmaf(-dm0, mins0[i], p0[i]);
+                    p1[i] = __builtin_fmaf(-dm1, mins1[i], p1[i]);
+                }
+            }
+        }
+    }
+    const float *XD = reinterpret_cast<const float *>(X + XI_DX);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float4 dx = *reinterpret_cast<const float4 *>(XD + 32 * tg + 8 * q + 4 * hl);
+        const float dv[4] = {dx.x, dx.y, dx.z, dx.w};
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            const u32x4v raw = lds_ld128(W + W8<T>::WQ + c * 2048 + pl_off(wrow, h));
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int j = 2 * c + e;
-                u32x4v bq;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    uint32_t v = (raw[i] >> (4 * e)) & 0x0F0F0F0Fu;
-                    if constexpr (T == T_Q5_K) v |= ((qh[i] >> j) & 0x01010101u) << 4;
-                    bq[i] = v;
-                }
-                const u32x4v aq = lds_ld128(S + L_XQ + j * 2048 + pl_off(atok, h));
-                const i32x16 R = __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i4(aq), as_i4(bq), zero16, 0, 0, 0);
-#pragma unroll
-                for (int i = 0; i < 16; ++i) pi[i] += __mul24(R[i], (int)sc[j]);
-            }
+            acc0[4 * q + c] = __builtin_fmaf(p0[4 * q + c], dv[c], acc0[4 * q + c]);
+            acc1[4 * q + c] = __builtin_fmaf(p1[4 * q + c], dv[c], acc1[4 * q + c]);
         }
-        // sum_j m_j * bsum_j: A = the token's 16 block sums of 16 (k = 8h + i), B = m_(k/2)
-        const u32x4v bsr = lds_ld128(S + L_XB + pl_off(atok, h));
-        const f16x8 am = __builtin_bit_cast(f16x8, bsr);
-        f16x8 bm;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) bm[i] = (_Float16)(float)mn[4 * h + (i >> 1)];
-        const f32x16 zf = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        const f32x16 mins = __builtin_amdgcn_mfma_f32_32x32x16_f16(am, bm, zf, 0, 0, 0);
-        const float d = h2f((uint16_t)(hd[0] & 0xffff)), dmin = h2f((uint16_t)(hd[0] >> 16));
-#pragma unroll
-        for (int i = 0; i < 16; ++i) p[i] = __builtin_fmaf(d, (float)pi[i], -dmin * mins[i]);
-    }
-    const float *XD = reinterpret_cast<const float *>(S + L_XD);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        const float4 dx = *reinterpret_cast<const float4 *>(XD + 32 * tg + 8 * g + 4 * h);
-        acc[4 * g + 0] = __builtin_fmaf(p[4 * g + 0], dx.x, acc[4 * g + 0]);
-        acc[4 * g + 1] = __builtin_fmaf(p[4 * g + 1], dx.y, acc[4 * g + 1]);
-        acc[4 * g + 2] = __builtin_fmaf(p[4 * g + 2], dx.z, acc[4 * g + 2]);
-        acc[4 * g + 3] = __builtin_fmaf(p[4 * g + 3], dx.w, acc[4 * g + 3]);
     }
 }
 
-// grid: (ceil(N / 64), Mpad / 64, slices); KG K-groups of 4 waves
-template <int T, int KG>
-__global__ __launch_bounds__(256 * KG) void mmq8_kernel(const MmArgs a, const int8_t *__restrict__ x8,
-                                                        const float *__restrict__ xd,
-                                                        const _Float16 *__restrict__ xbs, int Mpad, uint32_t w_extent) {
-    constexpr int SBYTES = stage_bytes<T>();
-    constexpr bool KSUM = T == T_Q4_K || T == T_Q5_K;
-    __shared__ __align__(16) uint8_t lds[KG * SBYTES];
-    const int K = a.K, n_sb = K / Q8_QK;
-    const int slice = blockIdx.z;
+// copy one activation image (XB bytes, whole KiB pieces) into LDS: wave w takes pieces w, w+NW, ..
+template <int T, int NW>
+__device__ __forceinline__ void q8_x_dma(__amdgpu_buffer_rsrc_t xr, uint32_t img_off, uint8_t *X, int wave, int lane) {
+    constexpr int NP = ximg_bytes<T>() / 1024;
+#pragma unroll
+    for (int p = wave; p < NP; p += NW) q8_dma16(xr, X + p * 1024, img_off + p * 1024 + lane * 16);
+}
+
+// grid.x = n_rt * ksplit * n_tt (token tiles fastest; XCD-remapped when a multiple of 8),
+// grid.y = slices. TR weight rows x TT tokens per workgroup, TR / 16 waves of 64 rows x 32
+// tokens:
+//   TT = 64:  two K-groups of waves split every super-block (blocks 0-3 / 4-7), reduced through
+//             LDS at the end;
+//   TT = 128: every wave takes whole super-blocks (the weight stage serves twice the tokens).
+//   TR = 64 halves the workgroup (4 waves, ~70 KB of LDS) so that two run on one CU and their
+//   load / compute phases interleave.
+template <int T, int TT, int TR>
+__global__ __launch_bounds__(4 * TR) void mmq8_kernel(const MmArgs a, const uint8_t *__restrict__ ximg, int n_tt,
+                                                      int ksplit, int sb_per, uint32_t w_extent,
+                                                      float *__restrict__ part, int xcd_remap) {
+    constexpr int NW = TR / 16;                    // waves
+    constexpr int WB = wi_bytes<TR>();
+    constexpr int XB = ximg_bytes<T>();
+    constexpr int NI = TT / Q8_TOK;                // activation images per stage
+    constexpr int N_XS = (TT == 64 && TR == 128) ? 3 : 2;   // activation stage ring
+    constexpr int DX = N_XS - 1;                   // activation DMA distance (super-blocks ahead)
+    // LDS: two weight stages (decoded one super-block ahead from registers loaded two ahead) and
+    // the activation ring (LDS-DMA DX super-blocks ahead)
+    __shared__ __align__(16) uint8_t lds[2 * WB + N_XS * NI * XB];
+    uint8_t *const Xs = lds + 2 * WB;
+    const int n_sb = a.K / Q8_QK;
+    int v = blockIdx.x;
+    if (xcd_remap) v = (v & 7) * (int)(gridDim.x >> 3) + (v >> 3);
+    const int tt = v % n_tt;
+    v /= n_tt;
+    const int ks = v % ksplit, rt = v / ksplit;
+    const int sb0 = ks * sb_per, sb1 = min(n_sb, sb0 + sb_per);
+    const int slice = blockIdx.y;
     const int i12 = slice % a.ne12, i13 = slice / a.ne12;
     const uint8_t *wmat = a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03;
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void *)wmat, 0, w_extent, Q8_RSRC_W3);
-    const int row0 = blockIdx.x * Q8_TILE, tok0 = blockIdx.y * Q8_TILE;
-    const int64_t xrow0 = (int64_t)slice * Mpad + tok0;
-    const uint32_t nb01 = (uint32_t)a.nb01;
+    // the NI consecutive 64-token images of this tile: [slice][64-token tile][sb][image]
+    const uint8_t *xbase = ximg + ((int64_t)slice * n_tt * NI + (int64_t)tt * NI) * n_sb * XB;
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)xbase, 0, (uint32_t)(NI * n_sb * XB), Q8_RSRC_W3);
 
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int kg = wave >> 2, rg = wave & 1, tg = (wave >> 1) & 1;
-    const int j = threadIdx.x & 255;
-    uint8_t *S = lds + kg * SBYTES;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // wave roles: rg = 64-row group, tg = 32-token group, kg = K-group (TT = 64)
+    constexpr int NRG = TR / 64, NTG = TT / 32, NKG = NW / (NRG * NTG);
+    static_assert(NKG == (TT == 64 ? 2 : 1), "wave layout");
+    const int rg = wave % NRG, tg = (wave / NRG) % NTG, kg = wave / (NRG * NTG);
+    constexpr uint32_t SBB = (uint32_t)QT<T>::bytes * (Q8_QK / QT<T>::blck);   // bytes of one row's super-block
+    constexpr int NP_MIN = NI * (XB / 1024) / NW;  // fewest activation pieces one wave copies per stage
+    auto rowtile = [&](int sb) { return RowTile{rt * TR, a.N, (uint32_t)a.nb01, (uint32_t)sb * SBB}; };
 
-    WStage<T> ws;
-    XStage xs;
-    const int iters = (n_sb + KG - 1) / KG;
-    auto load = [&](int sb) {
-        if (sb < n_sb) {
-            ws.load(wr, (uint32_t)row0 * nb01 + (uint32_t)sb * W8<T>::SBB, nb01, j);
-            xs.load(x8, xd, xbs, xrow0, K, n_sb, sb, j, KSUM);
-        }
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { acc0[i] = 0.f; acc1[i] = 0.f; }
+
+    // a.diag (GGML_MI355X_DIAG, measurements only): bit0 skips the activation DMA, bit1 the
+    // weight loads / decode, bit2 the MFMA compute
+    const int diag = a.diag;
+    auto x_issue = [&](int sb) {
+        if (diag & 1) return;
+        uint8_t *dst = Xs + ((sb - sb0) % N_XS) * NI * XB;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) q8_x_dma<T, NW>(xr, (uint32_t)((i * n_sb + sb) * XB), dst + i * XB, wave, lane);
     };
-    f32x16 acc;
+    WStage8<T> wa, wb;
+    if (sb0 < sb1) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    load(kg);
-    for (int it = 0; it < iters; ++it) {
-        const int sb = kg + it * KG;
-        __syncthreads();   // the previous block's compute is done with the LDS image
-        if (sb < n_sb) {
-            ws.store(S + L_W, (uint32_t)row0 * nb01 + (uint32_t)sb * W8<T>::SBB, nb01, j);
-            xs.store(S, j, KSUM);
-        }
-        __syncthreads();
-        load(sb + KG);     // next block's global loads fly during this block's MFMAs
-        if (sb < n_sb) block_compute<T>(S, rg, tg, lane, acc);
+        for (int d = 0; d < DX; ++d)
+            if (sb0 + d < sb1) x_issue(sb0 + d);
+        if (!(diag & 2)) wa.template load<TR>(wr, rowtile(sb0), tid);
+        if (sb0 + 1 < sb1 && !(diag & 2)) wb.template load<TR>(wr, rowtile(sb0 + 1), tid);
+        if (!(diag & 2)) wa.template store<TR>(lds, rowtile(sb0), tid);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
     }
-    // K-group reduction through LDS, then the store: dst[token][row] (coalesced rows per i)
-    if constexpr (KG > 1) {
-        __syncthreads();
+    // one super-block: X(sb+DX) DMA and W(sb+2) loads into `ld` (the set that held sb), MFMAs of
+    // sb, decode of W(sb+1) from `st` into its stage, wait for X(sb+1), one barrier
+    auto step = [&](int sb, WStage8<T> &ld, WStage8<T> &st) {
+        const int it = sb - sb0;
+        const bool xmore = sb + DX < sb1, wmore = sb + 2 < sb1;
+        if (xmore) x_issue(sb + DX);
+        if (wmore && !(diag & 2)) ld.template load<TR>(wr, rowtile(sb + 2), tid);
+        if (!(diag & 4)) {
+            const uint8_t *Xc = Xs + (it % N_XS) * NI * XB;
+            if constexpr (TT == 64)
+                q8_sb_compute<T, 1, TR>(lds + (it & 1) * WB, Xc, kg, rg, tg, lane, acc0, acc1);
+            else
+                q8_sb_compute<T, 2, TR>(lds + (it & 1) * WB, Xc + (tg >> 1) * XB, 0, rg, tg & 1, lane, acc0, acc1);
+        }
+        if (sb + 1 < sb1 && !(diag & 2)) st.template store<TR>(lds + ((it + 1) & 1) * WB, rowtile(sb + 1), tid);
+        // X(sb+1) must have landed: the only younger memory operations are this step's W(sb+2)
+        // loads and (DX = 2) this step's X(sb+2) pieces
+        if (wmore && (DX == 1 || xmore)) {
+            if constexpr (DX == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WStage8<T>::VMEM + NP_MIN) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WStage8<T>::VMEM) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        lds_barrier();
+    };
+    for (int sb = sb0; sb < sb1; sb += 2) {
+        step(sb, wa, wb);
+        if (sb + 1 < sb1) step(sb + 1, wb, wa);
+    }
+
+    // K-group reduction through LDS (the stages are free after the loop's last barrier)
+    if constexpr (NKG == 2) {
         float *red = reinterpret_cast<float *>(lds);
-        if (kg > 0) {
+        const int wl = wave % (NW / 2);
+        if (kg == 1) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) red[(((kg - 1) * 4 + (wave & 3)) * 16 + i) * 64 + lane] = acc[i];
+            for (int i = 0; i < 16; ++i) {
+                red[((wl * 2 + 0) * 16 + i) * 64 + lane] = acc0[i];
+                red[((wl * 2 + 1) * 16 + i) * 64 + lane] = acc1[i];
+            }
         }
-        __syncthreads();
-        if (kg > 0) return;
+        lds_barrier();
+        if (kg == 1) return;
 #pragma unroll
-        for (int g = 1; g < KG; ++g)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) acc[i] += red[(((g - 1) * 4 + wave) * 16 + i) * 64 + lane];
+        for (int i = 0; i < 16; ++i) {
+            acc0[i] += red[((wl * 2 + 0) * 16 + i) * 64 + lane];
+            acc1[i] += red[((wl * 2 + 1) * 16 + i) * 64 + lane];
+        }
     }
-    const int row = row0 + 32 * rg + (lane & 31);
-    if (row >= a.N) return;
-    uint8_t *dmat = a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3;
+    const int r = lane & 31, hl = lane >> 5;
+    const int tok0 = tt * TT + 32 * tg + 4 * hl;
+    const int rowA = rt * TR + 64 * rg + r, rowB = rowA + 32;
+    uint8_t *dbase;
+    int64_t ldd;
+    if (ksplit > 1) {   // part[ks][slice][token][row]
+        dbase = reinterpret_cast<uint8_t *>(part + ((int64_t)ks * gridDim.y + slice) * a.M * a.N);
+        ldd = (int64_t)a.N * 4;
+    } else {
+        dbase = a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3;
+        ldd = a.nb1;
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        const int tok = tok0 + 32 * tg + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-        if (tok < a.M) reinterpret_cast<float *>(dmat + (int64_t)tok * a.nb1)[row] = acc[i];
+        const int tok = tok0 + 8 * (i >> 2) + (i & 3);
+        if (tok < a.M) {
+            float *drow = reinterpret_cast<float *>(dbase + (int64_t)tok * ldd);
+            if (rowA < a.N) drow[rowA] = acc0[i];
+            if (rowB < a.N) drow[rowB] = acc1[i];
+        }
     }
+}
+
+// dst[slice][token][row] = sum over s of part[s][slice][token][row], in s order
+__global__ __launch_bounds__(256) void mmq8_split_reduce(const MmArgs a, const float *__restrict__ part, int ksplit,
+                                                         int slices) {
+    const int64_t per_slice = (int64_t)a.M * a.N;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= per_slice * slices) return;
+    const int slice = (int)(i / per_slice);
+    const int64_t rem = i % per_slice;
+    const int tok = (int)(rem / a.N), row = (int)(rem % a.N);
+    float v = 0.f;
+    for (int s = 0; s < ksplit; ++s) v += part[((int64_t)s * slices + slice) * per_slice + rem];
+    const int i12 = slice % a.ne12, i13 = slice / a.ne12;
+    reinterpret_cast<float *>(a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3 + (int64_t)tok * a.nb1)[row] = v;
 }
 
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
-bool mmq8_supported(int type, const MmArgs &a) {
-    if (!(type == T_Q4_0 || type == T_Q8_0 || type == T_Q4_K || type == T_Q5_K)) return false;
-    if (a.K % Q8_QK != 0 || a.M <= 0) return false;
-    // dword-aligned rows (Q4_0 / Q8_0 windows), 16-B aligned 256-k row segments (K-quants)
-    const uintptr_t al = (type == T_Q4_K || type == T_Q5_K) ? 15 : 3;
-    if ((reinterpret_cast<uintptr_t>(a.w) & al) || (a.nb01 & al) || (a.nb02 & al) || (a.nb03 & al)) return false;
-    const int64_t row_b = (int64_t)a.K / type_blck(type) * type_bytes(type);
-    const int64_t w_span = (int64_t)(a.N + Q8_TILE) * a.nb01 + row_b;
-    const int64_t slices = (int64_t)a.ne12 * a.ne13;
-    const int64_t mpad = (a.M + Q8_TILE - 1) / Q8_TILE * Q8_TILE;
-    return a.nb01 >= row_b && w_span < (1LL << 32) && slices * mpad * a.K < (1LL << 31);
+static int ximg_bytes_rt(int type) {
+    switch (type) {
+        case T_Q4_K: case T_Q5_K: return ximg_bytes<T_Q4_K>();
+        default: return ximg_bytes<T_Q8_0>();
+    }
 }
 
-template <int T, int KG>
-static void launch8(const MmArgs &a, const int8_t *x8, const float *xd, const _Float16 *xbs, int Mpad, int slices,
-                    hipStream_t st) {
-    const dim3 grid((a.N + Q8_TILE - 1) / Q8_TILE, Mpad / Q8_TILE, slices);
-    const int64_t row_b = (int64_t)a.K / QT<T>::blck * QT<T>::bytes;
-    // windows of the last block may reach 2 bytes past the row: round the range up to a dword
-    const uint32_t w_extent = (uint32_t)(((int64_t)(a.N - 1) * a.nb01 + row_b + 3) & ~(int64_t)3);
-    hipLaunchKernelGGL((mmq8_kernel<T, KG>), grid, dim3(256 * KG), 0, st, a, x8, xd, xbs, Mpad, w_extent);
+bool mmq8_supported(int type, const MmArgs &a) {
+    if (!(type == T_Q4_0 || type == T_Q8_0 || type == T_Q4_K || type == T_Q5_K || type == T_Q6_K)) return false;
+    if (a.K % Q8_QK != 0 || a.M <= 0) return false;
+    // Q4_K / Q5_K: 16-B aligned row super-blocks; Q4_0 / Q8_0: dword-aligned (the block parity
+    // pattern of WStage8 relies on it)
+    // (Q6_K: matrices dword-aligned, rows 2-byte aligned: realigned per lane)
+    const uintptr_t al = (type == T_Q4_K || type == T_Q5_K) ? 15 : 3;
+    const uintptr_t al1 = type == T_Q6_K ? 1 : al;
+    // (the matrix strides matter only where there is more than one matrix)
+    const bool many2 = a.ne12 / a.r2 > 1, many3 = a.ne13 / a.r3 > 1;
+    if ((reinterpret_cast<uintptr_t>(a.w) & al) || (a.nb01 & al1) || (many2 && (a.nb02 & al)) || (many3 && (a.nb03 & al)))
+        return false;
+    const int64_t row_b = (int64_t)a.K / type_blck(type) * type_bytes(type);
+    const int64_t w_span = (int64_t)a.N * a.nb01 + row_b + 4;
+    const int64_t n_tt = (a.M + Q8_TOK - 1) / Q8_TOK;
+    const int64_t img_slice = n_tt * (a.K / Q8_QK) * ximg_bytes_rt(type);
+    return a.nb01 >= row_b && w_span < (1LL << 32) && img_slice < (1LL << 31);
 }
 
 template <int T>
-static void launch8_kg(int kg, const MmArgs &a, const int8_t *x8, const float *xd, const _Float16 *xbs, int Mpad,
-                       int slices, hipStream_t st) {
-    if (kg >= 2) launch8<T, 2>(a, x8, xd, xbs, Mpad, slices, st);
-    else launch8<T, 1>(a, x8, xd, xbs, Mpad, slices, st);
+static void launch8(const MmArgs &a, uint8_t *ximg, int tr_rows, int tt_tok, int n_tt, int slices, int ksplit,
+                    int sb_per, float *part, hipStream_t st) {
+    const int n_sb = a.K / Q8_QK;
+    const int n_img = n_tt * (tt_tok / Q8_TOK);   // 64-token images per slice (tokens past M: zeros)
+    hipLaunchKernelGGL(mmq8_quant_x<T>, dim3((unsigned)(n_img * (Q8_TOK / 16) * n_sb), slices), dim3(256), 0, st, a, ximg,
+                       n_img, n_sb);
+    const int64_t row_b = (int64_t)a.K / QT<T>::blck * QT<T>::bytes;
+    // windows of the last super-block may reach 2 bytes past the row: round the range up to a dword
+    const uint32_t w_extent = (uint32_t)(((int64_t)(a.N - 1) * a.nb01 + row_b + 3) & ~(int64_t)3);
+    const int n_rt = (a.N + tr_rows - 1) / tr_rows;
+    const unsigned gx = (unsigned)(n_rt * ksplit * n_tt);
+    const int remap = (gx % 8 == 0) ? 1 : 0;
+    const dim3 grid(gx, slices);
+#define Q8_LAUNCH(TTv, TRv)                                                                                          \
+    hipLaunchKernelGGL((mmq8_kernel<T, TTv, TRv>), grid, dim3(4 * TRv), 0, st, a, (const uint8_t *)ximg, n_tt, ksplit, \
+                       sb_per, w_extent, part, remap)
+    if (tt_tok == 128) Q8_LAUNCH(128, 128);
+    else if (tr_rows == 128) Q8_LAUNCH(64, 128);
+    else Q8_LAUNCH(64, 64);   // measured slower than 128 rows at every shape; kept for A/B
+#undef Q8_LAUNCH
+    if (ksplit > 1) {
+        const int64_t n = (int64_t)slices * a.M * a.N;
+        hipLaunchKernelGGL(mmq8_split_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, (const float *)part,
+                           ksplit, slices);
+    }
 }
 
 hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch) {
     const int slices = a.ne12 * a.ne13;
-    const int Mpad = (a.M + Q8_TILE - 1) / Q8_TILE * Q8_TILE;
     const int n_sb = a.K / Q8_QK;
-    const size_t x8_bytes = ((size_t)slices * Mpad * a.K + 255) & ~(size_t)255;
-    const size_t xd_bytes = ((size_t)slices * Mpad * n_sb * sizeof(float) + 255) & ~(size_t)255;
-    const size_t xb_bytes = (size_t)slices * Mpad * n_sb * 16 * sizeof(_Float16);
-    uint8_t *buf = static_cast<uint8_t *>(scratch.get(x8_bytes + xd_bytes + xb_bytes, st));
+    // rows x tokens per workgroup: 128-token tiles once they alone give every CU a workgroup
+    // (the weight stage then serves twice the tokens); GGML_MI355X_MMQ8_TT / _TR override
+    // (measurements; 128 tokens always run 128 rows)
+    int tt_tok = (int64_t)((a.N + 127) / 128) * ((a.M + 127) / 128) * slices >= 256 ? 128 : 64;
+    if (const char *e = getenv("GGML_MI355X_MMQ8_TT")) tt_tok = atoi(e) == 128 ? 128 : 64;
+    int tr_rows = 128;
+    if (const char *e = getenv("GGML_MI355X_MMQ8_TR")) tr_rows = (atoi(e) == 64 && tt_tok == 64) ? 64 : 128;
+    const int n_rt = (a.N + tr_rows - 1) / tr_rows;
+    const int n_tt = (a.M + tt_tok - 1) / tt_tok;
+    // split-K over workgroups while the tile grid leaves CUs idle (>= 2 super-blocks per split)
+    const char *env = getenv("GGML_MI355X_MMQ8_KSPLIT");   // per call: tests switch it
+    const int64_t tiles = (int64_t)n_rt * n_tt * slices;
+    int ksplit = 1;
+    while (tiles * ksplit * 2 <= 256 && n_sb >= 4 * ksplit) ksplit *= 2;
+    if (env) ksplit = std::max(1, std::min(atoi(env), n_sb));
+    const int sb_per = (n_sb + ksplit - 1) / ksplit;
+    ksplit = (n_sb + sb_per - 1) / sb_per;
+    const size_t img_bytes = ((size_t)slices * n_tt * (tt_tok / Q8_TOK) * n_sb * ximg_bytes_rt(type) + 255) & ~(size_t)255;
+    const size_t part_bytes = ksplit > 1 ? (size_t)ksplit * slices * a.M * a.N * sizeof(float) : 0;
+    uint8_t *buf = static_cast<uint8_t *>(scratch.get(img_bytes + part_bytes, st));
     if (!buf) return hipErrorOutOfMemory;
-    int8_t *x8 = reinterpret_cast<int8_t *>(buf);
-    float *xd = reinterpret_cast<float *>(buf + x8_bytes);
-    _Float16 *xbs = reinterpret_cast<_Float16 *>(buf + x8_bytes + xd_bytes);
-    const int64_t items = (int64_t)Mpad * n_sb;
-    hipLaunchKernelGGL(mmq8_quant_x, dim3((unsigned)((items + 3) / 4), slices), dim3(256), 0, st, a, x8, xd, xbs, Mpad,
-                       n_sb);
-    // K-groups: split K inside the workgroup while the grid alone leaves CUs short of 2 workgroups
-    static const char *env = getenv("GGML_MI355X_MMQ8_KG");
-    const int64_t wgs = (int64_t)((a.N + Q8_TILE - 1) / Q8_TILE) * (Mpad / Q8_TILE) * slices;
-    int kg = (wgs < 1024 && n_sb >= 2) ? 2 : 1;
-    if (env) kg = atoi(env);
+    float *part = reinterpret_cast<float *>(buf + img_bytes);
     switch (type) {
-        case T_Q4_0: launch8_kg<T_Q4_0>(kg, a, x8, xd, xbs, Mpad, slices, st); break;
-        case T_Q8_0: launch8_kg<T_Q8_0>(kg, a, x8, xd, xbs, Mpad, slices, st); break;
-        case T_Q4_K: launch8_kg<T_Q4_K>(kg, a, x8, xd, xbs, Mpad, slices, st); break;
-        case T_Q5_K: launch8_kg<T_Q5_K>(kg, a, x8, xd, xbs, Mpad, slices, st); break;
+        case T_Q4_0: launch8<T_Q4_0>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, st); break;
+        case T_Q8_0: launch8<T_Q8_0>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, st); break;
+        case T_Q4_K: launch8<T_Q4_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, st); break;
+        case T_Q5_K: launch8<T_Q5_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, st); break;
+        case T_Q6_K: launch8<T_Q6_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

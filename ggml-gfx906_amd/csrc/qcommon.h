@@ -119,10 +119,11 @@ template <> __device__ __forceinline__ float xchg<1>(float v) { return dpp_f<DPP
 // Workgroup barrier for LDS hand-offs only: this wave's LDS operations complete, then s_barrier.
 // __syncthreads() is a release/acquire fence at workgroup scope, which also waits for every
 // outstanding global load (vmcnt(0)) — it would drain a weight stream issued ahead of the
-// barrier. No kernel here passes data between waves through global memory.
+// barrier. No kernel here passes data between waves through global memory. Both instructions
+// sit in ONE asm statement with a "memory" clobber: __builtin_amdgcn_s_barrier() alone is
+// modelled as touching no memory, so LDS accesses could legally be moved across it.
 __device__ __forceinline__ void lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // full 64-lane sum, result in every lane

@@ -15,6 +15,9 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libggml-hip-mi355x.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
+# diagnostics: A/B a variant build of the same library (scripts/*); unset in every product run
+if os.environ.get("GGML_MI355X_LIB"):
+    LIB_PATH = os.environ["GGML_MI355X_LIB"]
 HEADER = os.path.join(os.path.dirname(HERE), "include", "ggml-mi355x.h")
 
 F32, Q4_0, Q8_0, Q4_K, Q5_K, Q6_K, I32 = 0, 2, 8, 12, 13, 14, 26
@@ -35,6 +38,8 @@ class Mi355xError(RuntimeError):
 def build(force: bool = False) -> str:
     """Compile the HIP library in-tree (gfx950) if missing or stale."""
     srcs = [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc"))]
+    if os.environ.get("GGML_MI355X_LIB"):
+        return LIB_PATH
     stale = not os.path.exists(LIB_PATH) or any(os.path.getmtime(s) > os.path.getmtime(LIB_PATH) for s in srcs)
     if force or stale:
         subprocess.check_call(["make", "-s", "-C", HERE, "-j8", LIB_NAME])

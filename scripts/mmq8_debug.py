@@ -1,53 +1,43 @@
-"""int8 MFMA mat-mat debugging probe: one-hot activations make dst[t][r] = w[r][t] (dequantized),
-so index-mapping errors show up as permutations. Usage: python scripts/mmq8_debug.py"""
+"""Diagnostic: int8 mat-mat (GGML_MI355X_MMQ=i8) vs the oracle on small shapes, per type, with
+the error split by token / row so a layout fault shows its pattern."""
 import os
 import sys
 
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for p in (ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "ggml-gfx906_amd")):
+for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "ggml-gfx906_amd"), os.path.join(ROOT, "tests")):
     sys.path.insert(0, p)
 os.environ["GGML_MI355X_MMQ"] = "i8"
-import torch  # noqa: E402
+import torch  # noqa: E402,F401
 
 import golden_cases as G  # noqa: E402
-import qref  # noqa: E402
-from test_gpu_parity import run_mul_mat  # noqa: E402
 import mi355x_qmm as M  # noqa: E402
+import qref  # noqa: E402
+import test_gpu_parity as T  # noqa: E402
 
 M.build()
-np.set_printoptions(linewidth=200, precision=3, suppress=True)
-for t in (qref.Q8_0, qref.Q4_0, qref.Q4_K):
-    N, Mc, K = 64, 64, 256
-    w = qref.quantize(t, qref.fill_uniform(N * K, 5), n_per_row=K)
-    wd = qref.dequantize(t, w, N * K).reshape(N, K)
-    x = np.zeros((Mc, K), np.float32)
-    for i in range(Mc):
-        x[i, (3 * i) % K] = 1.0
-    a = G.Operand(t, w, [K, N, 1, 1], qref.contiguous_nb(t, [K, N, 1, 1]))
-    b = G.Operand(qref.F32, x.ravel(), [K, Mc, 1, 1], qref.contiguous_nb(qref.F32, [K, Mc, 1, 1]))
-    got = run_mul_mat(M, a, b, [N, Mc, 1, 1]).reshape(Mc, N)
-    want = (x @ wd.T)
-    print(qref.NAMES[t], "nmse", qref.nmse(got.ravel(), want.ravel()))
-    print("got[0:6,0:8]\n", got[0:6, 0:8], "\nwant\n", want[0:6, 0:8])
-    bad = np.abs(got - want) > 1e-3 * (np.abs(want) + 1e-3)
-    blk = np.array([((3 * i) % K) // 32 for i in range(Mc)])
-    print("bad count", bad.sum(), "of", bad.size)
-    for bb in range(8):
-        rows = bad[blk == bb]
-        print(f"  block {bb}: tokens {np.nonzero(blk == bb)[0][:3].tolist()}.. bad per row-octet",
-              [int(rows[:, 8 * o:8 * o + 8].sum()) for o in range(8)])
-    print("bad rows per token", bad.sum(axis=1).tolist())
-    if t in (qref.Q8_0, qref.Q4_0):
-        bs = 34 if t == qref.Q8_0 else 18
-        d = np.frombuffer(w.tobytes(), np.uint8).reshape(N, 8, bs)[:, :, :2].copy().view(np.float16)[:, :, 0].astype(np.float32)
-        for (ti, ri) in ((12, 0), (12, 5), (23, 2), (33, 40)):
-            b = ((3 * ti) % K) // 32
-            ratio = got[ti, ri] / want[ti, ri]
-            print(f"tok {ti} row {ri} blk {b}: ratio {ratio:.4f}; d ratios", (d[ri] / d[ri, b]).round(4).tolist())
-    # where does want[t][r] show up in got?
-    for (ti, ri) in ((0, 0), (1, 0), (0, 1), (5, 3), (33, 40)):
-        v = want[ti, ri]
-        hits = np.argwhere(np.abs(got - v) < 1e-3 * max(1e-6, abs(v)))
-        print(f"want[{ti},{ri}]={v:.4f} found at", hits[:6].tolist())
+shapes = [tuple(map(int, a.split('x'))) for a in os.environ.get('SHAPES', '64x64x256 128x64x512 256x128x1024 200x100x1536').split()]
+for t in [qref.TYPE_BY_NAME[n] for n in os.environ.get('TYPES', 'q8_0 q4_0 q4_K q5_K q6_K').split()] if hasattr(qref, 'TYPE_BY_NAME') else [{'q8_0': qref.Q8_0, 'q4_0': qref.Q4_0, 'q4_K': qref.Q4_K, 'q5_K': qref.Q5_K, 'q6_K': qref.Q6_K}[n] for n in os.environ.get('TYPES', 'q8_0 q4_0 q4_K q5_K q6_K').split()]:
+    for N, M_, K in shapes:
+        w = qref.quantize(t, qref.fill_uniform(N * K, 1), n_per_row=K)
+        x = qref.fill_uniform(M_ * K, 2)
+        a = G.Operand(t, w, [K, N, 1, 1], qref.contiguous_nb(t, [K, N, 1, 1]))
+        b = G.Operand(qref.F32, x, [K, M_, 1, 1], qref.contiguous_nb(qref.F32, [K, M_, 1, 1]))
+        got = T.run_mul_mat(M, a, b, [N, M_, 1, 1]).reshape(M_, N)
+        want = G.oracle_mul_mat(a, b, [N, M_, 1, 1]).reshape(M_, N)
+        err = qref.nmse(got, want)
+        print(f"{qref.NAMES[t]:5s} N={N} M={M_} K={K} nmse {err:.3e}", flush=True)
+        if err > float(os.environ.get('SHOW', '1e-3')):
+            tok_err = np.sqrt(((got - want) ** 2).mean(1) / (want ** 2).mean())
+            row_err = np.sqrt(((got - want) ** 2).mean(0) / (want ** 2).mean())
+            print("  got[0,:6] ", got[0, :6])
+            print("  want[0,:6]", want[0, :6])
+            print("  per-token rel err (first 16):", np.round(tok_err[:16], 3))
+            print("  per-row rel err (first 40):", np.round(row_err[:40], 3))
+            ratio = np.median(got / np.where(want == 0, 1, want))
+            print("  median got/want", ratio)
+            e = np.abs(got - want)
+            for f in np.argsort(e.ravel())[::-1][:12]:
+                tk, rw = divmod(int(f), N)
+                print(f"  worst tok {tk} row {rw}: got {got[tk, rw]:.4f} want {want[tk, rw]:.4f}")

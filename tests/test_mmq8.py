@@ -3,8 +3,9 @@
 The path is forced with GGML_MI355X_MMQ=i8 (read on every call). Its activations are quantized
 exactly like the CPU backend's Q8_K blocks (quantize_row_q8_K_ref, reference
 src/ggml-quants.c:2555-2591) and its block dot products are exact int32 sums, so:
-  * Q4_K / Q5_K: the oracle (ggml_vec_dot_q4_K_q8_K / _q5_K_ semantics on the same Q8_K blocks)
-    differs only by the fp32 order of the per-block scale accumulation: NMSE <= 1e-9;
+  * Q4_K / Q5_K / Q6_K: the oracle (ggml_vec_dot_q4_K_q8_K / _q5_K_ / _q6_K_ semantics on the
+    same Q8_K blocks) differs only by the fp32 order of the per-block scale accumulation:
+    NMSE <= 1e-9;
   * Q4_0 / Q8_0: the CPU quantizes activations per 32 (Q8_0 blocks), this path per 256:
     NMSE <= 5e-4 (the reference's MUL_MAT bar, test-backend-ops.cpp:3106-3108), and against the
     exact float64 product of the bit-exact dequantized weights within the activation rounding.
@@ -22,8 +23,8 @@ torch = pytest.importorskip("torch")
 
 pytestmark = pytest.mark.gpu
 
-TYPES = [qref.Q4_0, qref.Q8_0, qref.Q4_K, qref.Q5_K]
-TIGHT = {qref.Q4_K: 1e-9, qref.Q5_K: 1e-9, qref.Q4_0: 5e-4, qref.Q8_0: 5e-4}
+TYPES = [qref.Q4_0, qref.Q8_0, qref.Q4_K, qref.Q5_K, qref.Q6_K]
+TIGHT = {qref.Q4_K: 1e-9, qref.Q5_K: 1e-9, qref.Q6_K: 1e-9, qref.Q4_0: 5e-4, qref.Q8_0: 5e-4}
 
 
 @pytest.fixture(autouse=True)
@@ -42,9 +43,11 @@ def exact(t, w, N, K, x, M_):
     return (x.reshape(M_, K).astype(np.float64) @ wd.T).astype(np.float64).ravel()
 
 
-def case(mm, t, N, M_, K, seed=1, kg=None):
-    if kg is not None:
-        os.environ["GGML_MI355X_MMQ8_KG"] = str(kg)
+def case(mm, t, N, M_, K, seed=1, ksplit=None, tt=None):
+    if ksplit is not None:
+        os.environ["GGML_MI355X_MMQ8_KSPLIT"] = str(ksplit)
+    if tt is not None:
+        os.environ["GGML_MI355X_MMQ8_TT"] = str(tt)
     try:
         w = qref.quantize(t, qref.fill_uniform(N * K, seed), n_per_row=K)
         x = qref.fill_uniform(M_ * K, seed + 1)
@@ -52,7 +55,8 @@ def case(mm, t, N, M_, K, seed=1, kg=None):
         b = G.Operand(qref.F32, x, [K, M_, 1, 1], qref.contiguous_nb(qref.F32, [K, M_, 1, 1]))
         got = run_mul_mat(mm, a, b, [N, M_, 1, 1])
     finally:
-        os.environ.pop("GGML_MI355X_MMQ8_KG", None)
+        os.environ.pop("GGML_MI355X_MMQ8_KSPLIT", None)
+        os.environ.pop("GGML_MI355X_MMQ8_TT", None)
     assert np.all(np.isfinite(got))
     want = G.oracle_mul_mat(a, b, [N, M_, 1, 1])
     err = qref.nmse(got, want)
@@ -64,7 +68,8 @@ def case(mm, t, N, M_, K, seed=1, kg=None):
 
 
 @pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])
-@pytest.mark.parametrize("shape", [(64, 64, 256), (100, 37, 512), (256, 130, 1280), (33, 9, 768), (512, 200, 4096)],
+@pytest.mark.parametrize("shape", [(64, 64, 256), (100, 37, 512), (256, 130, 1280), (33, 9, 768), (512, 200, 4096),
+                                   (300, 129, 2048), (128, 512, 1024)],
                          ids=lambda s: "x".join(map(str, s)))
 def test_mmq8_shapes(mm, t, shape):
     N, M_, K = shape
@@ -72,13 +77,52 @@ def test_mmq8_shapes(mm, t, shape):
 
 
 @pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])
-@pytest.mark.parametrize("kg", [1, 2])
-def test_mmq8_kgroups(mm, t, kg):
-    """both K-group layouts, with an odd block count (one group idles on the last block)"""
-    case(mm, t, 192, 96, 256 * 5, seed=7, kg=kg)
+@pytest.mark.parametrize("ksplit", [1, 2, 3])
+def test_mmq8_ksplit(mm, t, ksplit):
+    """split-K over workgroups (fixed-order reduce), with a super-block count the splits do not
+    divide evenly"""
+    case(mm, t, 192, 96, 256 * 5, seed=7, ksplit=ksplit)
 
 
-@pytest.mark.parametrize("t", [qref.Q4_0, qref.Q4_K], ids=lambda t: qref.NAMES[t])
+@pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])
+@pytest.mark.parametrize("tt", [64, 128])
+def test_mmq8_token_tiles(mm, t, tt):
+    """both workgroup shapes (128 rows x 64 tokens with two K-groups, 128 x 128 with whole
+    super-blocks per wave), with ragged rows and tokens"""
+    case(mm, t, 200, 300, 768, seed=11, tt=tt)
+
+
+@pytest.mark.parametrize("t,big", [(qref.Q8_0, 7.0e4), (qref.Q4_K, 2.0e3), (qref.Q4_0, 1.0e5), (qref.Q6_K, 3.0e3),
+                                   (qref.Q5_K, 2.0e3)])
+@pytest.mark.parametrize("M_", [16, 200, 512])
+def test_mmq8_huge_scales(mm, t, big, M_):
+    """block scales far beyond what quantized weights hold (|w| in the thousands),
+    at token counts that run the full 128 x 64 tiles: the int8 path converts every scale to f32,
+    so there is no f16 range to overflow"""
+    K, N = 512, 160
+    f = qref.fill_uniform(N * K, 77).reshape(N, K)
+    f[5::7] *= big
+    w = qref.quantize(t, f.reshape(-1), n_per_row=K)
+    x = qref.fill_uniform(M_ * K, 78)
+    a = G.Operand(t, w, [K, N, 1, 1], qref.contiguous_nb(t, [K, N, 1, 1]))
+    b = G.Operand(qref.F32, x, [K, M_, 1, 1], qref.contiguous_nb(qref.F32, [K, M_, 1, 1]))
+    got = run_mul_mat(mm, a, b, [N, M_, 1, 1])
+    want = G.oracle_mul_mat(a, b, [N, M_, 1, 1])
+    assert np.all(np.isfinite(got))
+    assert qref.nmse(got, want) <= TIGHT[t]
+    keep = np.ones(N, bool)
+    keep[5::7] = False
+    assert qref.nmse(got.reshape(M_, N)[:, keep], want.reshape(M_, N)[:, keep]) <= TIGHT[t]
+
+
+@pytest.mark.parametrize("K", [256, 768])
+def test_mmq8_q6_k_odd_rows(mm, K):
+    """Q6_K rows of an odd number of super-blocks are 2-byte aligned every other row
+    (210-byte super-blocks): the staging realigns each lane's windows"""
+    case(mm, qref.Q6_K, 131, 70, K, seed=9)
+
+
+@pytest.mark.parametrize("t", [qref.Q4_0, qref.Q4_K, qref.Q6_K], ids=lambda t: qref.NAMES[t])
 def test_mmq8_broadcast_and_strided_rows(mm, t):
     """weights [K,N,2,1] broadcast over activations [K,M,4,3] with padded rows (nb11 > 4K)"""
     K, N, M_ = 512, 96, 40

@@ -1,8 +1,13 @@
-"""The mat-mat path's f16 range guard (csrc/mmq.hip, mmq_wave_kernel): weights are decoded to
-f16 inside the kernel, so rows whose block scales reach 1.0 (|w| in the hundreds or more, far
-outside what quantized LLM weights hold) take an exact fp32 recomputation instead of
-overflowing. Checked against the CPU oracle on rows mixing ordinary and huge scales, at token
-counts that select the register-decode tile (M <= 64)."""
+"""Huge block scales on the mat-mat path.
+  * f16 kernels (csrc/mmq.hip, forced with GGML_MI355X_MMQ=f16; still the path for K % 256 != 0,
+    misaligned rows and MUL_MAT_ID): weights are decoded to f16 inside the register-decode tile,
+    so rows whose block scales reach 1.0 (|w| in the hundreds or more, far outside what quantized
+    LLM weights hold) take an exact fp32 recomputation instead of overflowing (M <= 64);
+  * the default int8 tile (csrc/mmq8.hip) converts every scale to f32: exact at any M
+    (tests/test_mmq8.py also covers M = 200 and 512 for all five types).
+Checked against the CPU oracle on rows mixing ordinary and huge scales."""
+import os
+
 import numpy as np
 import pytest
 
@@ -23,9 +28,20 @@ def mm():
     return M
 
 
+@pytest.fixture(params=["f16", "i8"])
+def path(request):
+    old = os.environ.get("GGML_MI355X_MMQ")
+    os.environ["GGML_MI355X_MMQ"] = request.param
+    yield request.param
+    if old is None:
+        del os.environ["GGML_MI355X_MMQ"]
+    else:
+        os.environ["GGML_MI355X_MMQ"] = old
+
+
 @pytest.mark.parametrize("t,big", [(qref.Q8_0, 7.0e4), (qref.Q4_K, 2.0e3), (qref.Q4_0, 1.0e5)])
 @pytest.mark.parametrize("M", [16, 40])
-def test_huge_scales_match_oracle(mm, t, big, M):
+def test_huge_scales_match_oracle(mm, path, t, big, M):
     K, N = 512, 160
     f = qref.fill_uniform(N * K, 77).reshape(N, K)
     f[5::7] *= big                      # every 7th row: block scales >= 1.0

@@ -70,3 +70,32 @@ def test_two_streams_one_thread_do_not_share_scratch():
     torch.cuda.synchronize()
     assert qref.nmse(k1[2].cpu().numpy(), want1) <= 5e-4
     assert qref.nmse(k2[2].cpu().numpy(), want2) <= 5e-4
+
+
+def test_two_threads_default_stream_growth():
+    """two host threads on the default stream (handle 0), the second needing a larger
+    scratch. The per-scratch mutex in mul_mat keeps the first call's buffer alive until its
+    kernels are queued; the grower synchronizes the stream behind them before freeing it."""
+    import torch
+    small = _operands(torch, qref.Q8_0, 1024, 256, 64, seed=11)
+    big = _operands(torch, qref.Q4_K, 4096, 512, 1024, seed=13)
+    errors = []
+
+    def worker(ops, reps):
+        (A, B, D), keep, want = ops
+        try:
+            for _ in range(reps):
+                M.mul_mat(A, B, D, None)
+            torch.cuda.synchronize()
+            err = qref.nmse(keep[2].cpu().numpy(), want)
+            if not err <= 5e-4:
+                errors.append(err)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(small, 40)), threading.Thread(target=worker, args=(big, 6))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errors, errors
