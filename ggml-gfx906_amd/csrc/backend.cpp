@@ -676,6 +676,203 @@ int be_split_mul_mat(BackendCtx *c, struct ggml_tensor *node) {
     return rc;
 }
 
+// ------------------------------------------------------------------------------------------
+// graph fusion. The reference fuses runs of nodes whose intermediates nobody else reads
+// (ggml_can_fuse, src/ggml-impl.h:548-603; ggml_cuda_can_fuse, ggml-cuda.cu:2813-2870). The same
+// rule decides here, on the whole graph's use counts, and a fused run is executed by ONE launch
+// that writes only the run's last node:
+//   [NORM, MUL, ADD,] MUL_MAT(hot quant, <= 8 columns) [, ADD bias [, GELU | ADD residual]]
+//       -> the layer-norm-prologue / bias-GELU-residual-epilogue mat-vec (mmvq_fused.hip)
+//   [SCALE,] [DIAG_MASK_INF,] SOFT_MAX  -> one soft_max launch applying its producers on load
+// A plain MUL_MAT (nothing around it to fuse) keeps the generic dispatch. GGML_MI355X_FUSION=0
+// turns fusion off.
+// ------------------------------------------------------------------------------------------
+bool fusion_on() {
+    static const bool on = !(getenv("GGML_MI355X_FUSION") && atoi(getenv("GGML_MI355X_FUSION")) == 0);
+    return on;
+}
+
+// the graph's use count of t (ggml_node_has_n_uses, ggml-impl.h:550-557), -1 when t is unknown
+int use_count(const struct ggml_cgraph *g, const struct ggml_tensor *t) {
+    const struct ggml_hash_set &h = g->visited_hash_set;
+    if (!g->use_counts || !h.used || !h.keys || h.size == 0) return -1;
+    const size_t h0 = ((size_t)(uintptr_t)t >> 4) % h.size;
+    size_t i = h0;
+    while (h.used[i >> 5] & (1u << (i & 31))) {
+        if (h.keys[i] == t) return g->use_counts[i];
+        i = (i + 1) % h.size;
+        if (i == h0) break;
+    }
+    return -1;
+}
+
+// an intermediate the fused launch may skip: one use in the whole graph, not a view (others may
+// read it through the view source), not a requested output
+bool skippable(const struct ggml_cgraph *g, const struct ggml_tensor *t) {
+    return use_count(g, t) == 1 && t->view_src == nullptr && !(t->flags & GGMLABI_TENSOR_FLAG_OUTPUT);
+}
+
+bool same_shape_t(const struct ggml_tensor *a, const struct ggml_tensor *b) {
+    for (int i = 0; i < 4; ++i)
+        if (a->ne[i] != b->ne[i]) return false;
+    return true;
+}
+
+// f32 vector of n elements, contiguous (the ln gamma / beta and bias operands)
+bool f32_vec(const struct ggml_tensor *t, int64_t n) {
+    return t->type == GGMLABI_TYPE_F32 && t->ne[0] == n && t->ne[1] == 1 && t->ne[2] == 1 && t->ne[3] == 1 && t->nb[0] == 4;
+}
+
+// f32 2-D [ne0, ne1] with unit element stride
+bool f32_2d(const struct ggml_tensor *t) {
+    return t->type == GGMLABI_TYPE_F32 && t->nb[0] == 4 && t->ne[2] == 1 && t->ne[3] == 1;
+}
+
+bool disjoint(const struct ggml_tensor *a, const struct ggml_tensor *b) {
+    const uintptr_t a0 = (uintptr_t)a->data, a1 = a0 + ggml_base().nbytes(a);
+    const uintptr_t b0 = (uintptr_t)b->data, b1 = b0 + ggml_base().nbytes(b);
+    return a1 <= b0 || b1 <= a0;
+}
+
+// the same bytes with the same layout (an in-place result): element-wise kernels read and write
+// each element in the same thread, so this aliasing is safe
+bool identical(const struct ggml_tensor *a, const struct ggml_tensor *b) {
+    if (a->data != b->data || a->type != b->type) return false;
+    for (int i = 0; i < 4; ++i)
+        if (a->ne[i] != b->ne[i] || a->nb[i] != b->nb[i]) return false;
+    return true;
+}
+
+// nodes consumed by a fused mat-vec run at node i (0: no fusion); rc receives the launch status
+int fuse_matvec(BackendCtx *c, const struct ggml_cgraph *g, int i, int n, int &rc) {
+    auto at = [&](int k) -> struct ggml_tensor * { return i + k < n ? g->nodes[i + k] : nullptr; };
+    const struct ggml_tensor *x = nullptr, *ln_g = nullptr, *ln_b = nullptr;
+    float eps = 0.f;
+    int k = 0;
+    struct ggml_tensor *t0 = at(0);
+    if (t0->op == GGMLABI_OP_NORM) {
+        struct ggml_tensor *mul = at(1), *add = at(2);
+        if (!mul || !add || mul->op != GGMLABI_OP_MUL || add->op != GGMLABI_OP_ADD) return 0;
+        if (mul->src[0] != t0 || add->src[0] != mul) return 0;
+        if (!skippable(g, t0) || !skippable(g, mul) || !skippable(g, add)) return 0;
+        x = t0->src[0];
+        if (!f32_2d(x) || !f32_2d(t0) || !same_shape_t(x, t0) || !same_shape_t(mul, t0) || !same_shape_t(add, t0)) return 0;
+        if (!f32_vec(mul->src[1], x->ne[0]) || !f32_vec(add->src[1], x->ne[0])) return 0;
+        ln_g = mul->src[1];
+        ln_b = add->src[1];
+        std::memcpy(&eps, &t0->op_params[0], sizeof eps);
+        k = 3;
+    }
+    struct ggml_tensor *mm = at(k);
+    if (!mm || mm->op != GGMLABI_OP_MUL_MAT) return 0;
+    const struct ggml_tensor *w = mm->src[0];
+    if (x != nullptr) {
+        if (mm->src[1] != at(k - 1)) return 0;
+    } else {
+        x = mm->src[1];
+    }
+    if (!is_hot_quant(w->type) || (w->buffer && is_split_buft(w->buffer->buft))) return 0;
+    if (w->ne[2] != 1 || w->ne[3] != 1 || (int64_t)w->nb[0] != type_bytes(w->type)) return 0;
+    const int64_t K = w->ne[0], N = w->ne[1], M = mm->ne[1];
+    if (K != x->ne[0] || K % 64 != 0 || K > 8192 || K % type_blck(w->type) != 0) return 0;
+    if (!f32_2d(x) || x->ne[1] != M || M < 1 || M > 8 || !f32_2d(mm) || mm->ne[0] != N || N > (1LL << 31) - 1) return 0;
+    if ((uintptr_t)x->data % 16 != 0 || x->nb[1] % 16 != 0) return 0;
+    int last = k, epi = 0;
+    const struct ggml_tensor *bias = nullptr, *resid = nullptr;
+    struct ggml_tensor *b1 = at(k + 1);
+    if (b1 && b1->op == GGMLABI_OP_ADD && b1->src[0] == mm && f32_vec(b1->src[1], N) && same_shape_t(b1, mm) && skippable(g, mm)) {
+        bias = b1->src[1];
+        last = k + 1;
+        struct ggml_tensor *b2 = at(k + 2);
+        if (b2 && skippable(g, b1) && same_shape_t(b2, b1)) {
+            if (b2->op == GGMLABI_OP_UNARY && b2->op_params[0] == GGMLABI_UNARY_OP_GELU && b2->src[0] == b1) {
+                epi |= EPI_GELU;
+                last = k + 2;
+            } else if (b2->op == GGMLABI_OP_ADD && (b2->src[0] == b1) != (b2->src[1] == b1)) {
+                const struct ggml_tensor *r = b2->src[0] == b1 ? b2->src[1] : b2->src[0];
+                if (f32_2d(r) && same_shape_t(r, b1)) {
+                    resid = r;
+                    epi |= EPI_RESID;
+                    last = k + 2;
+                }
+            }
+        }
+    }
+    // every workgroup reads all of x while others already store rows of out, so out must not
+    // overlap x (ggml-alloc may have placed it there once x's last reader was done); the residual
+    // is read element by element where it is written, so it may be out itself. When the whole run
+    // fails that, retry without its last node.
+    const struct ggml_tensor *out = nullptr;
+    for (;; --last) {
+        if (last < k) return 0;   // not even the MUL_MAT's own result can take it
+        if (last < k + 2) { resid = nullptr; epi = 0; }
+        if (last < k + 1) bias = nullptr;
+        if (ln_g == nullptr && bias == nullptr) return 0;   // a lone MUL_MAT: generic dispatch
+        out = at(last);
+        if (!f32_2d(out) || !same_shape_t(out, mm)) return 0;
+        if (!disjoint(x, out)) continue;
+        if (resid && !disjoint(resid, out) && !(resid->data == out->data && resid->nb[1] == out->nb[1])) continue;
+        break;
+    }
+    MmArgs a{};
+    a.w = static_cast<const uint8_t *>(w->data);
+    a.nb01 = (int64_t)w->nb[1];
+    a.nb02 = a.nb03 = a.nb01 * N;
+    a.x = static_cast<const uint8_t *>(x->data);
+    a.nb11 = (int64_t)x->nb[1];
+    a.nb12 = a.nb13 = a.nb11 * M;
+    a.dst = static_cast<uint8_t *>(out->data);
+    a.nb1 = (int64_t)out->nb[1];
+    a.nb2 = a.nb3 = a.nb1 * M;
+    a.K = (int)K;
+    a.N = (int)N;
+    a.M = (int)M;
+    a.ne12 = a.ne13 = a.r2 = a.r3 = 1;
+    a.x_aligned16 = 1;
+    a.ln_g = ln_g ? static_cast<const float *>(ln_g->data) : nullptr;
+    a.ln_b = ln_b ? static_cast<const float *>(ln_b->data) : nullptr;
+    a.ln_eps = eps;
+    a.bias = bias ? static_cast<const float *>(bias->data) : nullptr;
+    a.epi = epi;
+    if (resid) {
+        a.resid = static_cast<const uint8_t *>(resid->data);
+        a.resid_nb1 = (int64_t)resid->nb[1];
+    }
+    a.fused = 1;
+    const hipError_t e = mmvq_fused_launch(w->type, a, mmvq_fused_pick_nc((int)M, (int)K), N >= 16384 ? 2 : 1, c->stream);
+    rc = e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
+    logf("fused %d nodes at %s (mat-vec %s, M=%d)\n", last + 1, t0->name, w->name, (int)M);
+    return last + 1;
+}
+
+// nodes consumed by a fused [SCALE,] [DIAG_MASK_INF,] SOFT_MAX run at node i (0: no fusion)
+int fuse_softmax(BackendCtx *c, const struct ggml_cgraph *g, int i, int n, int &rc) {
+    auto at = [&](int k) -> struct ggml_tensor * { return i + k < n ? g->nodes[i + k] : nullptr; };
+    SoftmaxPre pre{1.0f, 0.0f, -1};
+    int k = 0;
+    const struct ggml_tensor *in = at(0)->src[0];
+    if (at(0)->op == GGMLABI_OP_SCALE) {
+        std::memcpy(&pre.scale, &at(0)->op_params[0], sizeof(float));
+        std::memcpy(&pre.bias, &at(0)->op_params[1], sizeof(float));
+        k = 1;
+    }
+    if (at(k) && at(k)->op == GGMLABI_OP_DIAG_MASK_INF && (k == 0 || at(k)->src[0] == at(k - 1))) {
+        pre.n_past = at(k)->op_params[0];
+        ++k;
+    }
+    struct ggml_tensor *sm = at(k);
+    if (k == 0 || !sm || sm->op != GGMLABI_OP_SOFT_MAX || sm->src[0] != at(k - 1)) return 0;
+    for (int j = 0; j < k; ++j)
+        if (!skippable(g, at(j)) || !same_shape_t(at(j), sm) || at(j)->type != GGMLABI_TYPE_F32) return 0;
+    if (!disjoint(in, sm) && !identical(in, sm)) return 0;
+    GraphOp gop;
+    if (!graph_op_of(sm, gop)) return 0;
+    gop.src[0] = tv(in);
+    rc = run_soft_max_pre(gop, pre, c->stream);
+    logf("fused %d nodes at %s (soft_max)\n", k + 1, at(0)->name);
+    return k + 1;
+}
+
 enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
     BackendCtx *c = be_ctx(b);
     const GgmlBase &gb = ggml_base();
@@ -685,9 +882,16 @@ enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
     for (int i = 0; i < n; ++i) {
         struct ggml_tensor *node = gb.graph_node(g, i);
         if (is_empty(node) || is_view_op(node->op)) continue;
-        int rc;
+        int rc = GGML_MI355X_OK;
         GraphOp gop;
-        if (node->op == GGMLABI_OP_MUL_MAT && node->src[0]->buffer && is_split_buft(node->src[0]->buffer->buft)) {
+        int fused = 0;
+        if (fusion_on()) {
+            if (node->op == GGMLABI_OP_NORM || node->op == GGMLABI_OP_MUL_MAT) fused = fuse_matvec(c, g, i, n, rc);
+            else if (node->op == GGMLABI_OP_SCALE || node->op == GGMLABI_OP_DIAG_MASK_INF) fused = fuse_softmax(c, g, i, n, rc);
+        }
+        if (fused > 0) {
+            i += fused - 1;
+        } else if (node->op == GGMLABI_OP_MUL_MAT && node->src[0]->buffer && is_split_buft(node->src[0]->buffer->buft)) {
             rc = be_split_mul_mat(c, node);
         } else if (node->op == GGMLABI_OP_MUL_MAT && is_hot_quant(node->src[0]->type)) {
             rc = mul_mat(tv(node->src[0]), tv(node->src[1]), tv(node), c->stream, c->scratch);
@@ -762,6 +966,9 @@ ggml_backend_t dv_init_backend(ggml_backend_dev_t d, const char *) {
     c->name = dc->name;
     HIP_OK(hipSetDevice(c->device));
     HIP_OK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    // raise the fused mat-vec LDS limits now: that is not a stream operation, so it must not
+    // first happen inside a hipGraph capture of be_graph_compute
+    for (int t : {2, 8, 12, 13, 14}) HIP_OK(mmvq_fused_prepare(t));   // Q4_0 Q8_0 Q4_K Q5_K Q6_K
     auto *b = new ggml_backend();
     b->guid = &BACKEND_GUID;
     b->iface = BACKEND_IFACE;

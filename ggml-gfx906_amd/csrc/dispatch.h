@@ -72,5 +72,18 @@ struct GraphOp {
 };
 int check_graph_op(const GraphOp &g);
 int run_graph_op(const GraphOp &g, hipStream_t st);
+// fused producers of a SOFT_MAX (backend graph fusion of SCALE -> DIAG_MASK_INF -> SOFT_MAX)
+struct SoftmaxPre {
+    float scale, bias;   // SCALE's op_params
+    int n_past;          // DIAG_MASK_INF's n_past (-1: no mask node)
+};
+int run_graph_op_pre(const GraphOp &g, const SoftmaxPre *pre, hipStream_t st);
+int run_soft_max_pre(const GraphOp &g, const SoftmaxPre &pre, hipStream_t st);
+
+// quantized mat-vec with the decode-layer fusions (mmvq_fused.hip): layer-norm prologue,
+// bias / GELU / residual epilogue (MmArgs fields); nc columns per launch column group
+hipError_t mmvq_fused_launch(int type, const MmArgs &a, int nc, int rpw, hipStream_t st);
+hipError_t mmvq_fused_prepare(int type);
+int mmvq_fused_pick_nc(int M, int K);
 
 }  // namespace mi355x

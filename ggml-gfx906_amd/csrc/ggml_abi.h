@@ -7,6 +7,7 @@
 //   ggml_backend_dev_props / caps .... include/ggml-backend.h:140-159
 //   buffer type / buffer / backend /
 //   event / device / reg vtables ..... src/ggml-backend-impl.h:17-207
+//   struct ggml_hash_set / ggml_cgraph  src/ggml-impl.h:181-212, 311-325 (read for use counts)
 // tests/test_abi_layout.py compiles oracle/abi_check.cpp against the reference headers and
 // this file side by side and asserts every offset, size and enum value used here agrees.
 #pragma once
@@ -77,6 +78,32 @@ struct ggml_tensor {
     char name[GGMLABI_MAX_NAME];
     void *extra;
     char padding[8];
+};
+
+// include/ggml.h enum ggml_tensor_flag
+enum { GGMLABI_TENSOR_FLAG_OUTPUT = 2 };
+
+// the graph internals the fusion rules read (src/ggml-impl.h:181-212, 311-325): a graph's use
+// counts are indexed by the slot of the tensor in visited_hash_set (linear probing from
+// ((uintptr_t)t >> 4) % size, occupancy in the `used` bitset of 32-bit words). The scheduler's
+// split graphs are views (ggml_graph_view, src/ggml.c:6545-6560) that share the whole graph's
+// counts, so a use in another split is still counted.
+struct ggml_hash_set {
+    size_t size;
+    uint32_t *used;
+    struct ggml_tensor **keys;
+};
+struct ggml_cgraph {
+    int size;
+    int n_nodes;
+    int n_leafs;
+    struct ggml_tensor **nodes;
+    struct ggml_tensor **grads;
+    struct ggml_tensor **grad_accs;
+    struct ggml_tensor **leafs;
+    int32_t *use_counts;
+    struct ggml_hash_set visited_hash_set;
+    int32_t order;
 };
 
 typedef struct ggml_backend_buffer_type *ggml_backend_buffer_type_t;

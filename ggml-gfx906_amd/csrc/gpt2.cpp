@@ -32,6 +32,7 @@
 namespace mi355x {
 hipError_t mmvq_fused_launch(int type, const MmArgs &a, int nc, int rpw, hipStream_t st);
 hipError_t mmvq_fused_prepare(int type);
+int mmvq_fused_pick_nc(int M, int K);
 unsigned long long *stamps_buffer();
 hipError_t gpt2_embed_launch(int wtype, const void *wte, int64_t wte_nb1, const float *wpe, const int32_t *tokens,
                              const int32_t *pos, float *x, int n_seq, int n_embd, int n_vocab, int n_ctx, hipStream_t st);
@@ -141,12 +142,7 @@ int hip_status_at(hipError_t e, const char *where) {
 }
 #define hip_status(e) hip_status_at((e), #e)
 
-// widest column group with a kernel that divides n_seq (groups of 4 / 8 serve K <= 4096)
-int pick_nc(int n, int K) {
-    for (int nc : {8, 4, 3, 2, 1})
-        if (n % nc == 0 && (nc < 4 || K <= 4096)) return nc;
-    return 1;
-}
+int pick_nc(int n, int K) { return mmvq_fused_pick_nc(n, K); }
 
 // y[n_seq][N] (+)= W[N][K] . x[n_seq][K] with the fused prologue / epilogue
 int fused_matvec(const ggml_mi355x_gpt2_ctx *c, const Tensor &w, const float *x, float *y, const Tensor *ln_g, const Tensor *ln_b,

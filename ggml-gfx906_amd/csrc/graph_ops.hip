@@ -204,6 +204,12 @@ struct SoftMaxP {
     uint32_t n_head_log2;
     int mask_type;  // -1 none, 0 f32, 1 f16
     bool sinks;
+    // fused SCALE -> DIAG_MASK_INF producers (backend graph fusion): x <- x * pre_s (+ pre_b),
+    // then -inf where i0 > n_past + i1 (pre_n_past >= 0), exactly as scale_kernel /
+    // diag_mask_kernel write their outputs
+    bool pre;
+    float pre_s, pre_b;
+    int pre_n_past;
 };
 
 __global__ __launch_bounds__(256) void soft_max_kernel(const DevT d, const DevT a, const DevT m, const DevT sk, int64_t rows,
@@ -222,7 +228,12 @@ __global__ __launch_bounds__(256) void soft_max_kernel(const DevT d, const DevT 
                                                                   : powf(p.m1, (float)(2 * (h - p.n_head_log2) + 1)))
                                              : 1.f;
         auto w_at = [&](int64_t i) {
-            float w = *reinterpret_cast<const float *>(pa + i * a.nb[0]) * p.scale;
+            float x = *reinterpret_cast<const float *>(pa + i * a.nb[0]);
+            if (p.pre) {
+                x = p.pre_b == 0.f ? x * p.pre_s : fmaf(x, p.pre_s, p.pre_b);
+                if (p.pre_n_past >= 0 && i > p.pre_n_past + i1) x = -INFINITY;
+            }
+            float w = x * p.scale;
             if (pm) {
                 const float mv = p.mask_type == 0 ? *reinterpret_cast<const float *>(pm + i * m.nb[0])
                                                   : h2f_dev(*reinterpret_cast<const uint16_t *>(pm + i * m.nb[0]));
@@ -396,7 +407,16 @@ int check_graph_op(const GraphOp &g) {
     }
 }
 
-int run_graph_op(const GraphOp &g, hipStream_t st) {
+int run_graph_op(const GraphOp &g, hipStream_t st) { return run_graph_op_pre(g, nullptr, st); }
+
+// SCALE -> DIAG_MASK_INF -> SOFT_MAX as one launch (backend fusion): g is the SOFT_MAX node with
+// src[0] replaced by the SCALE node's input
+int run_soft_max_pre(const GraphOp &g, const SoftmaxPre &pre, hipStream_t st) {
+    if (g.op != GOP_SOFT_MAX) return GGML_MI355X_EINVAL;
+    return run_graph_op_pre(g, &pre, st);
+}
+
+int run_graph_op_pre(const GraphOp &g, const SoftmaxPre *pre, hipStream_t st) {
     const int rc = check_graph_op(g);
     if (rc != GGML_MI355X_OK) return rc;
     const TensorView &dv = g.dst, &av = g.src[0];
@@ -429,6 +449,12 @@ int run_graph_op(const GraphOp &g, hipStream_t st) {
             break;
         case GOP_SOFT_MAX: {
             SoftMaxP p{};
+            if (pre) {
+                p.pre = true;
+                p.pre_s = pre->scale;
+                p.pre_b = pre->bias;
+                p.pre_n_past = pre->n_past;
+            }
             p.scale = fparam(g, 0);
             p.max_bias = fparam(g, 1);
             const uint32_t n_head = (uint32_t)av.ne[2];

@@ -135,6 +135,13 @@ hipError_t mmvq_fused_prepare(int type) {
     }
 }
 
+// widest column group with a kernel that divides M (groups of 4 / 8 serve K <= 4096)
+int mmvq_fused_pick_nc(int M, int K) {
+    for (int nc : {8, 4, 3, 2, 1})
+        if (M % nc == 0 && (nc < 4 || K <= 4096)) return nc;
+    return 1;
+}
+
 // a.M columns in groups of nc (a.M % nc == 0); a.ne12 == a.ne13 == 1
 hipError_t mmvq_fused_launch(int type, const MmArgs &a, int nc, int rpw, hipStream_t st) {
     if (a.K % 64 != 0 || a.K > 8192 || !a.x_aligned16 || a.ne12 != 1 || a.ne13 != 1 || nc <= 0 || a.M % nc != 0)

@@ -634,7 +634,8 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
         const float *bp = a.bias != nullptr ? a.bias + row : reinterpret_cast<const float *>(dcol0 + (int64_t)em * a.nb1) + row;
         EpiOps e;
         e.bias = *bp;
-        e.resid = reinterpret_cast<const float *>(dcol0 + (int64_t)em * a.nb1)[row];
+        e.resid = a.resid != nullptr ? reinterpret_cast<const float *>(a.resid + (int64_t)(blockIdx.z * NC + em) * a.resid_nb1)[row]
+                                     : reinterpret_cast<const float *>(dcol0 + (int64_t)em * a.nb1)[row];
         return e;
     };
 

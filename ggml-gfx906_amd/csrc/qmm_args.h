@@ -47,6 +47,10 @@ struct MmArgs {
     float ln_eps;
     const float *bias;
     int epi;
+    //   EPI_RESID reads the residual from `resid` (column stride resid_nb1 bytes) when set,
+    //     else from dst itself (dst += v)
+    const uint8_t *resid;
+    int64_t resid_nb1;
     //   epi & EPI_ARGMAX: every workgroup also writes the (max, lowest row) of the rows it
     //     produced, per column c, to amax_v / amax_i [c * ARGMAX_SLOTS + blockIdx.x]
     float *amax_v;

@@ -2,7 +2,7 @@
 //
 // Compiled twice by tests/test_abi_layout.py:
 //   -DSIDE_REF  against the reference's own headers (include/ggml.h, include/ggml-backend.h,
-//               src/ggml-backend-impl.h)
+//               src/ggml-backend-impl.h, src/ggml-impl.h)
 //   -DSIDE_OURS against ggml-gfx906_amd/csrc/ggml_abi.h, the plugin's restatement
 // Both print "name value" lines for every struct size, field offset and enum value the plugin
 // relies on; the test requires the two listings to be identical, so the plugin's view of the
@@ -14,8 +14,12 @@
 #include "ggml.h"
 #include "ggml-backend.h"
 #include "ggml-backend-impl.h"
+#include "ggml-impl.h"
 #define E(ours, ref) std::printf("enum %s %d\n", #ours, (int)(ref));
 #define API_VERSION GGML_BACKEND_API_VERSION
+#include <cstdlib>
+// ggml-impl.h's static inline hash helpers reference ggml_abort; this listing never calls them
+extern "C" void ggml_abort(const char *, int, const char *, ...) { std::abort(); }
 #elif defined(SIDE_OURS)
 #include "ggml_abi.h"
 #define E(ours, ref) std::printf("enum %s %d\n", #ours, (int)(ours));
@@ -51,6 +55,7 @@ int main() {
     E(GGMLABI_OP_PERMUTE, GGML_OP_PERMUTE)
     E(GGMLABI_OP_TRANSPOSE, GGML_OP_TRANSPOSE)
     E(GGMLABI_OP_GET_ROWS, GGML_OP_GET_ROWS)
+    E(GGMLABI_TENSOR_FLAG_OUTPUT, GGML_TENSOR_FLAG_OUTPUT)
     E(GGMLABI_TYPE_F32, GGML_TYPE_F32)
     E(GGMLABI_TYPE_F16, GGML_TYPE_F16)
     E(GGMLABI_TYPE_I32, GGML_TYPE_I32)
@@ -67,6 +72,13 @@ int main() {
     F(ggml_tensor, type) F(ggml_tensor, buffer) F(ggml_tensor, ne) F(ggml_tensor, nb) F(ggml_tensor, op)
     F(ggml_tensor, op_params) F(ggml_tensor, flags) F(ggml_tensor, src) F(ggml_tensor, view_src)
     F(ggml_tensor, view_offs) F(ggml_tensor, data) F(ggml_tensor, name) F(ggml_tensor, extra)
+
+    S(ggml_hash_set)
+    F(ggml_hash_set, size) F(ggml_hash_set, used) F(ggml_hash_set, keys)
+    S(ggml_cgraph)
+    F(ggml_cgraph, size) F(ggml_cgraph, n_nodes) F(ggml_cgraph, n_leafs) F(ggml_cgraph, nodes) F(ggml_cgraph, grads)
+    F(ggml_cgraph, grad_accs) F(ggml_cgraph, leafs) F(ggml_cgraph, use_counts) F(ggml_cgraph, visited_hash_set)
+    F(ggml_cgraph, order)
 
     S(ggml_backend_dev_caps)
     F(ggml_backend_dev_caps, async) F(ggml_backend_dev_caps, host_buffer)

@@ -1,0 +1,250 @@
+// oracle/fusion_check.cpp — TEST INFRASTRUCTURE ONLY (never part of the product path).
+//
+// Drives the plugin's graph fusion (backend.cpp fuse_matvec / fuse_softmax) through the
+// REFERENCE ggml API: every case builds one ggml graph with the chains GPT-2 emits
+// (examples/gpt-2/main-sched.cpp:603-637, 690-706, 744-757, 765-822, 826-847), allocates it
+// with ggml-alloc (so in-place reuse and aliasing happen as in a real run), computes it on the
+// plugin's backend and on ggml-cpu, and compares every tensor the case reads back:
+//   * the run's result, NMSE <= 5e-4 (test-backend-ops' MUL_MAT bar, tests/test-backend-ops.cpp:3106);
+//   * in the negative cases, the intermediates that must NOT be skipped (an OUTPUT flag, a second
+//     consumer) read back equal to ggml-cpu too.
+// tests/test_graph_fusion.py runs it with fusion on (GGML_MI355X_DEBUG lists the fused runs) and
+// with GGML_MI355X_FUSION=0, and asserts which cases fused.
+//
+// usage: fusion_check PLUGIN   (exit 0 = every case within the bar)
+#include "ggml-alloc.h"
+#include "ggml-backend.h"
+#include "ggml-cpu.h"
+#include "ggml.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <random>
+#include <string>
+#include <vector>
+
+namespace {
+
+struct Inputs {
+    std::map<std::string, std::vector<uint8_t>> bytes;   // by tensor name
+};
+
+// builds the case's graph in ctx; returns the tensors to read back (first = the result)
+using Builder = std::function<std::vector<ggml_tensor *>(ggml_context *, ggml_cgraph *)>;
+
+std::vector<std::vector<float>> run(ggml_backend_t be, const Builder &build, const Inputs &in) {
+    ggml_init_params p = {ggml_tensor_overhead() * 256 + ggml_graph_overhead(), nullptr, true};
+    ggml_context *ctx = ggml_init(p);
+    ggml_cgraph *gf = ggml_new_graph(ctx);
+    std::vector<ggml_tensor *> outs = build(ctx, gf);
+    for (ggml_tensor *t : outs) ggml_build_forward_expand(gf, t);
+    ggml_gallocr_t ga = ggml_gallocr_new(ggml_backend_get_default_buffer_type(be));
+    if (!ggml_gallocr_alloc_graph(ga, gf)) { fprintf(stderr, "graph allocation failed\n"); exit(2); }
+    for (const auto &kv : in.bytes) {
+        ggml_tensor *t = ggml_get_tensor(ctx, kv.first.c_str());
+        if (!t) continue;   // an input this case does not use
+        if (ggml_nbytes(t) != kv.second.size()) { fprintf(stderr, "size mismatch %s\n", kv.first.c_str()); exit(2); }
+        ggml_backend_tensor_set(t, kv.second.data(), 0, kv.second.size());
+    }
+    if (ggml_backend_graph_compute(be, gf) != GGML_STATUS_SUCCESS) { fprintf(stderr, "graph_compute failed\n"); exit(2); }
+    std::vector<std::vector<float>> res;
+    for (ggml_tensor *t : outs) {
+        std::vector<float> v(ggml_nelements(t));
+        ggml_backend_tensor_get(t, v.data(), 0, v.size() * sizeof(float));
+        res.push_back(std::move(v));
+    }
+    ggml_gallocr_free(ga);
+    ggml_free(ctx);
+    return res;
+}
+
+ggml_tensor *input(ggml_context *ctx, const char *name, ggml_type t, int64_t n0, int64_t n1 = 1, int64_t n2 = 1) {
+    ggml_tensor *x = ggml_new_tensor_3d(ctx, t, n0, n1, n2);
+    ggml_set_name(x, name);
+    ggml_set_input(x);
+    return x;
+}
+
+// the layer input stays allocated after the norm read it, as GPT-2's residual stream does (its
+// residual add reads it later). Without that, ggml-alloc may place the chain's result over the
+// freed input, and the plugin then declines the fusion (every workgroup of the fused launch reads
+// the whole input while others already store results) — the "freed_input" case covers that.
+ggml_tensor *resident(ggml_tensor *x) {
+    ggml_set_output(x);
+    return x;
+}
+
+std::mt19937 rng(4321);
+
+std::vector<uint8_t> f32_bytes(size_t n, float lo, float hi) {
+    std::uniform_real_distribution<float> u(lo, hi);
+    std::vector<uint8_t> b(n * 4);
+    for (size_t i = 0; i < n; ++i) {
+        const float v = u(rng);
+        memcpy(&b[i * 4], &v, 4);
+    }
+    return b;
+}
+
+std::vector<uint8_t> q_bytes(ggml_type t, int64_t K, int64_t N) {
+    std::uniform_real_distribution<float> u(-1.f, 1.f);
+    std::vector<float> w((size_t)K * N);
+    for (auto &v : w) v = u(rng);
+    std::vector<uint8_t> q(ggml_row_size(t, K) * N);
+    ggml_quantize_chunk(t, w.data(), q.data(), 0, N, K, nullptr);
+    return q;
+}
+
+double nmse(const std::vector<float> &got, const std::vector<float> &want, bool *finite) {
+    double num = 0, den = 0;
+    for (size_t i = 0; i < got.size(); ++i) {
+        if (!std::isfinite(got[i]) && !(std::isinf(got[i]) && got[i] == want[i])) *finite = false;
+        if (std::isfinite(want[i])) {
+            num += (got[i] - want[i]) * (double)(got[i] - want[i]);
+            den += want[i] * (double)want[i];
+        }
+    }
+    return num / (den > 0 ? den : 1);
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    if (argc < 2) { fprintf(stderr, "usage: fusion_check PLUGIN\n"); return 2; }
+    ggml_backend_reg_t reg = ggml_backend_load(argv[1]);
+    if (!reg || ggml_backend_reg_dev_count(reg) == 0) { fprintf(stderr, "plugin has no devices\n"); return 2; }
+    ggml_backend_t gpu = ggml_backend_dev_init(ggml_backend_reg_dev_get(reg, 0), nullptr);
+    ggml_backend_t cpu = ggml_backend_cpu_init();
+    const float eps = 1e-5f;
+    int fails = 0;
+
+    auto check = [&](const std::string &name, const Builder &b, const Inputs &in) {
+        fprintf(stderr, "CASE %s\n", name.c_str());   // the plugin's debug log follows on stderr
+        const auto got = run(gpu, b, in);
+        const auto want = run(cpu, b, in);
+        bool ok = true;
+        std::string detail;
+        for (size_t j = 0; j < got.size(); ++j) {
+            bool finite = true;
+            const double e = nmse(got[j], want[j], &finite);
+            ok = ok && finite && e <= 5e-4;
+            char buf[64];
+            snprintf(buf, sizeof buf, " out%zu=%.3e%s", j, e, finite ? "" : "(nonfinite)");
+            detail += buf;
+        }
+        fails += !ok;
+        printf("%s %s%s\n", ok ? "OK  " : "FAIL", name.c_str(), detail.c_str());
+        fflush(stdout);
+    };
+
+    const ggml_type types[] = {GGML_TYPE_Q4_0, GGML_TYPE_Q8_0, GGML_TYPE_Q4_K, GGML_TYPE_Q5_K, GGML_TYPE_Q6_K};
+    for (ggml_type t : types) {
+        for (int M : {1, 3, 8}) {
+            const int E = 768, F = 4 * E;
+            Inputs in;
+            in.bytes["x"] = f32_bytes((size_t)E * M, -2.f, 2.f);
+            in.bytes["g"] = f32_bytes(E, 0.5f, 1.5f);
+            in.bytes["b"] = f32_bytes(E, -0.2f, 0.2f);
+            in.bytes["w_qkv"] = q_bytes(t, E, 3 * E);
+            in.bytes["b_qkv"] = f32_bytes(3 * E, -0.5f, 0.5f);
+            in.bytes["w_fc"] = q_bytes(t, E, F);
+            in.bytes["b_fc"] = f32_bytes(F, -0.5f, 0.5f);
+            in.bytes["w_mp"] = q_bytes(t, F, E);
+            in.bytes["b_mp"] = f32_bytes(E, -0.5f, 0.5f);
+            const std::string tag = std::string(ggml_type_name(t)) + " M=" + std::to_string(M);
+
+            // layer-norm -> c_attn + bias (main-sched.cpp:603-637)
+            check("ln_matvec_bias " + tag, [&](ggml_context *c, ggml_cgraph *) {
+                ggml_tensor *x = resident(input(c, "x", GGML_TYPE_F32, E, M));
+                ggml_tensor *h = ggml_add(c, ggml_mul(c, ggml_norm(c, x, eps), input(c, "g", GGML_TYPE_F32, E)), input(c, "b", GGML_TYPE_F32, E));
+                ggml_tensor *y = ggml_add(c, ggml_mul_mat(c, input(c, "w_qkv", t, E, 3 * E), h), input(c, "b_qkv", GGML_TYPE_F32, 3 * E));
+                return std::vector<ggml_tensor *>{y};
+            }, in);
+
+            // layer-norm -> fc + bias -> gelu -> proj + bias -> + residual (main-sched.cpp:765-822)
+            check("mlp " + tag, [&](ggml_context *c, ggml_cgraph *) {
+                ggml_tensor *x = resident(input(c, "x", GGML_TYPE_F32, E, M));
+                ggml_tensor *h = ggml_add(c, ggml_mul(c, ggml_norm(c, x, eps), input(c, "g", GGML_TYPE_F32, E)), input(c, "b", GGML_TYPE_F32, E));
+                h = ggml_gelu(c, ggml_add(c, ggml_mul_mat(c, input(c, "w_fc", t, E, F), h), input(c, "b_fc", GGML_TYPE_F32, F)));
+                ggml_tensor *y = ggml_add(c, ggml_add(c, ggml_mul_mat(c, input(c, "w_mp", t, F, E), h), input(c, "b_mp", GGML_TYPE_F32, E)), x);
+                return std::vector<ggml_tensor *>{y};
+            }, in);
+
+            // final layer-norm -> lm_head without bias (main-sched.cpp:826-847)
+            check("ln_matvec " + tag, [&](ggml_context *c, ggml_cgraph *) {
+                ggml_tensor *x = resident(input(c, "x", GGML_TYPE_F32, E, M));
+                ggml_tensor *h = ggml_add(c, ggml_mul(c, ggml_norm(c, x, eps), input(c, "g", GGML_TYPE_F32, E)), input(c, "b", GGML_TYPE_F32, E));
+                return std::vector<ggml_tensor *>{ggml_mul_mat(c, input(c, "w_fc", t, E, F), h)};
+            }, in);
+        }
+    }
+
+    // negative cases (Q4_0, M = 2): the skipped intermediates are needed elsewhere
+    {
+        const int E = 768, M = 2;
+        Inputs in;
+        in.bytes["x"] = f32_bytes((size_t)E * M, -2.f, 2.f);
+        in.bytes["g"] = f32_bytes(E, 0.5f, 1.5f);
+        in.bytes["b"] = f32_bytes(E, -0.2f, 0.2f);
+        in.bytes["w"] = q_bytes(GGML_TYPE_Q4_0, E, E);
+        in.bytes["bias"] = f32_bytes(E, -0.5f, 0.5f);
+        // the norm is a requested output: the chain must not fuse, and the norm reads back
+        check("neg_output_flag", [&](ggml_context *c, ggml_cgraph *) {
+            ggml_tensor *x = input(c, "x", GGML_TYPE_F32, E, M);
+            ggml_tensor *nrm = ggml_norm(c, x, eps);
+            ggml_set_output(nrm);
+            ggml_tensor *h = ggml_add(c, ggml_mul(c, nrm, input(c, "g", GGML_TYPE_F32, E)), input(c, "b", GGML_TYPE_F32, E));
+            ggml_tensor *y = ggml_add(c, ggml_mul_mat(c, input(c, "w", GGML_TYPE_Q4_0, E, E), h), input(c, "bias", GGML_TYPE_F32, E));
+            return std::vector<ggml_tensor *>{y, nrm};
+        }, in);
+        // the mat-vec result has a second consumer: the bias add may not swallow it
+        check("neg_second_use", [&](ggml_context *c, ggml_cgraph *) {
+            ggml_tensor *x = input(c, "x", GGML_TYPE_F32, E, M);
+            ggml_tensor *mm = ggml_mul_mat(c, input(c, "w", GGML_TYPE_Q4_0, E, E), x);
+            ggml_tensor *y = ggml_add(c, mm, input(c, "bias", GGML_TYPE_F32, E));
+            ggml_tensor *z = ggml_scale(c, mm, 0.5f);
+            return std::vector<ggml_tensor *>{y, z};
+        }, in);
+        // the chain's input is freed after the norm: correct whether or not the plugin fuses
+        check("freed_input", [&](ggml_context *c, ggml_cgraph *) {
+            ggml_tensor *x = input(c, "x", GGML_TYPE_F32, E, M);
+            ggml_tensor *h = ggml_add(c, ggml_mul(c, ggml_norm(c, x, eps), input(c, "g", GGML_TYPE_F32, E)), input(c, "b", GGML_TYPE_F32, E));
+            ggml_tensor *y = ggml_add(c, ggml_mul_mat(c, input(c, "w", GGML_TYPE_Q4_0, E, E), h), input(c, "bias", GGML_TYPE_F32, E));
+            return std::vector<ggml_tensor *>{y};
+        }, in);
+        // mat-vec + bias + residual with the residual as the FIRST operand of the add
+        check("resid_first_operand", [&](ggml_context *c, ggml_cgraph *) {
+            ggml_tensor *x = input(c, "x", GGML_TYPE_F32, E, M);
+            ggml_tensor *mm = ggml_add(c, ggml_mul_mat(c, input(c, "w", GGML_TYPE_Q4_0, E, E), x), input(c, "bias", GGML_TYPE_F32, E));
+            return std::vector<ggml_tensor *>{ggml_add(c, x, mm)};
+        }, in);
+    }
+
+    // attention weights: KQ -> scale -> causal mask -> soft_max (main-sched.cpp:690-706)
+    for (int n_past : {0, 5, 63}) {
+        for (int N : {1, 4}) {
+            const int H = 12, n_kv = n_past + N;
+            Inputs in;
+            in.bytes["kq"] = f32_bytes((size_t)n_kv * N * H, -8.f, 8.f);
+            const std::string tag = "n_past=" + std::to_string(n_past) + " N=" + std::to_string(N);
+            check("softmax_chain " + tag, [&](ggml_context *c, ggml_cgraph *) {
+                ggml_tensor *kq = input(c, "kq", GGML_TYPE_F32, n_kv, N, H);
+                ggml_tensor *kq2 = ggml_scale(c, ggml_add(c, kq, kq), 0.125f);   // a producer node, as KQ is
+                return std::vector<ggml_tensor *>{ggml_soft_max(c, ggml_diag_mask_inf(c, kq2, n_past))};
+            }, in);
+            check("softmax_mask_only " + tag, [&](ggml_context *c, ggml_cgraph *) {
+                ggml_tensor *kq = input(c, "kq", GGML_TYPE_F32, n_kv, N, H);
+                return std::vector<ggml_tensor *>{ggml_soft_max(c, ggml_diag_mask_inf(c, ggml_add(c, kq, kq), n_past))};
+            }, in);
+        }
+    }
+
+    ggml_backend_free(gpu);
+    ggml_backend_free(cpu);
+    printf("%s\n", fails ? "FUSION_CHECK_FAIL" : "FUSION_CHECK_OK");
+    return fails ? 1 : 0;
+}

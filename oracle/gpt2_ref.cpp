@@ -257,15 +257,31 @@ int main(int argc, char **argv) {
     };
 
     std::vector<float> logits((size_t)m.n_vocab * toks.size());
+    // host-side phase times of the timed decode (--time-tokens): graph build, scheduler
+    // split + allocation, compute (submission and wait), logits read-back
+    double ph[4] = {0, 0, 0, 0};
+    bool phases = false;
+    auto now = [] { return std::chrono::steady_clock::now(); };
     auto eval = [&](int n_past, int32_t tok, float *dst) {
+        auto t0 = now();
         ggml_cgraph *gf = build(n_past);
+        auto t1 = now();
         ggml_backend_sched_reset(sched);
         if (!ggml_backend_sched_alloc_graph(sched, gf)) die("sched alloc failed");
         ggml_backend_tensor_set(embd, &tok, 0, 4);
         ggml_backend_tensor_set(position, &n_past, 0, 4);
+        auto t2 = now();
         if (ggml_backend_sched_graph_compute(sched, gf) != GGML_STATUS_SUCCESS) die("compute failed");
         ggml_tensor *res = ggml_graph_node(gf, -1);
+        auto t3 = now();
         if (dst) ggml_backend_tensor_get(res, dst, 0, sizeof(float) * m.n_vocab);
+        auto t4 = now();
+        if (phases) {
+            ph[0] += std::chrono::duration<double>(t1 - t0).count();
+            ph[1] += std::chrono::duration<double>(t2 - t1).count();
+            ph[2] += std::chrono::duration<double>(t3 - t2).count();
+            ph[3] += std::chrono::duration<double>(t4 - t3).count();
+        }
     };
     for (size_t i = 0; i < toks.size(); ++i) eval((int)i, toks[i], logits.data() + i * m.n_vocab);
     fprintf(stderr, "gpt2_ref: %zu tokens evaluated, %d backends, %d splits\n", toks.size(), (int)backends.size(),
@@ -280,11 +296,14 @@ int main(int argc, char **argv) {
         std::vector<float> tmp(m.n_vocab);
         const int start = (int)toks.size();
         const int n = std::min(time_tokens, m.n_ctx - start);
+        phases = true;
         const auto t0 = std::chrono::steady_clock::now();
         for (int i = 0; i < n; ++i) eval(start + i, (int32_t)(i % m.n_vocab), tmp.data());
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        printf("{\"tokens\": %d, \"seconds\": %.6f, \"ms_per_token\": %.4f, \"tokens_per_s\": %.3f, \"threads\": %d}\n", n, s,
-               1e3 * s / n, n / s, threads);
+        printf("{\"tokens\": %d, \"seconds\": %.6f, \"ms_per_token\": %.4f, \"tokens_per_s\": %.3f, \"threads\": %d, "
+               "\"ms_build\": %.4f, \"ms_sched_alloc\": %.4f, \"ms_compute\": %.4f, \"ms_get\": %.4f, \"splits\": %d}\n",
+               n, s, 1e3 * s / n, n / s, threads, 1e3 * ph[0] / n, 1e3 * ph[1] / n, 1e3 * ph[2] / n, 1e3 * ph[3] / n,
+               ggml_backend_sched_get_n_splits(sched));
     }
     ggml_backend_sched_free(sched);
     for (auto b : bufs) ggml_backend_buffer_free(b);
