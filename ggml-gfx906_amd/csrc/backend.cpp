@@ -119,6 +119,13 @@ struct ShardLane {
     Scratch src1, dst, mm;            // src1 copy, the shard's [rows x cols] result, mat-mat scratch; on `device`
 };
 
+// graph fusion plan of one graph_compute (be_graph_compute): nodes skipped because a later fused
+// launch computes them, and the fused attention launches by node index
+struct FusePlan {
+    std::vector<int8_t> skip;
+    std::map<int, AttnView> attn;
+};
+
 struct BackendCtx {
     int device;
     hipStream_t stream = nullptr;
@@ -126,6 +133,7 @@ struct BackendCtx {
     Scratch scratch;
     hipEvent_t src1_ready = nullptr;  // recorded on `stream` before shards start (split mat-mul)
     std::vector<std::unique_ptr<ShardLane>> shards;
+    FusePlan plan;                    // reused across graph_compute calls (no per-call allocation)
 };
 
 const char *BUFT_TAG = "MI355X";
@@ -873,21 +881,260 @@ int fuse_softmax(BackendCtx *c, const struct ggml_cgraph *g, int i, int n, int &
     return k + 1;
 }
 
+// ------------------------------------------------------------------------------------------
+// attention fusion (a graph pre-pass; its nodes are not adjacent in the node order):
+//   [CONT Q] .. MUL_MAT(K, Q) [SCALE] [DIAG_MASK_INF] SOFT_MAX, MUL_MAT(V^T, .) [PERMUTE, CONT]
+// with [CONT V^T] earlier, is GPT-2's attention (main-sched.cpp:658-732). One run_attention
+// launch at the last node replaces them: K is read through its view of the cache, Q and V^T
+// through the sources of their CONT nodes when those are skippable, and the result is written
+// straight into the final CONT's layout. Every intermediate must be skippable, and every compute
+// node between the first skipped node and the launch must belong to the pattern (a skipped
+// node's memory may be handed to a later node by ggml-alloc, so nothing else may run between).
+// ------------------------------------------------------------------------------------------
+// dims (ne[k], flat element stride fs[k]) at flat element offset f0 of a contiguous tensor whose
+// flat element order is S's (what CONT makes) -> byte strides / offset into S. False when a dim
+// would carry across S's dimensions (then no strided view exists).
+bool flat_to_strided(int nd, const int64_t *ne, const int64_t *fs, int64_t f0, const struct ggml_tensor *S, int64_t *nb,
+                     int64_t &off) {
+    int64_t pre[5] = {1, 0, 0, 0, 0};
+    for (int m = 0; m < 4; ++m) pre[m + 1] = pre[m] * S->ne[m];
+    int64_t ext[4];
+    off = 0;
+    for (int m = 0; m < 4; ++m) {
+        ext[m] = (f0 / pre[m]) % S->ne[m];
+        off += ext[m] * (int64_t)S->nb[m];
+    }
+    if (f0 >= pre[4]) return false;
+    for (int k = 0; k < nd; ++k) {
+        nb[k] = 0;
+        if (ne[k] <= 1) continue;
+        int m = 3;
+        while (m > 0 && (pre[m] > fs[k] || fs[k] % pre[m] != 0)) --m;
+        const int64_t q = fs[k] / pre[m];
+        ext[m] += q * (ne[k] - 1);
+        nb[k] = q * (int64_t)S->nb[m];
+    }
+    for (int m = 0; m < 4; ++m)
+        if (ext[m] >= S->ne[m]) return false;
+    return true;
+}
+
+int next_compute(const struct ggml_cgraph *g, int i, int n) {
+    for (int j = i + 1; j < n; ++j)
+        if (!is_view_op(g->nodes[j]->op) && !is_empty(g->nodes[j])) return j;
+    return n;
+}
+
+bool is_plain_copy(const struct ggml_tensor *t) {
+    return (t->op == GGMLABI_OP_CPY || t->op == GGMLABI_OP_CONT || t->op == GGMLABI_OP_DUP) && !is_hot_quant(t->type);
+}
+
+// two independent copies with only view nodes between them (GPT-2's K and V cache writes,
+// main-sched.cpp:654-655) as one launch; returns the nodes consumed (0: no pair)
+int pair_copies(BackendCtx *c, const struct ggml_cgraph *g, int i, int n, int &rc) {
+    const struct ggml_tensor *a = g->nodes[i];
+    const int j = next_compute(g, i, n);
+    if (j >= n || c->plan.skip[j] || c->plan.attn.count(j)) return 0;
+    const struct ggml_tensor *b = g->nodes[j];
+    if (!is_plain_copy(b) || b->src[0] == a || !disjoint(a, b->src[0]) || !disjoint(b, a->src[0]) || !disjoint(a, b)) return 0;
+    GraphOp ga, gb;
+    if (!graph_op_of(a, ga) || !graph_op_of(b, gb) || !cpy_pairable(ga, gb)) return 0;
+    rc = run_cpy_pair(ga, &gb, c->stream);
+    logf("fused 2 copies at %s and %s\n", a->name, b->name);
+    return j - i + 1;
+}
+
+bool attn_type(const struct ggml_tensor *t) { return t->type == GGMLABI_TYPE_F32 || t->type == GGMLABI_TYPE_F16; }
+
+void match_attention(const struct ggml_cgraph *g, int n, int ism, FusePlan &plan) {
+    struct ggml_tensor *sm = g->nodes[ism];
+    if (sm->src[1] || sm->src[2] || sm->type != GGMLABI_TYPE_F32 || !skippable(g, sm)) return;
+    AttnView a{};
+    float max_bias;
+    std::memcpy(&a.sm_scale, &sm->op_params[0], sizeof(float));
+    std::memcpy(&max_bias, &sm->op_params[1], sizeof(float));
+    if (max_bias != 0.0f) return;
+    a.pre_s = 1.0f;
+    a.n_past = -1;
+    std::vector<const struct ggml_tensor *> skip = {sm};
+    struct ggml_tensor *t = sm->src[0];
+    if (t->op == GGMLABI_OP_DIAG_MASK_INF) {
+        a.n_past = t->op_params[0];
+        skip.push_back(t);
+        t = t->src[0];
+    }
+    if (t->op == GGMLABI_OP_SCALE) {
+        std::memcpy(&a.pre_s, &t->op_params[0], sizeof(float));
+        std::memcpy(&a.pre_b, &t->op_params[1], sizeof(float));
+        skip.push_back(t);
+        t = t->src[0];
+    }
+    const struct ggml_tensor *kq = t;
+    if (kq->op != GGMLABI_OP_MUL_MAT) return;
+    skip.push_back(kq);
+    for (const struct ggml_tensor *c : skip)
+        if (!skippable(g, c) || !same_shape_t(c, sm) || c->type != GGMLABI_TYPE_F32) return;
+    const struct ggml_tensor *K = kq->src[0], *Q = kq->src[1];
+    const int ikqv = next_compute(g, ism, n);
+    if (ikqv >= n) return;
+    struct ggml_tensor *kqv = g->nodes[ikqv];
+    if (kqv->op != GGMLABI_OP_MUL_MAT || kqv->src[1] != sm || kqv->type != GGMLABI_TYPE_F32) return;
+    const struct ggml_tensor *Vt = kqv->src[0];
+    const int64_t D = K->ne[0], n_kv = K->ne[1], Hk = K->ne[2], n_q = Q->ne[1], H = Q->ne[2];
+    if (!attn_type(K) || Q->type != GGMLABI_TYPE_F32 || !attn_type(Vt)) return;
+    if (K->ne[3] != 1 || Q->ne[3] != 1 || Q->ne[0] != D || Hk < 1 || H % Hk != 0) return;
+    if (kq->ne[0] != n_kv || kq->ne[1] != n_q || kq->ne[2] != H || kq->ne[3] != 1) return;
+    if (Vt->ne[0] != n_kv || Vt->ne[1] != D || Vt->ne[2] != Hk || Vt->ne[3] != 1) return;
+    if (kqv->ne[0] != D || kqv->ne[1] != n_q || kqv->ne[2] != H || kqv->ne[3] != 1) return;
+    if (D > ATTN_MAX_D || n_kv > ATTN_MAX_KV || n_q > 65535 || H > 65535) return;
+
+    // output: through PERMUTE + CONT when that is what follows, else kqv itself
+    int ianchor = ikqv;
+    const struct ggml_tensor *out = kqv;
+    int64_t onb[3] = {(int64_t)kqv->nb[0], (int64_t)kqv->nb[1], (int64_t)kqv->nb[2]};
+    const int io = next_compute(g, ikqv, n);
+    if (io < n) {
+        const struct ggml_tensor *o = g->nodes[io], *p = o->src[0];
+        if (o->op == GGMLABI_OP_CONT && o->type == GGMLABI_TYPE_F32 && p && p->op == GGMLABI_OP_PERMUTE && p->src[0] == kqv &&
+            p->view_src == kqv && p->view_offs == 0 && use_count(g, kqv) == 1 && use_count(g, p) == 1 &&
+            !(kqv->flags & GGMLABI_TENSOR_FLAG_OUTPUT) && !(p->flags & GGMLABI_TENSOR_FLAG_OUTPUT) && kqv->view_src == nullptr) {
+            int64_t P[5] = {1, 0, 0, 0, 0};
+            for (int j = 0; j < 4; ++j) P[j + 1] = P[j] * p->ne[j];
+            const int64_t ne[3] = {D, n_q, H};
+            int64_t fs[3] = {0, 0, 0}, nb[3], off;
+            bool ok = true;
+            for (int k = 0; k < 3 && ok; ++k) {
+                if (ne[k] <= 1) continue;
+                int jm = -1;
+                for (int j = 0; j < 4; ++j)
+                    if (p->nb[j] == kqv->nb[k] && p->ne[j] == kqv->ne[k]) jm = j;
+                if (jm < 0) ok = false;
+                else fs[k] = P[jm];
+            }
+            if (ok && flat_to_strided(3, ne, fs, 0, o, nb, off) && off == 0) {
+                out = o;
+                ianchor = io;
+                for (int k = 0; k < 3; ++k) onb[k] = nb[k];
+                skip.push_back(kqv);
+            }
+        }
+    }
+    a.o = out->data;
+    a.o_d = onb[0]; a.o_i = onb[1]; a.o_h = onb[2];
+
+    // Q: through its CONT when Q is a direct, single-use view of a skippable f32 CONT
+    const struct ggml_tensor *qsrc = Q;
+    a.q = Q->data;
+    a.q_d = Q->nb[0]; a.q_i = Q->nb[1]; a.q_h = Q->nb[2];
+    {
+        const struct ggml_tensor *c = Q->view_src;
+        if (is_view_op(Q->op) && c && Q->src[0] == c && c->op == GGMLABI_OP_CONT && c->type == GGMLABI_TYPE_F32 &&
+            use_count(g, Q) == 1 && skippable(g, c) && c->src[0]->type == GGMLABI_TYPE_F32 && Q->nb[0] % 4 == 0 &&
+            Q->nb[1] % 4 == 0 && Q->nb[2] % 4 == 0 && Q->view_offs % 4 == 0) {
+            const int64_t ne[3] = {Q->ne[0], Q->ne[1], Q->ne[2]};
+            const int64_t fs[3] = {(int64_t)Q->nb[0] / 4, (int64_t)Q->nb[1] / 4, (int64_t)Q->nb[2] / 4};
+            int64_t nb[3], off;
+            if (flat_to_strided(3, ne, fs, (int64_t)Q->view_offs / 4, c->src[0], nb, off)) {
+                qsrc = c->src[0];
+                a.q = static_cast<const char *>(qsrc->data) + off;
+                a.q_d = nb[0]; a.q_i = nb[1]; a.q_h = nb[2];
+                skip.push_back(c);
+            }
+        }
+    }
+    // V^T: through its CONT when that is skippable
+    const struct ggml_tensor *vsrc = Vt;
+    a.v = Vt->data;
+    a.v_f16 = Vt->type == GGMLABI_TYPE_F16;
+    a.v_j = Vt->nb[0]; a.v_d = Vt->nb[1]; a.v_h = Vt->nb[2];
+    if (Vt->op == GGMLABI_OP_CONT && skippable(g, Vt) && Vt->src[0]->type == Vt->type) {
+        const int64_t ne[3] = {Vt->ne[0], Vt->ne[1], Vt->ne[2]};
+        const int64_t fs[3] = {1, Vt->ne[0], Vt->ne[0] * Vt->ne[1]};
+        int64_t nb[3], off;
+        if (flat_to_strided(3, ne, fs, 0, Vt->src[0], nb, off)) {
+            vsrc = Vt->src[0];
+            a.v = static_cast<const char *>(vsrc->data) + off;
+            a.v_j = nb[0]; a.v_d = nb[1]; a.v_h = nb[2];
+            skip.push_back(Vt);
+        }
+    }
+    a.k = K->data;
+    a.k_f16 = K->type == GGMLABI_TYPE_F16;
+    a.k_d = K->nb[0]; a.k_j = K->nb[1]; a.k_h = K->nb[2];
+#define NOFUSE(why)                                                                  \
+    do {                                                                             \
+        logf("attention at %s not fused: %s\n", sm->name, why);                      \
+        return;                                                                      \
+    } while (0)
+    // the launch writes `out` while reading these. ggml-alloc may hand Q's source (freed once its
+    // CONT ran) to the output: that is safe only when every (query, head) reads its Q row exactly
+    // where it writes its result (a workgroup reads q before it writes o)
+    const bool q_exact = a.o == a.q && (D <= 1 || a.o_d == a.q_d) && (n_q <= 1 || a.o_i == a.q_i) && (H <= 1 || a.o_h == a.q_h);
+    if (!disjoint(out, qsrc) && !q_exact) NOFUSE("output overlaps Q");
+    if (!disjoint(out, K) || !disjoint(out, vsrc)) NOFUSE("output overlaps K or V");
+    int first = ianchor;
+    std::vector<int> sidx;
+    for (const struct ggml_tensor *x : skip) {   // the pattern's nodes sit shortly before the launch
+        int j = ianchor;
+        while (j >= 0 && ianchor - j < 256 && g->nodes[j] != x) --j;
+        if (j < 0 || ianchor - j >= 256 || plan.skip[j] || plan.attn.count(j)) NOFUSE("pattern nodes not found");
+        sidx.push_back(j);
+        first = std::min(first, j);
+    }
+    // a node outside the pattern that runs between its first skipped node and the launch may write
+    // what the launch reads only if it did so before the skipped node that read it (a cache write
+    // ahead of the attention); its own inputs are never skipped nodes (those have one use each)
+    auto pos = [&](const struct ggml_tensor *x) {
+        for (size_t u = 0; u < skip.size(); ++u)
+            if (skip[u] == x) return sidx[u];
+        return ianchor;
+    };
+    const int rd_k = pos(kq);
+    const int rd_q = qsrc == Q ? pos(kq) : pos(Q->view_src);
+    const int rd_v = vsrc == Vt ? ianchor : pos(Vt);
+    for (int j = first; j < ianchor; ++j) {
+        const struct ggml_tensor *x = g->nodes[j];
+        if (is_view_op(x->op) || is_empty(x) || std::find(sidx.begin(), sidx.end(), j) != sidx.end()) continue;
+        if ((!disjoint(x, qsrc) && j > rd_q) || (!disjoint(x, K) && j > rd_k) || (!disjoint(x, vsrc) && j > rd_v))
+            NOFUSE("an interleaved node overwrites an input");
+    }
+#undef NOFUSE
+    a.D = (int)D; a.n_q = (int)n_q; a.n_kv = (int)n_kv; a.H = (int)H; a.Hk = (int)Hk;
+    for (int j : sidx) plan.skip[j] = 1;
+    plan.attn[ianchor] = a;
+}
+
+void plan_fusion(const struct ggml_cgraph *g, int n, FusePlan &plan) {
+    plan.skip.assign(n, 0);
+    plan.attn.clear();
+    if (!fusion_on()) return;
+    for (int i = 0; i < n; ++i)
+        if (g->nodes[i]->op == GGMLABI_OP_SOFT_MAX) match_attention(g, n, i, plan);
+}
+
 enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
     BackendCtx *c = be_ctx(b);
     const GgmlBase &gb = ggml_base();
     if (!gb.ok) return GGML_STATUS_FAILED;
     HIP_OK(hipSetDevice(c->device));
     const int n = gb.graph_n_nodes(g);
+    FusePlan &plan = c->plan;
+    plan_fusion(g, n, plan);
     for (int i = 0; i < n; ++i) {
         struct ggml_tensor *node = gb.graph_node(g, i);
-        if (is_empty(node) || is_view_op(node->op)) continue;
+        if (is_empty(node) || is_view_op(node->op) || plan.skip[i]) continue;
         int rc = GGML_MI355X_OK;
         GraphOp gop;
         int fused = 0;
-        if (fusion_on()) {
+        auto at = plan.attn.find(i);
+        if (at != plan.attn.end()) {
+            rc = run_attention(at->second, c->stream);
+            logf("fused attention at %s (n_kv=%d, n_q=%d, H=%d)\n", node->name, at->second.n_kv, at->second.n_q, at->second.H);
+            fused = 1;
+        } else if (fusion_on()) {
             if (node->op == GGMLABI_OP_NORM || node->op == GGMLABI_OP_MUL_MAT) fused = fuse_matvec(c, g, i, n, rc);
             else if (node->op == GGMLABI_OP_SCALE || node->op == GGMLABI_OP_DIAG_MASK_INF) fused = fuse_softmax(c, g, i, n, rc);
+            else if (is_plain_copy(node)) fused = pair_copies(c, g, i, n, rc);
         }
         if (fused > 0) {
             i += fused - 1;

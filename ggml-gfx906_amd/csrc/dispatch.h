@@ -78,7 +78,26 @@ struct SoftmaxPre {
     int n_past;          // DIAG_MASK_INF's n_past (-1: no mask node)
 };
 int run_graph_op_pre(const GraphOp &g, const SoftmaxPre *pre, hipStream_t st);
+// two CPY nodes in one launch (same type pair and shape relation); independence is the caller's
+bool cpy_pairable(const GraphOp &g0, const GraphOp &g1);
+int run_cpy_pair(const GraphOp &g0, const GraphOp *g1, hipStream_t st);
 int run_soft_max_pre(const GraphOp &g, const SoftmaxPre &pre, hipStream_t st);
+
+// attention over strided views (backend graph fusion of MUL_MAT(K, Q) -> [SCALE] ->
+// [DIAG_MASK_INF] -> SOFT_MAX -> MUL_MAT(V^T, .) [-> PERMUTE -> CONT]); byte strides, per
+// (query i, head h): O[:, i, h] = sum_j softmax_j(w_j) V^T[j, :, hk], hk = h / (H / Hk),
+// w_j = ((K[:, j, hk] . Q[:, i, h]) * pre_s (+ pre_b), -inf where j > n_past + i) * sm_scale
+struct AttnView {
+    const void *q;  int64_t q_d, q_i, q_h;              // f32
+    const void *k;  int k_f16; int64_t k_d, k_j, k_h;   // f32 or f16
+    const void *v;  int v_f16; int64_t v_j, v_d, v_h;   // f32 or f16 (V^T[j, d, hk])
+    void *o;        int64_t o_d, o_i, o_h;              // f32
+    int D, n_q, n_kv, H, Hk;
+    float pre_s, pre_b, sm_scale;
+    int n_past;                                         // -1: no causal mask
+};
+constexpr int ATTN_MAX_D = 256, ATTN_MAX_KV = 14336;   // scores of one row live in LDS
+int run_attention(const AttnView &a, hipStream_t st);
 
 // quantized mat-vec with the decode-layer fusions (mmvq_fused.hip): layer-norm prologue,
 // bias / GELU / residual epilogue (MmArgs fields); nc columns per launch column group

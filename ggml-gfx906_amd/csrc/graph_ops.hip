@@ -11,7 +11,9 @@
 #include "dispatch.h"
 #include "qcommon.h"
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 namespace mi355x {
@@ -287,8 +289,18 @@ template <> __device__ __forceinline__ uint16_t cvt<float, uint16_t>(float v) { 
 template <> __device__ __forceinline__ float cvt<uint16_t, float>(uint16_t v) { return h2f_dev(v); }
 template <> __device__ __forceinline__ uint16_t cvt<uint16_t, uint16_t>(uint16_t v) { return v; }
 
+// up to two independent copies per launch (blockIdx.y picks one): the backend pairs adjacent
+// CPY nodes such as GPT-2's K and V cache writes (main-sched.cpp:654-655)
+struct CpyPair {
+    DevT d0, a0, d1, a1;
+    int64_t rows0, rows1;
+};
+
 template <typename TS, typename TD, bool SAME>
-__global__ __launch_bounds__(256) void cpy_kernel(const DevT d, const DevT a, int64_t rows) {
+__global__ __launch_bounds__(256) void cpy_kernel(const CpyPair c) {
+    const bool second = blockIdx.y != 0;
+    const DevT d = second ? c.d1 : c.d0, a = second ? c.a1 : c.a0;
+    const int64_t rows = second ? c.rows1 : c.rows0;
     // iterate over src rows; dst coordinates follow from the flattened index
     for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
         int64_t i1, i2, i3;
@@ -344,6 +356,184 @@ __global__ __launch_bounds__(256) void mm_float_kernel(const DevT d, const DevT 
         const float s = wave_sum(acc[c]);
         if (lane == c && c < nc)
             *reinterpret_cast<float *>(d.p + row * d.nb[0] + (c0 + c) * d.nb[1] + i12 * d.nb[2] + i13 * d.nb[3]) = s;
+    }
+}
+
+
+// ------------------------------------------------------------------------------------------
+// fused attention (backend graph fusion, see AttnView): one workgroup per (query, head).
+//   scores: 16 lanes per key, lane l reads d = l, l+16, ... (64-B runs of a key row), 4 DPP/
+//     shuffle steps reduce them; the scalar chain per score is the one ggml applies node by
+//     node: (dot * s [+ b]) -> -inf above the causal diagonal -> * soft_max scale.
+//   soft_max: block max, exp, sum in double (as soft_max_kernel / ggml-cpu ops.cpp:5685-5795).
+//   output: lane = d (256-B V^T row segments), 4 waves over keys, LDS sum, * 1/sum.
+// Latency-bound at decode sizes (n_q * H workgroups of n_kv * D * 8 bytes of K and V).
+// ------------------------------------------------------------------------------------------
+template <typename T> __device__ __forceinline__ float ldf(const char *p);
+template <> __device__ __forceinline__ float ldf<float>(const char *p) { return *reinterpret_cast<const float *>(p); }
+template <> __device__ __forceinline__ float ldf<uint16_t>(const char *p) { return h2f_dev(*reinterpret_cast<const uint16_t *>(p)); }
+
+template <typename TK, typename TV>
+__global__ __launch_bounds__(256) void attn_kernel(const AttnView a) {
+    extern __shared__ float sc[];                  // [n_kv] scores, then exp(score - max)
+    __shared__ float qs[ATTN_MAX_D];
+    __shared__ float red_f[4];
+    __shared__ double red_d[4];
+    __shared__ float part[4][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = tid & 15;
+    const int i = blockIdx.x, h = blockIdx.y, hk = h / (a.H / a.Hk);
+    const char *qp = static_cast<const char *>(a.q) + i * a.q_i + h * a.q_h;
+    for (int d = tid; d < a.D; d += 256) qs[d] = *reinterpret_cast<const float *>(qp + d * a.q_d);
+    __syncthreads();
+    const char *kb = static_cast<const char *>(a.k) + hk * a.k_h;
+    float mx = -INFINITY;
+    for (int j0 = 0; j0 < a.n_kv; j0 += 16) {
+        const int j = j0 + (tid >> 4);
+        float acc = 0.f;
+        if (j < a.n_kv) {
+            const char *kp = kb + (int64_t)j * a.k_j;
+            for (int d = l16; d < a.D; d += 16) acc = fmaf(ldf<TK>(kp + d * a.k_d), qs[d], acc);
+        }
+        acc += __shfl_xor(acc, 8, 64);
+        acc += __shfl_xor(acc, 4, 64);
+        acc += __shfl_xor(acc, 2, 64);
+        acc += __shfl_xor(acc, 1, 64);
+        if (j < a.n_kv) {
+            float x = a.pre_b == 0.f ? acc * a.pre_s : fmaf(acc, a.pre_s, a.pre_b);
+            if (a.n_past >= 0 && j > a.n_past + i) x = -INFINITY;
+            const float w = x * a.sm_scale;
+            if (l16 == 0) sc[j] = w;
+            mx = fmaxf(mx, w);
+        }
+    }
+    mx = block_reduce(mx, red_f, [](float x, float y) { return fmaxf(x, y); });
+    double sum = 0.0;
+    for (int j = tid; j < a.n_kv; j += 256) {
+        const float e = expf(sc[j] - mx);
+        sc[j] = e;
+        sum += (double)e;
+    }
+    sum = block_reduce(sum, red_d, [](double x, double y) { return x + y; });   // (its barriers publish sc)
+    const float inv = (float)(1.0 / sum);
+    const char *vb = static_cast<const char *>(a.v) + hk * a.v_h;
+    char *ob = static_cast<char *>(a.o) + i * a.o_i + h * a.o_h;
+    for (int d0 = 0; d0 < a.D; d0 += 64) {
+        const int d = d0 + lane;
+        float o = 0.f;
+        if (d < a.D)
+            for (int j = wave; j < a.n_kv; j += 4) o = fmaf(sc[j] * inv, ldf<TV>(vb + (int64_t)j * a.v_j + d * a.v_d), o);
+        part[wave][lane] = o;
+        __syncthreads();
+        if (wave == 0 && d < a.D)
+            *reinterpret_cast<float *>(ob + d * a.o_d) = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+        __syncthreads();
+    }
+}
+
+// D = 64, f32 K / V with unit d stride and 16-B aligned rows (GPT-2's caches): the same
+// arithmetic with one dependent memory round trip at decode sizes. Every load that does not
+// depend on a score is issued first: q, this thread's key row (16 float4) and the first
+// ATTN_VPRE V^T rows of its output slot; the softmax runs while they land.
+//   scores: one key per thread (more keys: further rounds of 256)
+//   output: 16 lanes x float4 cover d, 16 key slots per workgroup
+constexpr int ATTN_VPRE = 8;   // V^T rows prefetched per slot: n_kv <= 128 needs no further loads
+
+__global__ __launch_bounds__(256) void attn_kernel_d64(const AttnView a) {
+    extern __shared__ float sc[];
+    __shared__ float4 q4[16];
+    __shared__ float red_f[4];
+    __shared__ double red_d[4];
+    __shared__ float4 part[4][16];
+    const int tid = threadIdx.x, wave = tid >> 6, l16 = tid & 15, slot = tid >> 4;
+    const int i = blockIdx.x, h = blockIdx.y, hk = h / (a.H / a.Hk);
+    const char *qp = static_cast<const char *>(a.q) + i * a.q_i + h * a.q_h;
+    const char *kb = static_cast<const char *>(a.k) + hk * a.k_h;
+    const char *vb = static_cast<const char *>(a.v) + hk * a.v_h + l16 * 16;
+    const int n_kv = a.n_kv;
+    float qv = 0.f;
+    if (tid < 64) qv = *reinterpret_cast<const float *>(qp + tid * a.q_d);
+    float4 kv[16];
+    {
+        const float4 *kr = reinterpret_cast<const float4 *>(kb + (int64_t)min(tid, n_kv - 1) * a.k_j);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) kv[u] = kr[u];
+    }
+    float4 vv[ATTN_VPRE];
+#pragma unroll
+    for (int u = 0; u < ATTN_VPRE; ++u)
+        vv[u] = *reinterpret_cast<const float4 *>(vb + (int64_t)min(slot + 16 * u, n_kv - 1) * a.v_j);
+    if (tid < 64) reinterpret_cast<float *>(q4)[tid] = qv;
+    __syncthreads();
+    auto score = [&](int j, const float4 (&k)[16]) {
+        float acc = 0.f;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const float4 q = q4[u];
+            acc = fmaf(k[u].x, q.x, acc);
+            acc = fmaf(k[u].y, q.y, acc);
+            acc = fmaf(k[u].z, q.z, acc);
+            acc = fmaf(k[u].w, q.w, acc);
+        }
+        float x = a.pre_b == 0.f ? acc * a.pre_s : fmaf(acc, a.pre_s, a.pre_b);
+        if (a.n_past >= 0 && j > a.n_past + i) x = -INFINITY;
+        return x * a.sm_scale;
+    };
+    float mx = -INFINITY;
+    if (tid < n_kv) {
+        const float w = score(tid, kv);
+        sc[tid] = w;
+        mx = w;
+    }
+    for (int j = tid + 256; j < n_kv; j += 256) {
+        const float4 *kr = reinterpret_cast<const float4 *>(kb + (int64_t)j * a.k_j);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) kv[u] = kr[u];
+        const float w = score(j, kv);
+        sc[j] = w;
+        mx = fmaxf(mx, w);
+    }
+    mx = block_reduce(mx, red_f, [](float x, float y) { return fmaxf(x, y); });
+    double sum = 0.0;
+    for (int j = tid; j < n_kv; j += 256) {   // the keys this thread scored
+        const float e = expf(sc[j] - mx);
+        sc[j] = e;
+        sum += (double)e;
+    }
+    sum = block_reduce(sum, red_d, [](double x, double y) { return x + y; });   // (its barriers publish sc)
+    const float inv = (float)(1.0 / sum);
+    float4 o0 = make_float4(0.f, 0.f, 0.f, 0.f), o1 = o0;
+    auto acc4 = [](float4 &o, float p, float4 v) {
+        o.x = fmaf(p, v.x, o.x); o.y = fmaf(p, v.y, o.y); o.z = fmaf(p, v.z, o.z); o.w = fmaf(p, v.w, o.w);
+    };
+#pragma unroll
+    for (int u = 0; u < ATTN_VPRE; ++u) {
+        const int j = slot + 16 * u;
+        if (j < n_kv) acc4((u & 1) ? o1 : o0, sc[j] * inv, vv[u]);
+    }
+    int j = slot + 16 * ATTN_VPRE;
+    for (; j + 16 < n_kv; j += 32) {
+        const float4 v0 = *reinterpret_cast<const float4 *>(vb + (int64_t)j * a.v_j);
+        const float4 v1 = *reinterpret_cast<const float4 *>(vb + (int64_t)(j + 16) * a.v_j);
+        acc4(o0, sc[j] * inv, v0);
+        acc4(o1, sc[j + 16] * inv, v1);
+    }
+    if (j < n_kv) acc4(o0, sc[j] * inv, *reinterpret_cast<const float4 *>(vb + (int64_t)j * a.v_j));
+    float4 o = make_float4(o0.x + o1.x, o0.y + o1.y, o0.z + o1.z, o0.w + o1.w);
+    // the 4 key slots of a wave: lanes l16, l16+16, l16+32, l16+48
+#pragma unroll
+    for (int sh = 16; sh <= 32; sh <<= 1) {
+        o.x += __shfl_xor(o.x, sh, 64);
+        o.y += __shfl_xor(o.y, sh, 64);
+        o.z += __shfl_xor(o.z, sh, 64);
+        o.w += __shfl_xor(o.w, sh, 64);
+    }
+    if ((tid & 63) < 16) part[wave][l16] = o;
+    __syncthreads();
+    if (tid < 64) {
+        const int d = tid;   // 64 outputs, one per lane of wave 0
+        const float *pp = reinterpret_cast<const float *>(part);
+        const float r = (pp[d] + pp[64 + d]) + (pp[128 + d] + pp[192 + d]);
+        *reinterpret_cast<float *>(static_cast<char *>(a.o) + i * a.o_i + h * a.o_h + d * a.o_d) = r;
     }
 }
 
@@ -409,6 +599,66 @@ int check_graph_op(const GraphOp &g) {
 
 int run_graph_op(const GraphOp &g, hipStream_t st) { return run_graph_op_pre(g, nullptr, st); }
 
+namespace {
+int cpy_key(const GraphOp &g) { return (g.src[0].type == T_F16 ? 2 : 0) + (g.dst.type == T_F16 ? 1 : 0); }
+}  // namespace
+
+bool cpy_pairable(const GraphOp &g0, const GraphOp &g1) {
+    return g0.op == GOP_CPY && g1.op == GOP_CPY && check_graph_op(g0) == GGML_MI355X_OK && check_graph_op(g1) == GGML_MI355X_OK &&
+           cpy_key(g0) == cpy_key(g1) && same_shape(g0.src[0], g0.dst) == same_shape(g1.src[0], g1.dst);
+}
+
+// one CPY, or two pairable ones (cpy_pairable; the caller checked they are independent) in one launch
+int run_cpy_pair(const GraphOp &g0, const GraphOp *g1, hipStream_t st) {
+    int rc = check_graph_op(g0);
+    if (rc == GGML_MI355X_OK && g1) rc = cpy_pairable(g0, *g1) ? GGML_MI355X_OK : GGML_MI355X_EINVAL;
+    if (rc != GGML_MI355X_OK) return rc;
+    CpyPair c{};
+    c.d0 = dev(g0.dst);
+    c.a0 = dev(g0.src[0]);
+    c.rows0 = nelem(g0.dst) == 0 ? 0 : nrows(g0.src[0]);
+    if (g1) {
+        c.d1 = dev(g1->dst);
+        c.a1 = dev(g1->src[0]);
+        c.rows1 = nelem(g1->dst) == 0 ? 0 : nrows(g1->src[0]);
+    }
+    const int64_t rows = std::max(c.rows0, c.rows1);
+    if (rows == 0) return GGML_MI355X_OK;
+    const dim3 grid(grid_for(rows, 1), g1 ? 2 : 1);
+    const bool same = same_shape(g0.src[0], g0.dst);
+#define CPY_CASE(K, TS, TD)                                                                     \
+    case K:                                                                                     \
+        if (same) hipLaunchKernelGGL((cpy_kernel<TS, TD, true>), grid, dim3(256), 0, st, c);   \
+        else hipLaunchKernelGGL((cpy_kernel<TS, TD, false>), grid, dim3(256), 0, st, c);       \
+        break;
+    switch (cpy_key(g0)) {
+        CPY_CASE(0, float, float)
+        CPY_CASE(1, float, uint16_t)
+        CPY_CASE(2, uint16_t, float)
+        CPY_CASE(3, uint16_t, uint16_t)
+    }
+#undef CPY_CASE
+    return hipGetLastError() == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
+}
+
+int run_attention(const AttnView &a, hipStream_t st) {
+    if (a.D < 1 || a.D > ATTN_MAX_D || a.n_kv < 1 || a.n_kv > ATTN_MAX_KV || a.n_q < 1 || a.H < 1 || a.Hk < 1 ||
+        a.H % a.Hk != 0 || a.n_q > 65535 || a.H > 65535)
+        return GGML_MI355X_EINVAL;
+    const dim3 grid((unsigned)a.n_q, (unsigned)a.H);
+    const size_t lds = (size_t)a.n_kv * sizeof(float);
+    auto al16 = [](const void *p, int64_t s1, int64_t s2) { return (uintptr_t)p % 16 == 0 && s1 % 16 == 0 && s2 % 16 == 0; };
+    static const bool generic = getenv("GGML_MI355X_ATTN_GENERIC") != nullptr;   // A/B switch
+    if (!generic && a.D == 64 && !a.k_f16 && !a.v_f16 && a.k_d == 4 && a.v_d == 4 && al16(a.k, a.k_j, a.k_h) &&
+        al16(a.v, a.v_j, a.v_h)) {
+        hipLaunchKernelGGL(attn_kernel_d64, grid, dim3(256), lds, st, a);
+    } else if (a.k_f16 && a.v_f16) hipLaunchKernelGGL((attn_kernel<uint16_t, uint16_t>), grid, dim3(256), lds, st, a);
+    else if (a.k_f16) hipLaunchKernelGGL((attn_kernel<uint16_t, float>), grid, dim3(256), lds, st, a);
+    else if (a.v_f16) hipLaunchKernelGGL((attn_kernel<float, uint16_t>), grid, dim3(256), lds, st, a);
+    else hipLaunchKernelGGL((attn_kernel<float, float>), grid, dim3(256), lds, st, a);
+    return hipGetLastError() == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
+}
+
 // SCALE -> DIAG_MASK_INF -> SOFT_MAX as one launch (backend fusion): g is the SOFT_MAX node with
 // src[0] replaced by the SCALE node's input
 int run_soft_max_pre(const GraphOp &g, const SoftmaxPre &pre, hipStream_t st) {
@@ -471,25 +721,8 @@ int run_graph_op_pre(const GraphOp &g, const SoftmaxPre *pre, hipStream_t st) {
         case GOP_GELU:
             hipLaunchKernelGGL(gelu_kernel, dim3(grid_for(rows, 1)), blk, 0, st, d, a, rows);
             break;
-        case GOP_CPY: {
-            const int64_t srows = nrows(av);
-            const dim3 grid(grid_for(srows, 1));
-            const bool same = same_shape(av, dv);
-            const int key = (av.type == T_F16 ? 2 : 0) + (dv.type == T_F16 ? 1 : 0);
-#define CPY_CASE(K, TS, TD)                                                                                     \
-    case K:                                                                                                     \
-        if (same) hipLaunchKernelGGL((cpy_kernel<TS, TD, true>), grid, blk, 0, st, d, a, srows);              \
-        else hipLaunchKernelGGL((cpy_kernel<TS, TD, false>), grid, blk, 0, st, d, a, srows);                  \
-        break;
-            switch (key) {
-                CPY_CASE(0, float, float)
-                CPY_CASE(1, float, uint16_t)
-                CPY_CASE(2, uint16_t, float)
-                CPY_CASE(3, uint16_t, uint16_t)
-            }
-#undef CPY_CASE
-            break;
-        }
+        case GOP_CPY:
+            return run_cpy_pair(g, nullptr, st);
         case GOP_MUL_MAT: {
             const DevT b = dev(g.src[1]);
             const dim3 grid((unsigned)((av.ne[1] + 3) / 4), (unsigned)((g.src[1].ne[1] + 3) / 4),

@@ -90,6 +90,16 @@ std::vector<uint8_t> f32_bytes(size_t n, float lo, float hi) {
     return b;
 }
 
+std::vector<uint8_t> f16_bytes(size_t n) {
+    std::uniform_real_distribution<float> u(-1.f, 1.f);
+    std::vector<uint8_t> b(n * 2);
+    for (size_t i = 0; i < n; ++i) {
+        const ggml_fp16_t h = ggml_fp32_to_fp16(u(rng));
+        memcpy(&b[i * 2], &h, 2);
+    }
+    return b;
+}
+
 std::vector<uint8_t> q_bytes(ggml_type t, int64_t K, int64_t N) {
     std::uniform_real_distribution<float> u(-1.f, 1.f);
     std::vector<float> w((size_t)K * N);
@@ -240,6 +250,55 @@ int main(int argc, char **argv) {
                 ggml_tensor *kq = input(c, "kq", GGML_TYPE_F32, n_kv, N, H);
                 return std::vector<ggml_tensor *>{ggml_soft_max(c, ggml_diag_mask_inf(c, ggml_add(c, kq, kq), n_past))};
             }, in);
+        }
+    }
+
+    // GPT-2's attention block as main-sched.cpp:641-732 builds it (layer 1 of 2, so every cache
+    // view has an offset): the K / V cache writes, then Q . K^T -> scale -> causal mask ->
+    // soft_max -> V^T . -> merged heads. The plugin runs the whole read side as one launch.
+    for (int n_past : {0, 7, 100}) {
+        for (int N : {1, 4}) {
+            for (int variant : {0, 1, 2}) {   // 1: soft_max is an output, 2: f16 caches
+                const int sm_out = variant == 1;
+                const ggml_type ct = variant == 2 ? GGML_TYPE_F16 : GGML_TYPE_F32;
+                if (variant != 0 && n_past != 7) continue;
+                const int E = 768, H = 12, Dh = E / H, n_ctx = 128, n_layer = 2, il = 1;
+                const float kq_scale = 1.0f / sqrtf((float)Dh);
+                Inputs in;
+                in.bytes["cur"] = f32_bytes((size_t)3 * E * N, -1.f, 1.f);
+                const size_t n_cache = (size_t)n_layer * n_ctx * E;
+                in.bytes["memk"] = ct == GGML_TYPE_F16 ? f16_bytes(n_cache) : f32_bytes(n_cache, -1.f, 1.f);
+                in.bytes["memv"] = ct == GGML_TYPE_F16 ? f16_bytes(n_cache) : f32_bytes(n_cache, -1.f, 1.f);
+                const std::string tag = "n_past=" + std::to_string(n_past) + " N=" + std::to_string(N);
+                const char *kind = variant == 1 ? "attention_sm_output " : variant == 2 ? "attention_f16 " : "attention ";
+                check(std::string(kind) + tag, [&](ggml_context *c, ggml_cgraph *gf) {
+                    ggml_tensor *cur = resident(input(c, "cur", GGML_TYPE_F32, 3 * E, N));
+                    ggml_tensor *memk = resident(input(c, "memk", ct, (int64_t)n_layer * n_ctx * E));
+                    ggml_tensor *memv = resident(input(c, "memv", ct, (int64_t)n_layer * n_ctx * E));
+                    ggml_tensor *Qcur = ggml_view_2d(c, cur, E, N, cur->nb[1], 0 * sizeof(float) * E);
+                    ggml_tensor *Kcur = ggml_view_2d(c, cur, E, N, cur->nb[1], 1 * sizeof(float) * E);
+                    ggml_tensor *Vcur = ggml_view_2d(c, cur, E, N, cur->nb[1], 2 * sizeof(float) * E);
+                    ggml_tensor *k = ggml_view_1d(c, memk, N * E, (ggml_element_size(memk) * E) * (il * n_ctx + n_past));
+                    ggml_tensor *v = ggml_view_1d(c, memv, N * E, (ggml_element_size(memv) * E) * (il * n_ctx + n_past));
+                    ggml_build_forward_expand(gf, ggml_cpy(c, Kcur, k));
+                    ggml_build_forward_expand(gf, ggml_cpy(c, Vcur, v));
+                    ggml_tensor *Q = ggml_permute(c, ggml_cont_3d(c, Qcur, Dh, H, N), 0, 2, 1, 3);
+                    ggml_tensor *K = ggml_permute(c,
+                        ggml_reshape_3d(c, ggml_view_1d(c, memk, (n_past + N) * E, il * n_ctx * ggml_element_size(memk) * E), Dh, H, n_past + N),
+                        0, 2, 1, 3);
+                    ggml_tensor *KQ = ggml_mul_mat(c, K, Q);
+                    ggml_tensor *sm = ggml_soft_max(c, ggml_diag_mask_inf(c, ggml_scale(c, KQ, kq_scale), n_past));
+                    if (sm_out) ggml_set_output(sm);
+                    ggml_tensor *Vt = ggml_cont_3d(c,
+                        ggml_permute(c,
+                            ggml_reshape_3d(c, ggml_view_1d(c, memv, (n_past + N) * E, il * n_ctx * ggml_element_size(memv) * E), Dh, H, n_past + N),
+                            1, 2, 0, 3),
+                        n_past + N, Dh, H);
+                    ggml_tensor *KQV = ggml_mul_mat(c, Vt, sm);
+                    ggml_tensor *out = ggml_cont_2d(c, ggml_permute(c, KQV, 0, 2, 1, 3), E, N);
+                    return std::vector<ggml_tensor *>{out};
+                }, in);
+            }
         }
     }
 

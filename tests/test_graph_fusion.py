@@ -20,27 +20,35 @@ LIB = os.path.join(ROOT, "ggml-gfx906_amd", "libggml-hip-mi355x.so")
 pytestmark = pytest.mark.gpu
 
 
-def _run(fusion: bool):
+def _run(fusion: bool, **extra):
     if not os.path.exists(BIN):
         pytest.skip("oracle/_ref/fusion_check not built")
-    env = dict(os.environ, GGML_MI355X_DEBUG="1", GGML_MI355X_FUSION="1" if fusion else "0")
+    env = dict(os.environ, GGML_MI355X_DEBUG="1", GGML_MI355X_FUSION="1" if fusion else "0", **extra)
     r = subprocess.run([BIN, LIB], capture_output=True, text=True, env=env, timeout=300)
     fails = [l for l in r.stdout.splitlines() if l.startswith("FAIL")]
     assert r.returncode == 0 and "FUSION_CHECK_OK" in r.stdout, (fails, r.stdout[-1500:], r.stderr[-1500:])
-    fused = {}
+    fused, attn, pairs = {}, {}, {}
     case = None
     for line in r.stderr.splitlines():
         if line.startswith("CASE "):
             case = line[5:].strip()
             fused[case] = []
+            attn[case] = 0
+            pairs[case] = 0
         m = re.search(r"fused (\d+) nodes", line)
         if m and case is not None:
             fused[case].append(int(m.group(1)))
-    return fused
+        if "fused attention" in line and case is not None:
+            attn[case] += 1
+        if "fused 2 copies" in line and case is not None:
+            pairs[case] += 1
+    return fused, attn, pairs
 
 
-def test_fused_chains_match_cpu_and_fuse():
-    fused = _run(True)
+@pytest.mark.parametrize("attn_kernel", ["d64", "generic"])
+def test_fused_chains_match_cpu_and_fuse(attn_kernel):
+    extra = {"GGML_MI355X_ATTN_GENERIC": "1"} if attn_kernel == "generic" else {}
+    fused, attn, pairs = _run(True, **extra)
     for t in ("q4_0", "q8_0", "q4_K", "q5_K", "q6_K"):
         for m in (1, 3, 8):
             tag = f"{t} M={m}"
@@ -58,8 +66,14 @@ def test_fused_chains_match_cpu_and_fuse():
             assert v == [3], k
         elif k.startswith("softmax_mask_only"):
             assert v == [2], k
+        elif k.startswith("attention ") or k.startswith("attention_f16"):   # the read side is one launch,
+            assert v == [] and attn[k] == 1 and pairs[k] == 1, (k, v, attn[k], pairs[k])  # the cache writes another
+        elif k.startswith("attention_sm_output"):  # soft_max is an output: scale/mask/soft_max only
+            assert v == [3] and attn[k] == 0, (k, v, attn[k])
+    assert sum(1 for k in attn if k.startswith("attention ")) == 6
 
 
 def test_unfused_graph_matches_cpu():
-    fused = _run(False)
+    fused, attn, pairs = _run(False)
     assert all(v == [] for v in fused.values()), fused
+    assert not any(attn.values()) and not any(pairs.values()), (attn, pairs)
