@@ -126,6 +126,23 @@ struct FusePlan {
     std::map<int, AttnView> attn;
 };
 
+// hipGraph of the last graph_compute (cf. the reference's CUDA graphs, ggml-cuda.cu:2757-2998):
+// the node properties it was captured from, and how many calls in a row needed a new capture
+struct NodeProps {
+    const void *node, *data;
+    int32_t op, flags;
+    int64_t ne[4];
+    size_t nb[4];
+    int32_t op_params[16];
+    const void *src[GGMLABI_MAX_SRC], *src_data[GGMLABI_MAX_SRC];
+};
+struct GraphCache {
+    hipGraphExec_t exec = nullptr;
+    std::vector<NodeProps> props;
+    int updates = 0;
+    bool disabled = false;
+};
+
 struct BackendCtx {
     int device;
     hipStream_t stream = nullptr;
@@ -134,6 +151,7 @@ struct BackendCtx {
     hipEvent_t src1_ready = nullptr;  // recorded on `stream` before shards start (split mat-mul)
     std::vector<std::unique_ptr<ShardLane>> shards;
     FusePlan plan;                    // reused across graph_compute calls (no per-call allocation)
+    GraphCache hg;
 };
 
 const char *BUFT_TAG = "MI355X";
@@ -558,6 +576,7 @@ void be_free(ggml_backend_t b) {
     BackendCtx *c = be_ctx(b);
     HIP_OK(hipSetDevice(c->device));
     HIP_OK(hipStreamSynchronize(c->stream));
+    if (c->hg.exec) HIP_OK(hipGraphExecDestroy(c->hg.exec));
     HIP_OK(hipStreamDestroy(c->stream));
     if (c->src1_ready) HIP_OK(hipEventDestroy(c->src1_ready));
     for (auto &L : c->shards) {
@@ -1112,11 +1131,10 @@ void plan_fusion(const struct ggml_cgraph *g, int n, FusePlan &plan) {
         if (g->nodes[i]->op == GGMLABI_OP_SOFT_MAX) match_attention(g, n, i, plan);
 }
 
-enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
-    BackendCtx *c = be_ctx(b);
+// queue every node of g on the backend stream (fused runs as planned); quiet: a failure is
+// expected to be retried (inside a hipGraph capture) and is only logged in debug mode
+enum ggml_status run_nodes(BackendCtx *c, struct ggml_cgraph *g, bool quiet) {
     const GgmlBase &gb = ggml_base();
-    if (!gb.ok) return GGML_STATUS_FAILED;
-    HIP_OK(hipSetDevice(c->device));
     const int n = gb.graph_n_nodes(g);
     FusePlan &plan = c->plan;
     plan_fusion(g, n, plan);
@@ -1155,10 +1173,112 @@ enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
             return GGML_STATUS_FAILED;
         }
         if (rc != GGML_MI355X_OK) {
-            fprintf(stderr, "[ggml-mi355x] node %s (op %d) failed: %s\n", node->name, node->op, ggml_mi355x_strerror(rc));
+            if (quiet) logf("node %s (op %d) failed during capture: %s\n", node->name, node->op, ggml_mi355x_strerror(rc));
+            else fprintf(stderr, "[ggml-mi355x] node %s (op %d) failed: %s\n", node->name, node->op, ggml_mi355x_strerror(rc));
             return GGML_STATUS_FAILED;
         }
     }
+    return GGML_STATUS_SUCCESS;
+}
+
+// hipGraph use, as the reference decides for CUDA graphs (ggml-cuda.cu:2890-2998): on unless
+// GGML_MI355X_GRAPHS=0; never for graphs with row-split weights (their shards run on other
+// devices' streams); a graph whose nodes changed is re-captured and the executable updated in
+// place, and after GGML_MI355X_GRAPH_MAX_UPDATES (default 4) such calls in a row the backend
+// stops capturing (the graph changes every call, so capturing only adds host work).
+bool graphs_on() {
+    static const bool on = !(getenv("GGML_MI355X_GRAPHS") && atoi(getenv("GGML_MI355X_GRAPHS")) == 0);
+    return on;
+}
+int graph_max_updates() {
+    static const int v = getenv("GGML_MI355X_GRAPH_MAX_UPDATES") ? atoi(getenv("GGML_MI355X_GRAPH_MAX_UPDATES")) : 4;
+    return v;
+}
+
+void node_props(const struct ggml_tensor *t, NodeProps &p) {
+    std::memset(&p, 0, sizeof p);
+    p.node = t;
+    p.data = t->data;
+    p.op = t->op;
+    p.flags = t->flags;
+    for (int i = 0; i < 4; ++i) {
+        p.ne[i] = t->ne[i];
+        p.nb[i] = t->nb[i];
+    }
+    std::memcpy(p.op_params, t->op_params, sizeof p.op_params);
+    for (int i = 0; i < GGMLABI_MAX_SRC; ++i) {
+        p.src[i] = t->src[i];
+        p.src_data[i] = t->src[i] ? t->src[i]->data : nullptr;
+    }
+}
+
+// true when g has the nodes the cached graph was captured from; refreshes the cache either way
+bool graph_unchanged(GraphCache &hg, struct ggml_cgraph *g) {
+    const GgmlBase &gb = ggml_base();
+    const int n = gb.graph_n_nodes(g);
+    bool same = (int)hg.props.size() == n;
+    if (!same) hg.props.resize(n);
+    for (int i = 0; i < n; ++i) {
+        NodeProps p;
+        node_props(gb.graph_node(g, i), p);
+        if (same && std::memcmp(&p, &hg.props[i], sizeof p) != 0) same = false;
+        hg.props[i] = p;
+    }
+    return same;
+}
+
+bool has_split_weights(struct ggml_cgraph *g) {
+    const GgmlBase &gb = ggml_base();
+    const int n = gb.graph_n_nodes(g);
+    for (int i = 0; i < n; ++i) {
+        const struct ggml_tensor *t = gb.graph_node(g, i);
+        if (t->op == GGMLABI_OP_MUL_MAT && t->src[0]->buffer && is_split_buft(t->src[0]->buffer->buft)) return true;
+    }
+    return false;
+}
+
+enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
+    BackendCtx *c = be_ctx(b);
+    if (!ggml_base().ok) return GGML_STATUS_FAILED;
+    HIP_OK(hipSetDevice(c->device));
+    GraphCache &hg = c->hg;
+    if (!graphs_on() || hg.disabled || has_split_weights(g)) return run_nodes(c, g, false);
+    const bool same = graph_unchanged(hg, g);
+    if (same && hg.exec) {
+        hg.updates = 0;
+        HIP_OK(hipGraphLaunch(hg.exec, c->stream));
+        return GGML_STATUS_SUCCESS;
+    }
+    if (hg.exec && ++hg.updates >= graph_max_updates() && graph_max_updates() > 0) {
+        logf("graph changed on %d calls in a row: no more hipGraph capture on %s\n", hg.updates, c->name.c_str());
+        hg.disabled = true;
+        HIP_OK(hipGraphExecDestroy(hg.exec));
+        hg.exec = nullptr;
+        return run_nodes(c, g, false);
+    }
+    HIP_OK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed));
+    const enum ggml_status st = run_nodes(c, g, true);
+    hipGraph_t graph = nullptr;
+    const hipError_t ec = hipStreamEndCapture(c->stream, &graph);
+    if (st != GGML_STATUS_SUCCESS || ec != hipSuccess || graph == nullptr) {
+        // a launch that cannot be captured yet (first use of a scratch size): run eagerly once
+        (void)hipGetLastError();
+        if (graph) (void)hipGraphDestroy(graph);
+        hg.props.clear();
+        return run_nodes(c, g, false);
+    }
+    if (hg.exec) {
+        hipGraphNode_t err_node = nullptr;
+        hipGraphExecUpdateResult res;
+        if (hipGraphExecUpdate(hg.exec, graph, &err_node, &res) != hipSuccess || res != hipGraphExecUpdateSuccess) {
+            (void)hipGetLastError();
+            HIP_OK(hipGraphExecDestroy(hg.exec));
+            hg.exec = nullptr;
+        }
+    }
+    if (!hg.exec) HIP_OK(hipGraphInstantiate(&hg.exec, graph, nullptr, nullptr, 0));
+    HIP_OK(hipGraphDestroy(graph));
+    HIP_OK(hipGraphLaunch(hg.exec, c->stream));
     return GGML_STATUS_SUCCESS;
 }
 

@@ -71,10 +71,12 @@ hipError_t fused_nc_attn(const MmArgs &a, int nc, int grid_z, hipStream_t st) {
     }
 }
 
-// lanes per row of a fused mat-vec: as mmvq_pick_lpr, but short matrices take 64 lanes (8 rows
-// per workgroup instead of 32) so that they spread over more CUs
+// lanes per row of a fused mat-vec: as mmvq_pick_lpr, but short matrices (N <= 1024, e.g. GPT-2
+// 117M's 768-row projections) take 64 lanes (8 rows per workgroup instead of 32) so that they
+// spread over 4x the CUs: 4.9 -> 4.0-4.4 us per launch in the drop-in decode (scripts/
+// prof_plugin_shapes.sh), ~2% on the whole token
 static int fused_lpr(const MmArgs &a) {
-    static const int maxn = getenv("GGML_MI355X_FUSED_LPR64_MAXN") ? atoi(getenv("GGML_MI355X_FUSED_LPR64_MAXN")) : 0;
+    static const int maxn = getenv("GGML_MI355X_FUSED_LPR64_MAXN") ? atoi(getenv("GGML_MI355X_FUSED_LPR64_MAXN")) : 1024;
     return a.N <= maxn ? 64 : mmvq_pick_lpr(a.K);
 }
 
