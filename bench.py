@@ -311,7 +311,9 @@ def gpt2_leg(torch, world: int, rank: int, n_seq: int, ticks: int, warm: int) ->
 
     def sync():
         if world > 1:
-            dist.barrier()
+            # wait on the host: an RCCL barrier would leave a spinning kernel on the other GPUs
+            # while rank 0's scheduler run uses them
+            dist.barrier(group=cpu_group)
         torch.cuda.synchronize()
 
     # warm-up fills the ring (world - 1 ticks) and captures every context's hipGraph; the
@@ -344,10 +346,12 @@ def gpt2_leg(torch, world: int, rank: int, n_seq: int, ticks: int, warm: int) ->
     return out
 
 
-def sched_plugin_gpt2(threads: int, tokens: int = 64) -> dict | None:
+def sched_plugin_gpt2(threads: int, tokens: int = 64, devices: int = 1) -> dict | None:
     """the drop-in path: the reference's own ggml_backend_sched GPT-2 graph (oracle/_ref/gpt2_ref,
     restating examples/gpt-2/main-sched.cpp) with our plugin loaded as its GPU backend, on the same
-    synthetic 117M Q4_0 checkpoint; decode ms/token over `tokens` positions (1 GPU)"""
+    synthetic 117M Q4_0 checkpoint; decode ms/token over `tokens` positions. devices > 1: the
+    scheduler splits the layers over that many plugin devices (its pipeline form, hand-offs by
+    our cross-device cpy_tensor_async); run by rank 0 while the other ranks wait"""
     exe = os.path.join(ROOT, "oracle", "_ref", "gpt2_ref")
     if not os.path.exists(exe):
         return None
@@ -359,8 +363,8 @@ def sched_plugin_gpt2(threads: int, tokens: int = 64) -> dict | None:
     path = os.path.join(tempfile.gettempdir(), f"bench_gpt2_sched_{os.getpid()}.bin")
     gpt2_synth.write_model(path, gpt2_synth.GPT2_117M, qref.Q4_0, 1234)
     try:
-        r = subprocess.run([exe, path, "--tokens", "40", "--threads", str(threads), "--plugin", M.LIB_PATH, "--devices", "1",
-                            "--time-tokens", str(tokens)], capture_output=True, text=True, timeout=300)
+        r = subprocess.run([exe, path, "--tokens", "40", "--threads", str(threads), "--plugin", M.LIB_PATH, "--devices",
+                            str(devices), "--time-tokens", str(tokens)], capture_output=True, text=True, timeout=300)
         if r.returncode != 0:
             return None
         j = json.loads(r.stdout.strip().splitlines()[-1])
@@ -369,8 +373,9 @@ def sched_plugin_gpt2(threads: int, tokens: int = 64) -> dict | None:
     finally:
         os.remove(path)
     return {"value": round(j["tokens_per_s"], 2), "unit": "tokens/s", "ms_per_token": round(j["ms_per_token"], 3),
-            "path": "reference ggml_backend_sched + libggml-hip-mi355x.so (weights, KV and supported ops on MI355X, "
-                    f"the rest on ggml-cpu with {threads} threads)",
+            "devices": devices, "splits": j.get("splits"),
+            "path": f"reference ggml_backend_sched + libggml-hip-mi355x.so on {devices} device(s) (weights, KV and "
+                    f"supported ops on MI355X, the rest on ggml-cpu with {threads} threads)",
             "sample": f"GPT-2 117M Q4_0 (synthetic), 1 sequence, {tokens} decode positions after a 40-token prompt"}
 
 
@@ -508,8 +513,10 @@ def main() -> None:
         dry_run(args, world, rank)
         return
     torch.cuda.set_device(local)
+    cpu_group = None
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        cpu_group = dist.new_group(backend="gloo")
     if local == 0:
         M.build()                      # one rank per node compiles (if stale); the others wait
     if world > 1:
@@ -600,7 +607,12 @@ def main() -> None:
             gpt2["single_stream_tokens_per_s"] = round(1e3 / r1["latency_ms_per_token"], 1)
         if cpu is not None:
             cpu["gpt2"] = cpu_gpt2_example_baseline(cpu["cores"]) or cpu_gpt2_baseline(cpu["cores"])
-            gpt2["reference_scheduler_with_plugin"] = sched_plugin_gpt2(cpu["cores"])
+        if rank == 0:
+            # configs[4]'s scheduler form: the reference's scheduler over all `world` devices
+            gpt2["reference_scheduler_with_plugin"] = sched_plugin_gpt2(cpu["cores"] if cpu else cpu_threads(),
+                                                                        devices=world)
+        if world > 1:
+            dist.barrier()
 
     if rank == 0:
         line = {

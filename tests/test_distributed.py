@@ -66,14 +66,16 @@ def _bench_json(args, env=None):
     return r.returncode, (json.loads(line[-1]) if line else None), r.stderr
 
 
-def test_bench_gpus_2_starts_two_ranks():
-    """`bench.py --gpus 2` with no launcher starts its own torch.distributed.run child with two
-    ranks (gloo dry run: rank plumbing only) and reports n_gpus = 2 from the slowest rank"""
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_gpus_n_starts_n_ranks(n):
+    """`bench.py --gpus N` with no launcher starts its own torch.distributed.run child with N
+    ranks (gloo dry run: rank plumbing only) and reports n_gpus = N from the slowest rank;
+    N = 8 is the driver's scaling run"""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    rc, line, err = _bench_json(["--gpus", "2", "--dry-run"], env)
+    rc, line, err = _bench_json(["--gpus", str(n), "--dry-run"], env)
     assert rc == 0, err[-2000:]
-    assert line["n_gpus"] == 2 and line["ranks_seen"] == 2
-    assert line["ms_per_step"] == pytest.approx(20.0)    # max over ranks (rank 1: 20 ms)
+    assert line["n_gpus"] == n and line["ranks_seen"] == n
+    assert line["ms_per_step"] == pytest.approx(10.0 * n)    # max over ranks (rank n-1: 10 n ms)
 
 
 def test_bench_rejects_rank_count_mismatch():

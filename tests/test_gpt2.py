@@ -190,14 +190,17 @@ def test_pipeline_rejects_unsupported_micro_batching(world, n_micro):
         G.Pipeline(0, world, n_micro, 8, "cpu")
 
 
-@pytest.mark.parametrize("world,n_micro", [(2, 2), (3, 3), (4, 4)])
+@pytest.mark.parametrize("world,n_micro", [(2, 2), (3, 3), (4, 4), (8, 8)])
 def test_pipeline_ring_gloo(world, n_micro):
-    """ring protocol on CPU/gloo: every micro-batch's token advances by sum(r+1) per lap"""
+    """ring protocol on CPU/gloo: every micro-batch's token advances by sum(r+1) per lap
+    (world 8 = the driver's 8-GPU scaling run)"""
     import multiprocessing as mp
-    import random
+    import socket
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = random.randint(20000, 40000)
+    with socket.socket() as s:   # a port the OS just handed out, not a random guess
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
     n_ticks = 4 * world + 3
     ps = [ctx.Process(target=_ring_worker, args=(r, world, port, n_micro, n_ticks, q)) for r in range(world)]
     for p in ps:
