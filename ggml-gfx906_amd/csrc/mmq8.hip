@@ -56,6 +56,11 @@ constexpr int Q8_TOK = 64;                     // tokens per activation image
 // TR = weight rows per workgroup (128, or 64 for two workgroups per CU), 4 TR threads
 constexpr uint32_t Q8_MAGIC_I = 0x4B400000u;   // f32 bits of 12582912 = 1.5 * 2^23
 constexpr float Q8_MAGIC_F = 12582912.0f;
+// measurement builds only (scripts/mmq8_exp.sh): 1 no scale epilogue (Q8_0 / Q4_0), 2 no weight
+// decode + store, 4 no weight loads, 8 no MFMA phase, 16 no activation DMA. Results are wrong.
+#ifndef MMQ8_EXP
+#define MMQ8_EXP 0
+#endif
 
 // ---- activation image of one (token tile, super-block): the LDS bytes, 1-KiB pieces ----
 //   codes  [blk 8][h 2][tok 64][16 B]            (Q6_K: [blk 8][h 2][hl 2][tok 64][8 B])
@@ -73,7 +78,7 @@ template <int TR> constexpr int wi_bytes() { return 288 * TR; }
 // the XOR pattern is chosen per staging map so that the 16 lanes of a staging write, which hold
 // different pieces of few rows, land on 16 distinct 16-B slots as well.
 template <int T> __device__ __forceinline__ int swz16(int blk, int h) {
-    return q8_has_min<T>() ? (4 * h + 8 * ((blk >> 1) & 1)) : ((2 * blk + h) & 15);
+    return q8_has_min<T>() ? (4 * h + 8 * ((blk >> 1) & 1)) : (blk + 8 * h);
 }
 template <int T, int TR> __device__ __forceinline__ uint32_t wslot16(int blk, int h, int row) {
     return (uint32_t)(blk * 32 * TR + h * 16 * TR + ((row ^ swz16<T>(blk, h)) << 4));
@@ -265,7 +270,7 @@ template <> struct WStage8<T_Q4_0> {
 template <int T> struct WStageK8 {
     static constexpr bool Q5 = T == T_Q5_K;
     static constexpr uint32_t QS = Q5 ? 48 : 16;
-    static constexpr int VMEM = Q5 ? 4 : 3;   // the header load runs on one lane in four, in every wave
+    static constexpr int VMEM = Q5 ? 4 : 3;
     u32x4v c[2], qh, hd;
     template <int TR> __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, const RowTile &R, int tid) {
         const int q = tid & 3;
@@ -273,7 +278,7 @@ template <int T> struct WStageK8 {
         c[0] = bl128(rs, rb + QS + 16u * q);
         c[1] = bl128(rs, rb + QS + 16u * (q + 4));
         if constexpr (Q5) qh = bl128(rs, rb + 16 + 16u * (q & 1));
-        if (q == 0) hd = bl128(rs, rb);
+        hd = bl128(rs, rb);   // every lane (one line per row): no load under a branch
     }
     template <int TR> __device__ __forceinline__ void store(uint8_t *W, const RowTile &, int tid) const {
         const int q = tid & 3, row = tid >> 2, h = q & 1;
@@ -326,7 +331,7 @@ template <> struct WStage8<T_Q6_K> {
             w[p][0] = a0[0]; w[p][1] = a0[1]; w[p][2] = a0[2]; w[p][3] = a0[3];
             w[p][4] = bl32(rs, o4 + 16);
         }
-        if (q == 0) {
+        {   // scales + d, every lane (no load under a branch)
             const uint32_t o4 = (rb + 192) & ~3u;
             const u32x4v a0 = bl128(rs, o4);
             s[0] = a0[0]; s[1] = a0[1]; s[2] = a0[2]; s[3] = a0[3];
@@ -393,7 +398,19 @@ __device__ __forceinline__ void q8_sb_compute(const uint8_t *W, const uint8_t *X
         i32x16 magic;
 #pragma unroll
         for (int i = 0; i < 16; ++i) magic[i] = (int)Q8_MAGIC_I;
+        // the magic constant's share, -12582912 * sum(d_w), starts the sums (folded into the first
+        // fma of every output instead of a subtraction at the end)
+        // (NG = 2 reads the meta again per group rather than holding 16 more registers)
         float dsum0 = 0.f, dsum1 = 0.f;
+#pragma unroll
+        for (int g = g0; g < g0 + NG; ++g) {
+            const u32x4v m0 = ld128(W + wi_meta<TR>() + g * 16 * TR + row0 * 16);
+            const u32x4v m1 = ld128(W + wi_meta<TR>() + g * 16 * TR + row1 * 16);
+            dsum0 += (uf(m0[0]) + uf(m0[1])) + (uf(m0[2]) + uf(m0[3]));
+            dsum1 += (uf(m1[0]) + uf(m1[1])) + (uf(m1[2]) + uf(m1[3]));
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { p0[i] = -Q8_MAGIC_F * dsum0; p1[i] = -Q8_MAGIC_F * dsum1; }
 #pragma unroll
         for (int g = g0; g < g0 + NG; ++g) {
             const u32x4v m0 = ld128(W + wi_meta<TR>() + g * 16 * TR + row0 * 16);
@@ -407,6 +424,7 @@ __device__ __forceinline__ void q8_sb_compute(const uint8_t *W, const uint8_t *X
                 R1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i4(A), as_i4(B1), magic, 0, 0, 0);
             };
             auto consume = [&](int bi, const i32x16 &R0, const i32x16 &R1) {
+                if constexpr (MMQ8_EXP & 1) { asm volatile("" ::"v"(R0), "v"(R1)); return; }
                 const float d0 = uf(m0[bi]), d1 = uf(m1[bi]);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
@@ -427,12 +445,7 @@ __device__ __forceinline__ void q8_sb_compute(const uint8_t *W, const uint8_t *X
             consume(2, Ra0, Ra1);
             __builtin_amdgcn_sched_barrier(0);
             consume(3, Rb0, Rb1);
-            dsum0 += (uf(m0[0]) + uf(m0[1])) + (uf(m0[2]) + uf(m0[3]));
-            dsum1 += (uf(m1[0]) + uf(m1[1])) + (uf(m1[2]) + uf(m1[3]));
         }
-        const float c0 = Q8_MAGIC_F * dsum0, c1 = Q8_MAGIC_F * dsum1;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) { p0[i] -= c0; p1[i] -= c1; }
     } else {   // K-quants: integer sub-block (or 16-group) scales, exact int32 sums
         i32x16 pi0, pi1;
 #pragma unroll
@@ -526,11 +539,10 @@ __device__ __forceinline__ void q8_sb_compute(const uint8_t *W, const uint8_t *X
             }
         }
     }
-    const float *XD = reinterpret_cast<const float *>(X + XI_DX);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const float4 dx = *reinterpret_cast<const float4 *>(XD + 32 * tg + 8 * q + 4 * hl);
-        const float dv[4] = {dx.x, dx.y, dx.z, dx.w};
+        const u32x4v dx = ld128(X + XI_DX + 4 * (32 * tg + 8 * q + 4 * hl));
+        const float dv[4] = {uf(dx[0]), uf(dx[1]), uf(dx[2]), uf(dx[3])};
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             acc0[4 * q + c] = __builtin_fmaf(p0[4 * q + c], dv[c], acc0[4 * q + c]);
@@ -539,12 +551,31 @@ __device__ __forceinline__ void q8_sb_compute(const uint8_t *W, const uint8_t *X
     }
 }
 
-// copy one activation image (XB bytes, whole KiB pieces) into LDS: wave w takes pieces w, w+NW, ..
+// 4 B per lane from the buffer into LDS at lds_dst + 4 * lane (a 256-B piece per wave)
+__device__ __forceinline__ void q8_dma4(__amdgpu_buffer_rsrc_t r, uint8_t *lds_dst, uint32_t voff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds_dst, 4, voff, 0, 0, 0);
+}
+
+// copy one activation image into LDS with the same instruction count in every wave (the
+// counted vmcnt waits below rely on it): the 16 KiB of codes as 1-KiB pieces w, w+NW, ..; the
+// 256-B dx row by every wave (identical bytes to the same place); the 2-KiB bsums (Q4_K / Q5_K)
+// as 256-B shares w, w+NW, ..
+template <int T, int NW> constexpr int q8_x_vmem() { return 16 / NW + 1 + (q8_has_min<T>() ? 8 / NW : 0); }
 template <int T, int NW>
 __device__ __forceinline__ void q8_x_dma(__amdgpu_buffer_rsrc_t xr, uint32_t img_off, uint8_t *X, int wave, int lane) {
-    constexpr int NP = ximg_bytes<T>() / 1024;
 #pragma unroll
-    for (int p = wave; p < NP; p += NW) q8_dma16(xr, X + p * 1024, img_off + p * 1024 + lane * 16);
+    for (int p = 0; p < 16 / NW; ++p) {
+        const int pc = wave + p * NW;
+        q8_dma16(xr, X + pc * 1024, img_off + pc * 1024 + lane * 16);
+    }
+    q8_dma4(xr, X + XI_DX, img_off + XI_DX + lane * 4);
+    if constexpr (q8_has_min<T>()) {
+#pragma unroll
+        for (int s = 0; s < 8 / NW; ++s) {
+            const int sh = wave + s * NW;
+            q8_dma4(xr, X + XI_BS + sh * 256, img_off + XI_BS + sh * 256 + lane * 4);
+        }
+    }
 }
 
 // grid.x = n_rt * ksplit * n_tt (token tiles fastest; XCD-remapped when a multiple of 8),
@@ -585,68 +616,63 @@ __global__ __launch_bounds__(4 * TR) void mmq8_kernel(const MmArgs a, const uint
     const __amdgpu_buffer_rsrc_t xr =
         __builtin_amdgcn_make_buffer_rsrc((void *)xbase, 0, (uint32_t)(NI * n_sb * XB), Q8_RSRC_W3);
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar) roles
     // wave roles: rg = 64-row group, tg = 32-token group, kg = K-group (TT = 64)
     constexpr int NRG = TR / 64, NTG = TT / 32, NKG = NW / (NRG * NTG);
     static_assert(NKG == (TT == 64 ? 2 : 1), "wave layout");
     const int rg = wave % NRG, tg = (wave / NRG) % NTG, kg = wave / (NRG * NTG);
     constexpr uint32_t SBB = (uint32_t)QT<T>::bytes * (Q8_QK / QT<T>::blck);   // bytes of one row's super-block
-    constexpr int NP_MIN = NI * (XB / 1024) / NW;  // fewest activation pieces one wave copies per stage
+    constexpr int NXV = NI * q8_x_vmem<T, NW>();   // vector-memory instructions of one activation stage
     auto rowtile = [&](int sb) { return RowTile{rt * TR, a.N, (uint32_t)a.nb01, (uint32_t)sb * SBB}; };
 
     f32x16 acc0, acc1;
 #pragma unroll
     for (int i = 0; i < 16; ++i) { acc0[i] = 0.f; acc1[i] = 0.f; }
 
-    // a.diag (GGML_MI355X_DIAG, measurements only): bit0 skips the activation DMA, bit1 the
-    // weight loads / decode, bit2 the MFMA compute
-    const int diag = a.diag;
-    auto x_issue = [&](int sb) {
-        if (diag & 1) return;
-        uint8_t *dst = Xs + ((sb - sb0) % N_XS) * NI * XB;
+    // Every load below is issued unconditionally (past the last super-block the source is the
+    // last one again and the destination a stage nobody reads any more): a load under a branch
+    // makes the compiler's in-order vmcnt bookkeeping fall back to draining everything.
+    auto x_issue = [&](int it_dst, int sb) {   // activation images of sb into ring slot it_dst
+        uint8_t *dst = Xs + (it_dst % N_XS) * NI * XB;
 #pragma unroll
         for (int i = 0; i < NI; ++i) q8_x_dma<T, NW>(xr, (uint32_t)((i * n_sb + sb) * XB), dst + i * XB, wave, lane);
     };
+    const int n_steps = sb1 - sb0;
+    if (n_steps <= 0) return;   // (uniform: a whole workgroup with no k range)
+    auto sbc = [&](int it) { return sb0 + min(it, n_steps - 1); };
     WStage8<T> wa, wb;
-    if (sb0 < sb1) {
 #pragma unroll
-        for (int d = 0; d < DX; ++d)
-            if (sb0 + d < sb1) x_issue(sb0 + d);
-        if (!(diag & 2)) wa.template load<TR>(wr, rowtile(sb0), tid);
-        if (sb0 + 1 < sb1 && !(diag & 2)) wb.template load<TR>(wr, rowtile(sb0 + 1), tid);
-        if (!(diag & 2)) wa.template store<TR>(lds, rowtile(sb0), tid);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        lds_barrier();
-    }
-    // one super-block: X(sb+DX) DMA and W(sb+2) loads into `ld` (the set that held sb), MFMAs of
-    // sb, decode of W(sb+1) from `st` into its stage, wait for X(sb+1), one barrier
-    auto step = [&](int sb, WStage8<T> &ld, WStage8<T> &st) {
-        const int it = sb - sb0;
-        const bool xmore = sb + DX < sb1, wmore = sb + 2 < sb1;
-        if (xmore) x_issue(sb + DX);
-        if (wmore && !(diag & 2)) ld.template load<TR>(wr, rowtile(sb + 2), tid);
-        if (!(diag & 4)) {
-            const uint8_t *Xc = Xs + (it % N_XS) * NI * XB;
-            if constexpr (TT == 64)
-                q8_sb_compute<T, 1, TR>(lds + (it & 1) * WB, Xc, kg, rg, tg, lane, acc0, acc1);
-            else
-                q8_sb_compute<T, 2, TR>(lds + (it & 1) * WB, Xc + (tg >> 1) * XB, 0, rg, tg & 1, lane, acc0, acc1);
-        }
-        if (sb + 1 < sb1 && !(diag & 2)) st.template store<TR>(lds + ((it + 1) & 1) * WB, rowtile(sb + 1), tid);
-        // X(sb+1) must have landed: the only younger memory operations are this step's W(sb+2)
-        // loads and (DX = 2) this step's X(sb+2) pieces
-        if (wmore && (DX == 1 || xmore)) {
-            if constexpr (DX == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WStage8<T>::VMEM + NP_MIN) : "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WStage8<T>::VMEM) : "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+    for (int d = 0; d < DX; ++d) x_issue(d, sbc(d));
+    wa.template load<TR>(wr, rowtile(sbc(0)), tid);
+    wb.template load<TR>(wr, rowtile(sbc(1)), tid);
+    wa.template store<TR>(lds, rowtile(sbc(0)), tid);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    // step it: X(it+DX) DMA and W(it+2) loads into `ld` (the set that held it), MFMAs of it,
+    // decode of W(it+1) from `st` into its stage, wait for X(it+1), one barrier
+    auto step = [&](int it, WStage8<T> &ld, WStage8<T> &st) {
+        if constexpr (!(MMQ8_EXP & 16)) x_issue(it + DX, sbc(it + DX));
+        if constexpr (!(MMQ8_EXP & 4)) ld.template load<TR>(wr, rowtile(sbc(it + 2)), tid);
+        const uint8_t *Xc = Xs + (it % N_XS) * NI * XB;
+        if constexpr (MMQ8_EXP & 8) {
+        } else if constexpr (TT == 64)
+            q8_sb_compute<T, 1, TR>(lds + (it & 1) * WB, Xc, kg, rg, tg, lane, acc0, acc1);
+        else
+            q8_sb_compute<T, 2, TR>(lds + (it & 1) * WB, Xc + (tg >> 1) * XB, 0, rg, tg & 1, lane, acc0, acc1);
+        if constexpr (!(MMQ8_EXP & 2)) st.template store<TR>(lds + ((it + 1) & 1) * WB, rowtile(sbc(it + 1)), tid);
+        // X(it+1) must have landed: younger than it are this step's W(it+2) loads and (DX = 2)
+        // this step's X(it+2) pieces
+        if constexpr (DX == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WStage8<T>::VMEM + NXV) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WStage8<T>::VMEM) : "memory");
         lds_barrier();
     };
-    for (int sb = sb0; sb < sb1; sb += 2) {
-        step(sb, wa, wb);
-        if (sb + 1 < sb1) step(sb + 1, wb, wa);
+    for (int it = 0; it < n_steps; it += 2) {
+        step(it, wa, wb);
+        if (it + 1 < n_steps) step(it + 1, wb, wa);
     }
+    // the clamped prefetches of the last steps land before the workgroup can leave
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     // K-group reduction through LDS (the stages are free after the loop's last barrier)
     if constexpr (NKG == 2) {
