@@ -402,6 +402,14 @@ enum ggml_status split_buf_init_tensor(ggml_backend_buffer_t b, struct ggml_tens
         fprintf(stderr, "[ggml-mi355x] split buffers hold whole contiguous tensors only (%s)\n", t->name);
         return GGML_STATUS_FAILED;
     }
+    // only the quantized MUL_MAT weights this backend runs row-split; an F16 / F32 matrix placed
+    // here could be run by no backend (the CPU one cannot read split shards), so refuse it now
+    // rather than fail late in the scheduler (the reference's split buffer also serves F16/F32)
+    if (!is_hot_quant(t->type)) {
+        fprintf(stderr, "[ggml-mi355x] split buffers hold Q4_0/Q8_0/Q4_K/Q5_K/Q6_K weights only (%s has type %d)\n", t->name,
+                (int)t->type);
+        return GGML_STATUS_FAILED;
+    }
     const auto &bc = *static_cast<SplitBuftCtx *>(b->buft->context);
     auto *e = new SplitExtra();
     static_cast<SplitBufCtx *>(b->context)->extras.push_back(e);

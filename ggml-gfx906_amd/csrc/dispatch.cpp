@@ -89,9 +89,12 @@ bool is_hot_quant(int t) { return type_blck(t) != 0; }
 // more rows per workgroup amortize that; fewer rows give more workgroups. A single 4096-row
 // matrix needs all 512 workgroups of RPW=1 to cover 256 CUs twice; batched / taller problems
 // (rows x batch) switch to 2 and 4 rows per wave.
-static int pick_rpw(int64_t rows_total) {
+// Q6_K keeps one row per wave: its two-row kernel needs 133 VGPRs, which leaves one 8-wave
+// workgroup per CU instead of two (Q6_K 4096x11008 x24: 169 vs 178 us, profiles/r03_q6k_rpw.txt).
+static int pick_rpw(int type, int64_t rows_total) {
     static const int force = getenv("GGML_MI355X_RPW") ? atoi(getenv("GGML_MI355X_RPW")) : 0;
     if (force > 0) return force;
+    if (type == T_Q6_K) return 1;
     return rows_total >= 16384 ? 2 : 1;
 }
 
@@ -150,7 +153,7 @@ static MmArgs base_args(const TensorView &a, const TensorView &b, const TensorVi
 
 // mat-vec over columns [c0, c0 + ncols) in groups of at most 8
 static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st) {
-    const int rpw = pick_rpw((int64_t)m.N * m.ne12 * m.ne13);
+    const int rpw = pick_rpw(type, (int64_t)m.N * m.ne12 * m.ne13);
     while (ncols > 0) {
         int nc = mmvq_bigk(m.K) ? 1 : std::min(ncols, 8);
         while (nc > 1 && (!mmvq_has_nc(nc) || mmvq_lds_bytes(m.K, nc) > LDS_LIMIT || m.K > mmvq_max_k_for_nc(nc))) --nc;

@@ -110,6 +110,13 @@ struct ggml_mi355x_gpt2_model {
     Tensor wte, wpe, ln_f_g, ln_f_b, lm_head;
     std::vector<Layer> layers;                 // layers[l - l0]
     std::map<std::string, Tensor *> by_name;   // legacy names of the tensors this stage owns
+    // 32-block types, two-launch layer: per layer, head-major c_proj and slice-major MLP
+    // projection copies (gpt2_block_repack). One set per model, shared by its contexts;
+    // (re)made from the weights by every ctx_init, so a context created after weights were
+    // written through ggml_mi355x_gpt2_model_tensor sees them (the buffer never moves, so
+    // captured decode graphs of earlier contexts stay valid and see the same bytes).
+    uint8_t *rep = nullptr;
+    std::vector<const uint8_t *> rep_o, rep_mp;
 };
 
 struct ggml_mi355x_gpt2_ctx {
@@ -124,12 +131,8 @@ struct ggml_mi355x_gpt2_ctx {
     int32_t *amax_i = nullptr;
     // two-launch layer (gpt2_block.hip): materialized residuals after attention / after the MLP
     // and the K-split partial slabs [split][seq][n_embd] of c_proj (per head) and the MLP proj
-    bool block = false;
+    bool block = false, rep = false;           // rep: the layers read the model's repacked copies
     float *xr = nullptr, *xm = nullptr, *p_attn = nullptr, *p_mlp = nullptr;
-    // 32-block types: per layer, head-major c_proj and slice-major MLP projection copies
-    // (gpt2_block_repack), made from the model's weights when the context is created
-    uint8_t *rep = nullptr;
-    std::vector<const uint8_t *> rep_o, rep_mp;
     std::map<hipStream_t, hipGraphExec_t> graphs;
 };
 
@@ -211,17 +214,17 @@ int run_step(ggml_mi355x_gpt2_ctx *c, hipStream_t st) {
             float *kc = c->kc + (size_t)(l - m->l0) * cache_layer;
             float *vc = c->vc + (size_t)(l - m->l0) * cache_layer;
             auto f = [](const Tensor &t) { return reinterpret_cast<const float *>(t.data); };
-            const bool rp = c->rep != nullptr;
+            const bool rp = c->rep;
             rc = hip_status(gpt2_attn_block_launch(l - m->l0, m->wtype, base, bias, parts, np, c->xr, f(L.ln1_g), f(L.ln1_b), 1e-5f, L.attn_w.data,
                                                    row_bytes(m->wtype, E), f(L.attn_b), kc, vc, c->pos, kq_scale, hp.n_ctx,
-                                                   rp ? c->rep_o[l - m->l0] : L.proj_w.data, row_bytes(m->wtype, E), c->p_attn, E,
+                                                   rp ? m->rep_o[l - m->l0] : L.proj_w.data, row_bytes(m->wtype, E), c->p_attn, E,
                                                    hp.n_head, c->n_seq, emb_fused && l == 0 ? m->wte.data : nullptr,
                                                    row_bytes(m->wtype, E), reinterpret_cast<const float *>(m->wpe.data), c->tokens,
                                                    hp.n_vocab, st));
             if (rc) return rc;
             rc = hip_status(gpt2_mlp_block_launch(l - m->l0, m->wtype, c->xr, f(L.proj_b), c->p_attn, hp.n_head, c->xm, f(L.ln2_g), f(L.ln2_b),
                                                   1e-5f, L.fc_w.data, row_bytes(m->wtype, E), f(L.fc_b),
-                                                  rp ? c->rep_mp[l - m->l0] : L.mproj_w.data, row_bytes(m->wtype, 4 * E), c->p_mlp, E,
+                                                  rp ? m->rep_mp[l - m->l0] : L.mproj_w.data, row_bytes(m->wtype, 4 * E), c->p_mlp, E,
                                                   hp.n_head, c->n_seq, st));
             if (rc) return rc;
             base = c->xm;
@@ -448,8 +451,39 @@ int64_t ggml_mi355x_gpt2_model_bytes(const ggml_mi355x_gpt2_model *m) { return m
 void ggml_mi355x_gpt2_model_free(ggml_mi355x_gpt2_model *m) {
     if (!m) return;
     if (m->arena) (void)hipFree(m->arena);
+    if (m->rep) (void)hipFree(m->rep);
     delete m;
 }
+
+}  // extern "C"
+
+namespace {
+// (re)make the model's repacked c_proj / MLP-projection copies from its current weights
+int model_repack(ggml_mi355x_gpt2_model *m) {
+    const size_t n_layers = m->l1 - m->l0;
+    size_t ob = 0, mb = 0;
+    (void)gpt2_block_repack(m->wtype, m->hp.n_embd, nullptr, nullptr, nullptr, nullptr, &ob, &mb, nullptr);
+    if (!m->rep) {
+        if (hipMalloc(&m->rep, (ob + mb) * n_layers) != hipSuccess) {
+            m->rep = nullptr;
+            return GGML_MI355X_ENOMEM;
+        }
+        for (size_t l = 0; l < n_layers; ++l) {
+            m->rep_o.push_back(m->rep + l * (ob + mb));
+            m->rep_mp.push_back(m->rep + l * (ob + mb) + ob);
+        }
+    }
+    for (size_t l = 0; l < n_layers; ++l) {
+        const Layer &L = m->layers[l];
+        if (gpt2_block_repack(m->wtype, m->hp.n_embd, L.proj_w.data, const_cast<uint8_t *>(m->rep_o[l]), L.mproj_w.data,
+                              const_cast<uint8_t *>(m->rep_mp[l]), nullptr, nullptr, nullptr) != hipSuccess)
+            return GGML_MI355X_EHIP;
+    }
+    return hipDeviceSynchronize() == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
+}
+}  // namespace
+
+extern "C" {
 
 int ggml_mi355x_gpt2_ctx_init(ggml_mi355x_gpt2_model *m, int32_t n_seq, ggml_mi355x_gpt2_ctx **out) {
     if (!m || !out || n_seq < 1 || n_seq > 64) return GGML_MI355X_EINVAL;
@@ -507,27 +541,11 @@ int ggml_mi355x_gpt2_ctx_init(ggml_mi355x_gpt2_model *m, int32_t n_seq, ggml_mi3
         return GGML_MI355X_EHIP;
     }
     if (block && gpt2_block_repacks(m->wtype)) {
-        size_t ob = 0, mb = 0;
-        (void)gpt2_block_repack(m->wtype, hp.n_embd, nullptr, nullptr, nullptr, nullptr, &ob, &mb, nullptr);
-        if (hipMalloc(&c->rep, (ob + mb) * n_layers) != hipSuccess) {
-            (void)hipFree(c->arena);
-            delete c;
-            return GGML_MI355X_ENOMEM;
-        }
-        for (size_t l = 0; l < n_layers; ++l) {
-            uint8_t *o = c->rep + l * (ob + mb), *mp = o + ob;
-            const Layer &L = m->layers[l];
-            if (gpt2_block_repack(m->wtype, hp.n_embd, L.proj_w.data, o, L.mproj_w.data, mp, nullptr, nullptr, nullptr) != hipSuccess) {
-                ggml_mi355x_gpt2_ctx_free(c);
-                return GGML_MI355X_EHIP;
-            }
-            c->rep_o.push_back(o);
-            c->rep_mp.push_back(mp);
-        }
-        if (hipDeviceSynchronize() != hipSuccess) {
+        if (int rc = model_repack(m)) {
             ggml_mi355x_gpt2_ctx_free(c);
-            return GGML_MI355X_EHIP;
+            return rc;
         }
+        c->rep = true;
     }
     *out = c;
     return GGML_MI355X_OK;
@@ -570,7 +588,6 @@ void ggml_mi355x_gpt2_ctx_free(ggml_mi355x_gpt2_ctx *c) {
     if (!c) return;
     for (auto &kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
     if (c->arena) (void)hipFree(c->arena);
-    if (c->rep) (void)hipFree(c->rep);
     delete c;
 }
 

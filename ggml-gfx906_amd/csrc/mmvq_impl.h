@@ -322,53 +322,55 @@ template <> struct Frag<T_Q5_K> {
 // positions 128h + 16p + 32k + [0,16) for k = 0..3, i.e. ql[64h+16p..], ql[64h+32+16p..],
 // qh[32h+16p..] and scales 8h + p + 2k; sum (q-32)*x = sum q*x - 32 sum x per 16-run.
 template <> struct Frag<T_Q6_K> {
-    uint32_t L0[4], L1[4], QH[4], SC[2];
-    uint16_t dh;
-    int p;
+    // raw 4-byte-aligned windows, realigned in dot(): load() only issues loads, so the
+    // prefetched unit stays in flight until the dot product needs it
+    uint32_t R0[5], R1[5], RQ[5], RS[5];
+    uint32_t sh;
+    int p, h;
     // a super-block starts 2-byte aligned when sb is odd; 2-byte-misaligned 16-B loads stream
     // ~16 % slower on MI355X (scripts/hbm_probe.hip), 4-byte aligned ones at full rate, so
-    // every piece is loaded from its 4-byte-aligned floor and funnel-shifted into place.
-    __device__ static inline void ld16_a4(const uint8_t *p, uint32_t *o) {
-        const uintptr_t ip = reinterpret_cast<uintptr_t>(p);
-        const uint8_t *pa = reinterpret_cast<const uint8_t *>(ip & ~(uintptr_t)3);
-        const uint32_t sh = (uint32_t)(ip & 3);
+    // every piece is loaded from its 4-byte-aligned floor (all pieces of a block share the
+    // block's alignment) and funnel-shifted into place.
+    // (pointer arithmetic, not an integer round trip: a pointer rebuilt from an integer loses
+    // its global address space, every load becomes a flat load, and a flat load's wait drains
+    // the whole prefetch stream)
+    __device__ static inline void ld20(const uint8_t *pa, uint32_t *o) {
         const uint4 w = *reinterpret_cast<const uint4 *>(pa);    // 4-B aligned dwordx4
-        const uint32_t w4 = *reinterpret_cast<const uint32_t *>(pa + 16);
-        o[0] = __builtin_amdgcn_alignbyte(w.y, w.x, sh);
-        o[1] = __builtin_amdgcn_alignbyte(w.z, w.y, sh);
-        o[2] = __builtin_amdgcn_alignbyte(w.w, w.z, sh);
-        o[3] = __builtin_amdgcn_alignbyte(w4, w.w, sh);
+        o[0] = w.x; o[1] = w.y; o[2] = w.z; o[3] = w.w;
+        o[4] = *reinterpret_cast<const uint32_t *>(pa + 16);
+    }
+    __device__ static inline void al16(const uint32_t *w, uint32_t sh, uint32_t *o) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
     }
     template <bool RAG>
     __device__ inline void load(const uint8_t *row, int s, int) {
         const uint8_t *b = row + (size_t)(s >> 2) * 210;
-        const int h = (s >> 1) & 1;
+        h = (s >> 1) & 1;
         p = s & 1;
-        ld16_a4(b + 64 * h + 16 * p, L0);
-        ld16_a4(b + 64 * h + 32 + 16 * p, L1);
-        ld16_a4(b + 128 + 32 * h + 16 * p, QH);
-        {
-            const uintptr_t ip = reinterpret_cast<uintptr_t>(b + 192 + 8 * h);
-            const uint8_t *pa = reinterpret_cast<const uint8_t *>(ip & ~(uintptr_t)3);
-            const uint32_t sh = (uint32_t)(ip & 3);
-            const uint2 w = *reinterpret_cast<const uint2 *>(pa);
-            // third dword only matters when misaligned (then it ends at byte 209 of the block);
-            // aligned blocks re-read the second one, so the load is unconditional (no branch
-            // around a load, which would force a vmcnt(0) drain) and never passes the block end
-            const uint32_t w2 = *reinterpret_cast<const uint32_t *>(pa + (sh ? 8 : 4));
-            SC[0] = __builtin_amdgcn_alignbyte(w.y, w.x, sh);
-            SC[1] = __builtin_amdgcn_alignbyte(w2, w.y, sh);
-        }
-        dh = ld2(b + 208);
+        sh = (uint32_t)(reinterpret_cast<uintptr_t>(b) & 3);
+        const uint8_t *ba = b - sh;
+        ld20(ba + 64 * h + 16 * p, R0);
+        ld20(ba + 64 * h + 32 + 16 * p, R1);
+        ld20(ba + 128 + 32 * h + 16 * p, RQ);
+        // the 16 scale bytes and d (bytes 192..209) in one 20-B window: the last dword ends at
+        // byte 209 + (2 - sh), i.e. at most 2 bytes past the block, inside its dword
+        ld20(ba + 192, RS);
     }
     __device__ inline void zero() {
-        for (int i = 0; i < 4; ++i) L0[i] = L1[i] = QH[i] = 0;
-        SC[0] = SC[1] = 0;
-        dh = 0;
-        p = 0;
+        for (int i = 0; i < 5; ++i) R0[i] = R1[i] = RQ[i] = RS[i] = 0;
+        sh = 0;
+        p = h = 0;
     }
     // dx: d of the four 32-blocks 4h + k; sx: d*sum(q) of the four 16-runs
     __device__ inline float dot(const uint32_t X[16], const float *dx, const float *sx) const {
+        uint32_t L0[4], L1[4], QH[4], SC[2];
+        al16(R0, sh, L0);
+        al16(R1, sh, L1);
+        al16(RQ, sh, QH);
+        SC[0] = __builtin_amdgcn_alignbyte(h ? RS[3] : RS[1], h ? RS[2] : RS[0], sh);
+        SC[1] = __builtin_amdgcn_alignbyte(h ? RS[4] : RS[2], h ? RS[3] : RS[1], sh);
+        const uint16_t dh = (uint16_t)(RS[4] >> (8 * sh));   // d: block bytes 208..209
         int s[4] = {0, 0, 0, 0};
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -759,7 +761,11 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
         }
     }
     if (wstamp) wst[2] = __builtin_amdgcn_s_memrealtime();   // quantized, at the barrier
+#ifdef MMVQ_FENCE_BARRIER   // A/B measurement builds only (scripts/ab_singles.sh)
+    __syncthreads();
+#else
     lds_barrier();
+#endif
     if (stamp) a.stamps[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
 
     float acc[V];

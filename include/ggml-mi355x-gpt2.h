@@ -67,7 +67,11 @@ GGML_MI355X_API void ggml_mi355x_gpt2_model_free(ggml_mi355x_gpt2_model *model);
 
 /* A decode context: n_seq independent sequences (1..64) decoded together, with their KV cache
  * for this stage's layers ([layer][seq][n_ctx][n_embd] f32 K and V, the reference's
- * memory_k / memory_v, main-sched.cpp:384-420), positions and activation buffers. */
+ * memory_k / memory_v, main-sched.cpp:384-420), positions and activation buffers.
+ * For Q4_0 / Q8_0 stages on the two-launch layer, ctx_init also (re)makes the model's one shared
+ * set of head-/slice-major c_proj and MLP-projection copies from the current weights: weights
+ * written through ggml_mi355x_gpt2_model_tensor after a context exists reach decoding once a
+ * context is created after the write (every context of the model then reads the new copies). */
 GGML_MI355X_API int ggml_mi355x_gpt2_ctx_init(ggml_mi355x_gpt2_model *model, int32_t n_seq, ggml_mi355x_gpt2_ctx **out);
 
 /* Device buffers of the context:

@@ -104,6 +104,19 @@ int main(int argc, char **argv) {
         printf("%s %-5s K=%d N=%d M=%d roundtrip=%d supports_op=%d nmse=%.3e\n", ok ? "OK  " : "FAIL", ggml_type_name(cs.t), cs.K, cs.N,
                cs.M, rt, sup, nmse);
     }
+    // an F32 matrix is refused at allocation (init_tensor fails, ggml-alloc returns NULL), not
+    // accepted into shards that no backend could run
+    {
+        ggml_init_params pw = {ggml_tensor_overhead() * 2, nullptr, true};
+        ggml_context *cw = ggml_init(pw);
+        ggml_new_tensor_2d(cw, GGML_TYPE_F32, 256, 64);
+        ggml_backend_buffer_t wb = ggml_backend_alloc_ctx_tensors_from_buft(cw, sbt);
+        const bool refused = wb == nullptr;
+        if (wb) ggml_backend_buffer_free(wb);
+        ggml_free(cw);
+        fails += !refused;
+        printf("%s f32 weight in the split buffer refused=%d\n", refused ? "OK  " : "FAIL", refused);
+    }
     ggml_backend_free(gpu);
     ggml_backend_free(cpu);
     printf("%s\n", fails ? "SPLIT_CHECK_FAIL" : "SPLIT_CHECK_OK");
