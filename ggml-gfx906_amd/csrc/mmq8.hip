@@ -516,26 +516,32 @@ __device__ __forceinline__ void q8_sb_compute(const uint8_t *W, const uint8_t *X
 #pragma unroll
         for (int i = 0; i < 16; ++i) { p0[i] = dd0 * (float)pi0[i]; p1[i] = dd1 * (float)pi1[i]; }
         if constexpr (T == T_Q4_K || T == T_Q5_K) {
-            if (g0 == 0) {   // sum_j m_j * bsum_j over all 8 sub-blocks: k16-sum e pairs with m_(e>>1)
-                const f16x8 As = __builtin_bit_cast(f16x8, ld128(X + XI_BS + hl * 1024 + tok * 16));
-                const uint32_t mw0 = *reinterpret_cast<const uint32_t *>(W + wi_meta<TR>() + hl * 16 * TR + row0 * 16 + 12);
-                const uint32_t mw1 = *reinterpret_cast<const uint32_t *>(W + wi_meta<TR>() + hl * 16 * TR + row1 * 16 + 12);
-                f16x8 Bm0, Bm1;
+            // sum_j m_j * bsum_j over all 8 sub-blocks (k16-sum e pairs with m_(e>>1)) as one f16
+            // MFMA on exact integers per tile; the two K-groups take one tile each (the partials
+            // meet in the K-group reduction), a wave holding both groups (NG = 2) both tiles
+            const f16x8 As = __builtin_bit_cast(f16x8, ld128(X + XI_BS + hl * 1024 + tok * 16));
+            f32x16 zf;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    Bm0[e] = (_Float16)(float)((mw0 >> (8 * (e >> 1))) & 0xffu);
-                    Bm1[e] = (_Float16)(float)((mw1 >> (8 * (e >> 1))) & 0xffu);
+            for (int i = 0; i < 16; ++i) zf[i] = 0.f;
+            auto mins_of = [&](int row) {
+                const uint32_t mw = *reinterpret_cast<const uint32_t *>(W + wi_meta<TR>() + hl * 16 * TR + row * 16 + 12);
+                u32x4v bm;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t hb = __builtin_bit_cast(uint16_t, (_Float16)(float)((mw >> (8 * k)) & 0xffu));
+                    bm[k] = hb | (hb << 16);
                 }
-                f32x16 zf;
+                return __builtin_amdgcn_mfma_f32_32x32x16_f16(As, __builtin_bit_cast(f16x8, bm), zf, 0, 0, 0);
+            };
+            if (NG == 2 || g0 == 0) {
+                const f32x16 mins0 = mins_of(row0);
 #pragma unroll
-                for (int i = 0; i < 16; ++i) zf[i] = 0.f;
-                const f32x16 mins0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(As, Bm0, zf, 0, 0, 0);
-                const f32x16 mins1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(As, Bm1, zf, 0, 0, 0);
+                for (int i = 0; i < 16; ++i) p0[i] = __builtin_fmaf(-dm0, mins0[i], p0[i]);
+            }
+            if (NG == 2 || g0 != 0) {
+                const f32x16 mins1 = mins_of(row1);
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    p0[i] = __builtin_fmaf(-dm0, mins0[i], p0[i]);
-                    p1[i] = __builtin_fmaf(-dm1, mins1[i], p1[i]);
-                }
+                for (int i = 0; i < 16; ++i) p1[i] = __builtin_fmaf(-dm1, mins1[i], p1[i]);
             }
         }
     }
