@@ -778,6 +778,64 @@ bool identical(const struct ggml_tensor *a, const struct ggml_tensor *b) {
     return true;
 }
 
+int next_compute(const struct ggml_cgraph *g, int i, int n);
+bool is_plain_copy(const struct ggml_tensor *t);
+
+// f32 elements stored densely in row-major order (what a flat copy writes)
+bool f32_dense(const struct ggml_tensor *t) {
+    if (t->type != GGMLABI_TYPE_F32 || t->nb[0] != 4) return false;
+    int64_t expect = 4;
+    for (int d = 0; d < 4; ++d) {
+        if (t->ne[d] > 1 && (int64_t)t->nb[d] != expect) return false;
+        expect *= t->ne[d];
+    }
+    return true;
+}
+
+// the copies right after a fused run whose source is a row range of its output `out` (GPT-2's
+// K / V cache writes after the qkv mat-vec + bias, main-sched.cpp:648-655): at most two, only
+// view nodes between. The fused launch stores those rows to the copy destinations as well, and
+// the copy nodes are marked done in the plan. `last`: graph index of the run's last node.
+// Returns how many were taken.
+int absorb_copies(BackendCtx *c, const struct ggml_cgraph *g, int last, int n, const struct ggml_tensor *out,
+                  const struct ggml_tensor *x, MmArgs &a) {
+    int taken = 0, j = last, j_first = -1;
+#define NOFOLD(why)                                                                 \
+    {                                                                               \
+        logf("copy %s not folded into the mat-vec: %s\n", g->nodes[j]->name, why); \
+        break;                                                                      \
+    }
+    while (taken < 2) {
+        j = next_compute(g, j, n);
+        if (j >= n) break;
+        const struct ggml_tensor *cp = g->nodes[j];
+        const struct ggml_tensor *src = cp->src[0];
+        if (!is_plain_copy(cp) || !src) break;   // not a copy: nothing to fold (quiet)
+        if (c->plan.skip[j] || c->plan.attn.count(j)) NOFOLD("planned elsewhere");
+        if (src->view_src != out) NOFOLD("source is not a view of the mat-vec's output");
+        if (src->type != GGMLABI_TYPE_F32 || src->nb[0] != 4 || src->nb[1] != out->nb[1] || src->ne[1] != out->ne[1] ||
+            src->ne[2] != 1 || src->ne[3] != 1)
+            NOFOLD("source layout");
+        const int64_t off = (int64_t)((const uint8_t *)src->data - (const uint8_t *)out->data);
+        if (off < 0 || off % 4 != 0 || off / 4 + src->ne[0] > out->ne[0]) NOFOLD("source rows");
+        if (!f32_dense(cp) || ggml_base().nbytes(cp) != (size_t)(4 * src->ne[0] * src->ne[1])) NOFOLD("destination layout");
+        // the destination (the copy node's own data, a view of its src[1]) must not be read or
+        // written by the fused launch otherwise, nor overlap the other folded copy
+        if (!disjoint(cp, out) || !disjoint(cp, x)) NOFOLD("destination overlaps the mat-vec's input or output");
+        if (taken == 1 && !disjoint(cp, g->nodes[j_first])) NOFOLD("destinations overlap");
+        a.cp_dst[taken] = static_cast<float *>(cp->data);
+        a.cp_r0[taken] = (int)(off / 4);
+        a.cp_n[taken] = (int)src->ne[0];
+        a.cp_nb1[taken] = 4 * src->ne[0];
+        c->plan.skip[j] = 1;
+        if (taken == 0) j_first = j;
+        logf("copy %s folded into the mat-vec's epilogue\n", cp->name);
+        ++taken;
+    }
+#undef NOFOLD
+    return taken;
+}
+
 // nodes consumed by a fused mat-vec run at node i (0: no fusion); rc receives the launch status
 int fuse_matvec(BackendCtx *c, const struct ggml_cgraph *g, int i, int n, int &rc) {
     auto at = [&](int k) -> struct ggml_tensor * { return i + k < n ? g->nodes[i + k] : nullptr; };
@@ -874,6 +932,7 @@ int fuse_matvec(BackendCtx *c, const struct ggml_cgraph *g, int i, int n, int &r
         a.resid_nb1 = (int64_t)resid->nb[1];
     }
     a.fused = 1;
+    if (bias != nullptr && !(epi & EPI_ARGMAX)) absorb_copies(c, g, i + last, n, out, x, a);   // (last: offset from i)
     const hipError_t e = mmvq_fused_launch(w->type, a, mmvq_fused_pick_nc((int)M, (int)K), N >= 16384 ? 2 : 1, c->stream);
     rc = e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
     logf("fused %d nodes at %s (mat-vec %s, M=%d)\n", last + 1, t0->name, w->name, (int)M);

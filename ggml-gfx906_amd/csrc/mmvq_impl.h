@@ -829,6 +829,13 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
                             if (v > best_v || best_c < 0) { best_v = v; best_i = r0 + r; }   // rows ascend per lane
                             best_c = m;
                         }
+#pragma unroll
+                        for (int cpi = 0; cpi < 2; ++cpi) {   // copy-out (graph_compute's cache writes)
+                            const unsigned cr = (unsigned)(r0 + r - a.cp_r0[cpi]);
+                            if (a.cp_dst[cpi] != nullptr && cr < (unsigned)a.cp_n[cpi])
+                                reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(a.cp_dst[cpi]) +
+                                                          (int64_t)(blockIdx.z * NC + m) * a.cp_nb1[cpi])[cr] = v;
+                        }
                     }
                     *out = v;
                 }

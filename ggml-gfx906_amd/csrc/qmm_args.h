@@ -60,6 +60,12 @@ struct MmArgs {
     //     part[((col * n_head + h) * ATTN_SPLITS + i) * ATTN_PART_STRIDE + {0: m, 1: l, 4..67: o}]
     const float *attn_part;
     int n_head;
+    //   copy-out (graph_compute: the K / V cache writes that follow a fused qkv mat-vec,
+    //     main-sched.cpp:648-655): output rows [cp_r0[i], cp_r0[i] + cp_n[i]) of column m are
+    //     also stored to cp_dst[i] + m * cp_nb1[i] bytes + (row - cp_r0[i]) floats
+    float *cp_dst[2];
+    int cp_r0[2], cp_n[2];
+    int64_t cp_nb1[2];
     int fused;
     // diagnostics (GGML_MI355X_STAMPS): per-workgroup s_memrealtime stamps, or nullptr
     unsigned long long *stamps;

@@ -165,6 +165,8 @@ int main(int argc, char **argv) {
             in.bytes["b_fc"] = f32_bytes(F, -0.5f, 0.5f);
             in.bytes["w_mp"] = q_bytes(t, F, E);
             in.bytes["b_mp"] = f32_bytes(E, -0.5f, 0.5f);
+            in.bytes["memk"] = f32_bytes((size_t)2 * 32 * E, -1.f, 1.f);
+            in.bytes["memv"] = f32_bytes((size_t)2 * 32 * E, -1.f, 1.f);
             const std::string tag = std::string(ggml_type_name(t)) + " M=" + std::to_string(M);
 
             // layer-norm -> c_attn + bias (main-sched.cpp:603-637)
@@ -182,6 +184,25 @@ int main(int argc, char **argv) {
                 h = ggml_gelu(c, ggml_add(c, ggml_mul_mat(c, input(c, "w_fc", t, E, F), h), input(c, "b_fc", GGML_TYPE_F32, F)));
                 ggml_tensor *y = ggml_add(c, ggml_add(c, ggml_mul_mat(c, input(c, "w_mp", t, F, E), h), input(c, "b_mp", GGML_TYPE_F32, E)), x);
                 return std::vector<ggml_tensor *>{y};
+            }, in);
+
+            // c_attn + bias, then the K / V cache writes of the new token(s) (main-sched.cpp:620-655,
+            // layer 1 of 2 at n_past = 5): the plugin folds both copies into the mat-vec's epilogue
+            check("qkv_cache " + tag, [&](ggml_context *c, ggml_cgraph *gf) {
+                const int n_ctx = 32, il = 1, n_past = 5;
+                ggml_tensor *x = resident(input(c, "x", GGML_TYPE_F32, E, M));
+                ggml_tensor *memk = resident(input(c, "memk", GGML_TYPE_F32, 2 * n_ctx * E));
+                ggml_tensor *memv = resident(input(c, "memv", GGML_TYPE_F32, 2 * n_ctx * E));
+                // an unfused node first, so the fused run does not start at node 0
+                ggml_tensor *xs = resident(ggml_scale(c, x, 0.5f));
+                ggml_tensor *cur = ggml_add(c, ggml_mul_mat(c, input(c, "w_qkv", t, E, 3 * E), xs), input(c, "b_qkv", GGML_TYPE_F32, 3 * E));
+                ggml_tensor *Kcur = ggml_view_2d(c, cur, E, M, cur->nb[1], 1 * sizeof(float) * E);
+                ggml_tensor *Vcur = ggml_view_2d(c, cur, E, M, cur->nb[1], 2 * sizeof(float) * E);
+                ggml_tensor *k = ggml_view_1d(c, memk, M * E, (ggml_element_size(memk) * E) * (il * n_ctx + n_past));
+                ggml_tensor *v = ggml_view_1d(c, memv, M * E, (ggml_element_size(memv) * E) * (il * n_ctx + n_past));
+                ggml_build_forward_expand(gf, ggml_cpy(c, Kcur, k));
+                ggml_build_forward_expand(gf, ggml_cpy(c, Vcur, v));
+                return std::vector<ggml_tensor *>{cur, memk, memv};
             }, in);
 
             // final layer-norm -> lm_head without bias (main-sched.cpp:826-847)

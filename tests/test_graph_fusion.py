@@ -20,6 +20,9 @@ LIB = os.path.join(ROOT, "ggml-gfx906_amd", "libggml-hip-mi355x.so")
 pytestmark = pytest.mark.gpu
 
 
+folds = {}   # copies folded into a fused mat-vec, by case (filled by _run)
+
+
 def _run(fusion: bool, **extra):
     if not os.path.exists(BIN):
         pytest.skip("oracle/_ref/fusion_check not built")
@@ -28,6 +31,7 @@ def _run(fusion: bool, **extra):
     fails = [l for l in r.stdout.splitlines() if l.startswith("FAIL")]
     assert r.returncode == 0 and "FUSION_CHECK_OK" in r.stdout, (fails, r.stdout[-1500:], r.stderr[-1500:])
     fused, attn, pairs = {}, {}, {}
+    folds.clear()
     case = None
     for line in r.stderr.splitlines():
         if line.startswith("CASE "):
@@ -35,6 +39,9 @@ def _run(fusion: bool, **extra):
             fused[case] = []
             attn[case] = 0
             pairs[case] = 0
+            folds[case] = 0
+        if "folded into the mat-vec's epilogue" in line and case is not None:
+            folds[case] += 1
         m = re.search(r"fused (\d+) nodes", line)
         if m and case is not None:
             fused[case].append(int(m.group(1)))
@@ -55,6 +62,8 @@ def test_fused_chains_match_cpu_and_fuse(attn_kernel):
             assert fused[f"ln_matvec_bias {tag}"] == [5], tag
             assert fused[f"mlp {tag}"] == [6, 3], tag
             assert fused[f"ln_matvec {tag}"] == [4], tag
+            # c_attn + bias fuses and both cache writes ride in its epilogue (caches read back whole)
+            assert fused[f"qkv_cache {tag}"] == [2] and folds[f"qkv_cache {tag}"] == 2, (tag, fused[f"qkv_cache {tag}"])
     # the norm is an output: at most MUL_MAT + bias fuses ([]: its result landed on the freed input)
     assert fused["neg_output_flag"] in ([2], [])
     assert fused["neg_second_use"] == []        # the mat-vec result has two consumers
@@ -76,4 +85,4 @@ def test_fused_chains_match_cpu_and_fuse(attn_kernel):
 def test_unfused_graph_matches_cpu():
     fused, attn, pairs = _run(False)
     assert all(v == [] for v in fused.values()), fused
-    assert not any(attn.values()) and not any(pairs.values()), (attn, pairs)
+    assert not any(attn.values()) and not any(pairs.values()) and not any(folds.values()), (attn, pairs, folds)
