@@ -58,6 +58,10 @@ MFMA_F16_PEAK_TFLOPS = 2500.0   # dense f16/bf16 MFMA peak, MI355X_MICROARCH.md 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 HBM_MEASURED_GBS = 6290.0      # float4 copy measured on MI355X (same guide)
 I8_PEAK_TOPS = 5000.0          # dense int8 / fp8 MFMA (no sparsity)
+# BENCH_ONE_GPU_REHEARSAL=1 with --gpus N: all N ranks share GPU 0 and exchange over gloo through
+# host memory — the N > 1 code paths (rank plumbing, row-split all-gather, pipeline ring,
+# timing reduction) on a one-GPU box. Its numbers are not scaling numbers.
+REHEARSAL = os.environ.get("BENCH_ONE_GPU_REHEARSAL") == "1"
 F16_PEAK_TFLOPS = 2500.0       # dense f16/bf16 MFMA
 
 
@@ -183,7 +187,7 @@ def rowsplit_configs(torch, world: int, rank: int, reps: int = 20) -> dict:
         w = [torch.from_numpy(synthetic_weights(t, max(hi - lo, 1), K, 1234 + rank).reshape(-1)).to(dev) for _ in range(copies)]
         x = torch.from_numpy(np.random.default_rng(5).uniform(-1, 1, (Mc, K)).astype(np.float32)).to(dev)
         y = torch.zeros((Mc, N), dtype=torch.float32, device=dev)
-        mms = [RS.ShardedMatMul(torch, t, K, N, rank, world, wi) for wi in w]
+        mms = [RS.ShardedMatMul(torch, t, K, N, rank, world, wi, comm_device="cpu" if REHEARSAL else None) for wi in w]
 
         def sync():
             if world > 1:
@@ -198,7 +202,7 @@ def rowsplit_configs(torch, world: int, rank: int, reps: int = 20) -> dict:
             mms[i % copies].forward(x, y)
         sync()
         el = time.perf_counter() - t0
-        t_max = max_over_ranks(el, dev) if world > 1 else el
+        t_max = max_over_ranks(el, torch.device("cpu") if REHEARSAL else dev) if world > 1 else el
         us = t_max / reps * 1e6
         gbytes = alg_bytes(t, K, N, Mc)
         out[name] = {"us": round(us, 3), "GB/s": round(gbytes / us / 1e3, 1), "TFLOP/s": round(2.0 * K * N * Mc / us / 1e6, 3),
@@ -272,9 +276,10 @@ def cpu_baseline(seconds: float) -> dict:
             "us_per_mul_mat": round(per * 1e6, 2)}
 
 
-def gpt2_leg(torch, world: int, rank: int, n_seq: int, ticks: int, warm: int) -> dict:
+def gpt2_leg(torch, world: int, rank: int, n_seq: int, ticks: int, warm: int, cpu_group=None) -> dict:
     """GPT-2 117M Q4_0 decode through the pipeline ring (gpt2.Pipeline): stage `rank` of
-    `world`, n_micro = world micro-batches of n_seq sequences. Returns this rank's timing."""
+    `world`, n_micro = world micro-batches of n_seq sequences. Returns this rank's timing.
+    cpu_group: a gloo group for host-side waits (world > 1)."""
     import gpt2 as G
     import torch.distributed as dist
     hp = G.make_hparams(M.Q4_0)
@@ -306,7 +311,7 @@ def gpt2_leg(torch, world: int, rank: int, n_seq: int, ticks: int, warm: int) ->
         c._copy(send[mb].data_ptr(), src, 4 * n_seq if stage.last else c.hidden_bytes, st)
         return send[mb]
 
-    pipe = G.Pipeline(rank, world, n_micro, n_seq * E, dev)
+    pipe = G.Pipeline(rank, world, n_micro, n_seq * E, dev, comm_device="cpu" if REHEARSAL else None)
     first = lambda mb: prompt[mb].view(torch.float32)  # noqa: E731
 
     def sync():
@@ -512,12 +517,19 @@ def main() -> None:
     if args.dry_run:
         dry_run(args, world, rank)
         return
+    builder = local == 0
+    if REHEARSAL:
+        local = 0                      # every rank on GPU 0; exchanges over gloo through host memory
     torch.cuda.set_device(local)
     cpu_group = None
-    if world > 1:
+    reduce_dev = torch.device("cpu") if REHEARSAL else torch.device("cuda", local)
+    if world > 1 and REHEARSAL:
+        dist.init_process_group("gloo")
+        cpu_group = dist.group.WORLD
+    elif world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         cpu_group = dist.new_group(backend="gloo")
-    if local == 0:
+    if builder:
         M.build()                      # one rank per node compiles (if stale); the others wait
     if world > 1:
         dist.barrier()
@@ -544,7 +556,7 @@ def main() -> None:
         g.launch(i)
     barrier()
     elapsed = time.perf_counter() - t0
-    t_max = max_over_ranks(elapsed, torch.device("cuda", local)) if world > 1 else elapsed
+    t_max = max_over_ranks(elapsed, reduce_dev) if world > 1 else elapsed
 
     kernel_us = g.launch_us(max(8, args.steps))
     value = job_gbps(g.bytes, args.steps, world, t_max)
@@ -591,8 +603,8 @@ def main() -> None:
         torch.cuda.empty_cache()
         runs = {}
         for n_seq in (1, 8):
-            r = gpt2_leg(torch, world, rank, n_seq, args.gpt2_ticks, 8)
-            t_g = max_over_ranks(r["elapsed"], torch.device("cuda", local)) if world > 1 else r["elapsed"]
+            r = gpt2_leg(torch, world, rank, n_seq, args.gpt2_ticks, 8, cpu_group)
+            t_g = max_over_ranks(r["elapsed"], reduce_dev) if world > 1 else r["elapsed"]
             runs[n_seq] = (r, t_g)
         r1, t1 = runs[1]
         gpt2 = {"metric": "GPT-2 117M Q4_0 greedy decode tokens/s", "unit": "tokens/s",
@@ -610,9 +622,9 @@ def main() -> None:
         if rank == 0:
             # configs[4]'s scheduler form: the reference's scheduler over all `world` devices
             gpt2["reference_scheduler_with_plugin"] = sched_plugin_gpt2(cpu["cores"] if cpu else cpu_threads(),
-                                                                        devices=world)
+                                                                        devices=1 if REHEARSAL else world)
         if world > 1:
-            dist.barrier()
+            dist.barrier(group=cpu_group)   # host wait: rank 0's scheduler run uses the other GPUs
 
     if rank == 0:
         line = {

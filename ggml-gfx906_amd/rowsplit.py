@@ -59,8 +59,11 @@ class ShardedMatMul:
     [lo, hi) = row_split(N, world, fractions)[rank]. Call forward(x, out) on every rank."""
 
     def __init__(self, torch, t: int, K: int, N: int, rank: int, world: int, w_local, fractions=None, group=None,
-                 compute=None):
+                 compute=None, comm_device=None):
+        """comm_device "cpu": the all-gather runs on host copies (process groups that cannot move
+        device tensors, e.g. gloo with ranks sharing one GPU)"""
         self.torch, self.t, self.K, self.N, self.rank, self.world, self.group = torch, t, K, N, rank, world, group
+        self.comm_device = comm_device
         self.shards = row_split(N, world, fractions)
         self.lo, self.hi = self.shards[rank]
         self.rows = self.hi - self.lo
@@ -98,6 +101,12 @@ class ShardedMatMul:
             return
         local, gathered = self._buffers(M, x.device)
         self.compute(x, local)
+        if self.comm_device is not None and self.comm_device != str(x.device):
+            host = [t.to(self.comm_device) for t in (local, gathered)]
+            dist.all_gather_into_tensor(host[1].view(-1), host[0].view(-1), group=self.group)
+            gathered.copy_(host[1])
+            assemble(list(gathered), self.shards, out)
+            return
         if M == 1 and self.equal:
             # dst rows of all ranks are contiguous and equal: gather straight into out
             dist.all_gather_into_tensor(out.view(-1), local.view(-1), group=self.group)

@@ -82,3 +82,22 @@ def test_bench_rejects_rank_count_mismatch():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     rc, line, err = _bench_json(["--gpus", "2", "--dry-run"], env)
     assert rc != 0 and line is None and "--gpus 2" in err
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_one_gpu_rehearsal():
+    """bench.py's N > 1 legs end to end on the one-GPU test box: BENCH_ONE_GPU_REHEARSAL=1 puts
+    both ranks on GPU 0 with gloo exchanges through host memory, so the row-split all-gather,
+    the GPT-2 pipeline ring, the host-side waits and the slowest-rank reductions all run (the
+    driver's 8-GPU run takes the same code with RCCL). Numbers are not checked, only that every
+    leg produced one."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["BENCH_ONE_GPU_REHEARSAL"] = "1"
+    rc, line, err = _bench_json(["--gpus", "2", "--steps", "3", "--warmup", "1", "--gpt2-ticks", "16",
+                                 "--cpu-seconds", "1"], env)
+    assert rc == 0, err[-3000:]
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    for k in ("q4_K_4096x11008_m1_rowsplit", "q8_0_4096x4096_m512_rowsplit"):
+        assert line["configs"][k]["shards"] == 2 and line["configs"][k]["us"] > 0
+    assert line["gpt2"]["value"] > 0 and line["gpt2"]["batched_n_seq8_tokens_per_s"] > 0
+    assert line["gpt2"]["parallelism"].startswith("pp2")
