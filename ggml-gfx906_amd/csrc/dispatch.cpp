@@ -47,6 +47,8 @@ bool mmq_id_supported(int type, const MmArgs &a);
 hipError_t mmq_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
 bool mmq8_supported(int type, const MmArgs &a);
 hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
+bool mmq8_id_supported(int type, const MmArgs &a);
+hipError_t mmq8_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
 
 // mat-mat kernel family: the int8 MFMA tile (csrc/mmq8.hip) wherever it applies (K a multiple
 // of 256, aligned rows): it is exact in the block scales (no f16 range to overflow) and measured
@@ -223,9 +225,14 @@ int mul_mat_id(const TensorView &as, const TensorView &b, const TensorView &ids,
     m.n_expert = (int)as.ne[2];
     m.x_aligned16 = aligned16(b.data, m.nb11, m.nb12, m.nb13);
     static const int min_pairs = getenv("GGML_MI355X_MMQ_ID_MIN") ? atoi(getenv("GGML_MI355X_MMQ_ID_MIN")) : MMQ_ID_MIN_PAIRS;
-    const bool grouped = m.n_used * m.n_tok >= min_pairs && mmq_id_supported(as.type, m);
+    const bool grouped = m.n_used * m.n_tok >= min_pairs;
+    // the grouped int8 tile unless GGML_MI355X_MMQ=f16 (as for MUL_MAT)
+    const char *mq = getenv("GGML_MI355X_MMQ");
+    const bool i8 = grouped && !(mq && !strcmp(mq, "f16")) && mmq8_id_supported(as.type, m);
     std::lock_guard<std::mutex> hold(scratch.mu);
-    const hipError_t e = grouped ? mmq_id_launch(as.type, m, st, scratch) : mmvq_id_launch(as.type, m, 1, st);
+    const hipError_t e = i8 ? mmq8_id_launch(as.type, m, st, scratch)
+                         : grouped && mmq_id_supported(as.type, m) ? mmq_id_launch(as.type, m, st, scratch)
+                                                                   : mmvq_id_launch(as.type, m, 1, st);
     if (e == hipErrorOutOfMemory) return GGML_MI355X_ENOMEM;
     return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
 }

@@ -1830,6 +1830,11 @@ __global__ __launch_bounds__(1024) void moe_prep(const MmArgs a, int *offsets, i
     for (int p = threadIdx.x; p < P; p += 1024) pos_pair[atomicAdd(&cur[expert_of(p)], 1)] = p;
 }
 
+hipError_t moe_prep_launch(const MmArgs &a, int *offsets, int *tile_off, int *pos_pair, hipStream_t st) {
+    hipLaunchKernelGGL(moe_prep, dim3(1), dim3(1024), 0, st, a, offsets, tile_off, pos_pair);
+    return hipGetLastError();
+}
+
 bool mmq_id_supported(int type, const MmArgs &a) {
     const int P = a.n_used * a.n_tok;
     MmArgs b = a;

@@ -69,6 +69,29 @@ constexpr float Q8_MAGIC_F = 12582912.0f;
 constexpr int XI_DX = 16384, XI_BS = 16640;
 template <int T> constexpr bool q8_has_min() { return T == T_Q4_K || T == T_Q5_K; }
 template <int T> constexpr int ximg_bytes() { return q8_has_min<T>() ? 19456 : 17408; }
+// ---- MUL_MAT_ID: expert-sorted (slot, token) pairs (moe_prep in mmq.hip), 64-pair token tiles
+//   offsets[e] .. offsets[e+1]: sorted positions of expert e's pairs; tile_off[e]: first tile of
+//   expert e (prefix sum of ceil(count / 64)); pos_pair[q]: pair t * n_used + slot at position q
+struct Moe8 {
+    const int *offsets, *tile_off, *pos_pair;
+    int n_expert, n_used;
+};
+// tile j -> expert e, first sorted position q0, pairs in the tile; false past the last tile.
+// The largest e with tile_off[e] <= j is the non-empty expert holding j (empty experts share
+// their successor's offset).
+__device__ __forceinline__ bool moe8_tile(const Moe8 &m, int j, int &e, int &q0, int &cnt) {
+    if (j >= m.tile_off[m.n_expert]) return false;
+    int lo = 0, hi = m.n_expert - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (m.tile_off[mid] <= j) lo = mid; else hi = mid - 1;
+    }
+    e = lo;
+    q0 = m.offsets[e] + (j - m.tile_off[e]) * 64;
+    cnt = min(64, m.offsets[e + 1] - q0);
+    return true;
+}
+
 // ---- weight image: codes [blk 8][h 2][row TR][16 B] (Q6_K [blk][h][hl][row][8 B]) + meta [kg][row][16 B]
 template <int TR> constexpr int wi_meta() { return 256 * TR; }
 template <int TR> constexpr int wi_bytes() { return 288 * TR; }
@@ -116,20 +139,32 @@ __device__ __forceinline__ void q8_dma16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_
 // (token t, piece p) holds k = 16p..16p+15 (64 B read per lane, a token's 1 KB by 16 lanes),
 // i.e. exactly one 16-B code piece of the image and one 16-element block sum.
 // ------------------------------------------------------------------------------------------
-template <int T>
-__global__ __launch_bounds__(256) void mmq8_quant_x(const MmArgs a, uint8_t *__restrict__ ximg, int n_tt, int n_sb) {
+// MOE: token index = position in the tile-padded pair list (tile tok / 64 of moe), its column
+// gathered from src1 (slot % ne11, token) as mmq_convert_x does; padding positions are zeros.
+template <int T, bool MOE = false>
+__global__ __launch_bounds__(256) void mmq8_quant_x(const MmArgs a, uint8_t *__restrict__ ximg, int n_tt, int n_sb,
+                                                    const Moe8 moe) {
     constexpr int XB = ximg_bytes<T>();
     const int tid = threadIdx.x, p = tid & 15;
     const int tok = (blockIdx.x / n_sb) * 16 + (tid >> 4), sb = blockIdx.x % n_sb;
     const int slice = blockIdx.y;
     const int i12 = slice % a.ne12, i13 = slice / a.ne12;
+    const uint8_t *row = nullptr;
+    if constexpr (MOE) {
+        int e, q0, cnt;
+        if (!moe8_tile(moe, tok >> 6, e, q0, cnt)) return;   // (uniform: 16 tokens of one tile)
+        if ((tok & 63) < cnt) {
+            const int pair = moe.pos_pair[q0 + (tok & 63)];
+            row = a.x + (int64_t)((pair % moe.n_used) % a.ne11_b) * a.nb11 + (int64_t)(pair / moe.n_used) * a.nb12;
+        }
+    } else if (tok < a.M) {
+        row = a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13 + (int64_t)tok * a.nb11;
+    }
     float v[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = 0.f;
-    if (tok < a.M) {
-        const float *src = reinterpret_cast<const float *>(a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13 +
-                                                           (int64_t)tok * a.nb11) +
-                           sb * Q8_QK + p * 16;
+    if (row != nullptr) {
+        const float *src = reinterpret_cast<const float *>(row) + sb * Q8_QK + p * 16;
         if (a.x_aligned16) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -592,10 +627,10 @@ __device__ __forceinline__ void q8_x_dma(__amdgpu_buffer_rsrc_t xr, uint32_t img
 //   TT = 128: every wave takes whole super-blocks (the weight stage serves twice the tokens).
 //   TR = 64 halves the workgroup (4 waves, ~70 KB of LDS) so that two run on one CU and their
 //   load / compute phases interleave.
-template <int T, int TT, int TR>
+template <int T, int TT, int TR, bool MOE = false>
 __global__ __launch_bounds__(4 * TR) void mmq8_kernel(const MmArgs a, const uint8_t *__restrict__ ximg, int n_tt,
                                                       int ksplit, int sb_per, uint32_t w_extent,
-                                                      float *__restrict__ part, int xcd_remap) {
+                                                      float *__restrict__ part, int xcd_remap, const Moe8 moe) {
     constexpr int NW = TR / 16;                    // waves
     constexpr int WB = wi_bytes<TR>();
     constexpr int XB = ximg_bytes<T>();
@@ -613,9 +648,13 @@ __global__ __launch_bounds__(4 * TR) void mmq8_kernel(const MmArgs a, const uint
     v /= n_tt;
     const int ks = v % ksplit, rt = v / ksplit;
     const int sb0 = ks * sb_per, sb1 = min(n_sb, sb0 + sb_per);
-    const int slice = blockIdx.y;
+    const int slice = blockIdx.y;   // MOE: the token tile
     const int i12 = slice % a.ne12, i13 = slice / a.ne12;
-    const uint8_t *wmat = a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03;
+    int ex = 0, q0 = 0, n_tok = a.M;   // MOE: expert, first sorted pair, pairs of the tile
+    if constexpr (MOE)
+        if (!moe8_tile(moe, slice, ex, q0, n_tok)) return;   // (uniform, before any barrier)
+    const uint8_t *wmat = MOE ? a.w + (int64_t)ex * a.nb02
+                              : a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03;
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void *)wmat, 0, w_extent, Q8_RSRC_W3);
     // the NI consecutive 64-token images of this tile: [slice][64-token tile][sb][image]
     const uint8_t *xbase = ximg + ((int64_t)slice * n_tt * NI + (int64_t)tt * NI) * n_sb * XB;
@@ -714,8 +753,15 @@ __global__ __launch_bounds__(4 * TR) void mmq8_kernel(const MmArgs a, const uint
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int tok = tok0 + 8 * (i >> 2) + (i & 3);
-        if (tok < a.M) {
-            float *drow = reinterpret_cast<float *>(dbase + (int64_t)tok * ldd);
+        if (tok < n_tok) {
+            float *drow;
+            if constexpr (MOE) {   // scatter to dst[slot][token] of the pair
+                const int pair = moe.pos_pair[q0 + tok];
+                drow = reinterpret_cast<float *>(a.dst + (int64_t)(pair % moe.n_used) * a.nb1 +
+                                                 (int64_t)(pair / moe.n_used) * a.nb2);
+            } else {
+                drow = reinterpret_cast<float *>(dbase + (int64_t)tok * ldd);
+            }
             if (rowA < a.N) drow[rowA] = acc0[i];
             if (rowB < a.N) drow[rowB] = acc1[i];
         }
@@ -772,7 +818,7 @@ static void launch8(const MmArgs &a, uint8_t *ximg, int tr_rows, int tt_tok, int
     const int n_sb = a.K / Q8_QK;
     const int n_img = n_tt * (tt_tok / Q8_TOK);   // 64-token images per slice (tokens past M: zeros)
     hipLaunchKernelGGL(mmq8_quant_x<T>, dim3((unsigned)(n_img * (Q8_TOK / 16) * n_sb), slices), dim3(256), 0, st, a, ximg,
-                       n_img, n_sb);
+                       n_img, n_sb, Moe8{});
     const int64_t row_b = (int64_t)a.K / QT<T>::blck * QT<T>::bytes;
     // windows of the last super-block may reach 2 bytes past the row: round the range up to a dword
     const uint32_t w_extent = (uint32_t)(((int64_t)(a.N - 1) * a.nb01 + row_b + 3) & ~(int64_t)3);
@@ -782,7 +828,7 @@ static void launch8(const MmArgs &a, uint8_t *ximg, int tr_rows, int tt_tok, int
     const dim3 grid(gx, slices);
 #define Q8_LAUNCH(TTv, TRv)                                                                                          \
     hipLaunchKernelGGL((mmq8_kernel<T, TTv, TRv>), grid, dim3(4 * TRv), 0, st, a, (const uint8_t *)ximg, n_tt, ksplit, \
-                       sb_per, w_extent, part, remap)
+                       sb_per, w_extent, part, remap, Moe8{})
     if (tt_tok == 128) Q8_LAUNCH(128, 128);
     else if (tr_rows == 128) Q8_LAUNCH(64, 128);
     else Q8_LAUNCH(64, 64);   // measured slower than 128 rows at every shape; kept for A/B
@@ -825,6 +871,65 @@ hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scrat
         case T_Q4_K: launch8<T_Q4_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, st); break;
         case T_Q5_K: launch8<T_Q5_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, st); break;
         case T_Q6_K: launch8<T_Q6_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// MUL_MAT_ID on the int8 tile (prefill / many tokens): moe_prep groups the (slot, token) pairs
+// by expert, mmq8_quant_x gathers and quantizes their columns into one 64-token image per
+// tile, and every tile runs the 128 x 64 kernel on its expert's matrix, the epilogue scattering
+// rows to dst[slot][token]. grid.y is the bound ceil(P / 64) + n_expert; surplus workgroups
+// exit at once, so nothing waits on the host. (Reference: ggml_cuda_mul_mat_id,
+// src/ggml-cuda/ggml-cuda.cu:2092-2230, which runs its int8 MMQ per expert.)
+// ------------------------------------------------------------------------------------------
+hipError_t moe_prep_launch(const MmArgs &a, int *offsets, int *tile_off, int *pos_pair, hipStream_t st);
+constexpr int MOE8_MAX_EXPERTS = 1024;   // moe_prep's LDS counters
+
+static int64_t moe8_tiles(const MmArgs &a) { return ((int64_t)a.n_used * a.n_tok + 63) / 64 + a.n_expert; }
+
+bool mmq8_id_supported(int type, const MmArgs &a) {
+    if (a.n_expert > MOE8_MAX_EXPERTS || a.n_expert < 1) return false;
+    MmArgs b = a;
+    b.M = a.n_used * a.n_tok;
+    b.ne12 = a.n_expert; b.ne13 = 1; b.r2 = 1; b.r3 = 1;   // every expert matrix: alignment of nb02
+    if (!mmq8_supported(type, b)) return false;
+    return moe8_tiles(a) <= 65535 && moe8_tiles(a) * (a.K / Q8_QK) * ximg_bytes_rt(type) < (1LL << 31);
+}
+
+template <int T>
+static void launch8_id(const MmArgs &a, uint8_t *ximg, int n_tiles, const Moe8 &moe, hipStream_t st) {
+    const int n_sb = a.K / Q8_QK;
+    hipLaunchKernelGGL((mmq8_quant_x<T, true>), dim3((unsigned)(n_tiles * (Q8_TOK / 16) * n_sb), 1), dim3(256), 0, st, a,
+                       ximg, n_tiles, n_sb, moe);
+    const int64_t row_b = (int64_t)a.K / QT<T>::blck * QT<T>::bytes;
+    const uint32_t w_extent = (uint32_t)(((int64_t)(a.N - 1) * a.nb01 + row_b + 3) & ~(int64_t)3);
+    const unsigned gx = (unsigned)((a.N + 127) / 128);
+    const int remap = (gx % 8 == 0) ? 1 : 0;
+    hipLaunchKernelGGL((mmq8_kernel<T, 64, 128, true>), dim3(gx, (unsigned)n_tiles), dim3(512), 0, st, a,
+                       (const uint8_t *)ximg, 1, 1, n_sb, w_extent, (float *)nullptr, remap, moe);
+}
+
+hipError_t mmq8_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch) {
+    const int P = a.n_used * a.n_tok, E = a.n_expert, n_sb = a.K / Q8_QK;
+    const int n_tiles = (int)moe8_tiles(a);
+    const size_t img_bytes = ((size_t)n_tiles * n_sb * ximg_bytes_rt(type) + 255) & ~(size_t)255;
+    const size_t map_bytes = sizeof(int) * (2 * (size_t)(E + 1) + P);
+    uint8_t *buf = static_cast<uint8_t *>(scratch.get(img_bytes + map_bytes, st));
+    if (!buf) return hipErrorOutOfMemory;
+    int *offsets = reinterpret_cast<int *>(buf + img_bytes);
+    int *tile_off = offsets + (E + 1);
+    int *pos_pair = tile_off + (E + 1);
+    hipError_t e = moe_prep_launch(a, offsets, tile_off, pos_pair, st);
+    if (e != hipSuccess) return e;
+    const Moe8 moe{offsets, tile_off, pos_pair, E, a.n_used};
+    switch (type) {
+        case T_Q4_0: launch8_id<T_Q4_0>(a, buf, n_tiles, moe, st); break;
+        case T_Q8_0: launch8_id<T_Q8_0>(a, buf, n_tiles, moe, st); break;
+        case T_Q4_K: launch8_id<T_Q4_K>(a, buf, n_tiles, moe, st); break;
+        case T_Q5_K: launch8_id<T_Q5_K>(a, buf, n_tiles, moe, st); break;
+        case T_Q6_K: launch8_id<T_Q6_K>(a, buf, n_tiles, moe, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -15,7 +15,7 @@ import bench  # noqa: E402
 M = bench.M
 TYPES = {"q4_0": M.Q4_0, "q8_0": M.Q8_0, "q4_K": M.Q4_K, "q5_K": M.Q5_K, "q6_K": M.Q6_K}
 M.build()
-tag = os.environ.get("GGML_MI355X_MMQ_ID_MIN", "default")
+tag = os.environ.get("GGML_MI355X_MMQ_ID_MIN", "default") + "/" + os.environ.get("GGML_MI355X_MMQ", "i8")
 for sh in sys.argv[1:] or ["q4_K:4096:11008:8:2:512", "q4_0:4096:4096:64:8:256"]:
     tn, K, N, E, U, T = sh.split(":")
     t, K, N, E, U, T = TYPES[tn], int(K), int(N), int(E), int(U), int(T)
@@ -28,9 +28,9 @@ for sh in sys.argv[1:] or ["q4_K:4096:11008:8:2:512", "q4_0:4096:4096:64:8:256"]
     B = M.tensor(M.F32, x.data_ptr(), [K, U, T, 1], M.contiguous_nb(M.F32, [K, U, T]))
     I = M.tensor(M.I32, ids.data_ptr(), [U, T, 1, 1], M.contiguous_nb(M.I32, [U, T]))
     D = M.tensor(M.F32, y.data_ptr(), [N, U, T, 1], M.contiguous_nb(M.F32, [N, U, T]))
-    M.mul_mat_id(A, B, I, D)
-    torch.cuda.synchronize()
     s = torch.cuda.Stream()
+    M.mul_mat_id(A, B, I, D, s)     # eager first: the stream's scratch grows outside the capture
+    torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
         for _ in range(4):

@@ -230,7 +230,10 @@ def test_mmq_activation_range(mm, scale, path, bar, monkeypatch):
 # ------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("t", qref.HOT_TYPES, ids=lambda t: qref.NAMES[t])
 @pytest.mark.parametrize("bcast", [False, True], ids=["b_per_slot", "b_shared"])
-def test_mul_mat_id_grouped(mm, t, bcast):
+@pytest.mark.parametrize("path", ["i8", "f16"])
+def test_mul_mat_id_grouped(mm, t, bcast, path, monkeypatch):
+    """both grouped tiles: the int8 one (default) and the f16 one (GGML_MI355X_MMQ=f16)"""
+    monkeypatch.setenv("GGML_MI355X_MMQ", path)
     K = 512 if qref.BLCK[t] == 256 else 96 * 3
     N, E, U, T = 300, 8, 2, 200
     w = qref.quantize(t, qref.fill_uniform(N * K * E, 51), n_per_row=K)

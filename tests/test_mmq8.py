@@ -165,3 +165,64 @@ def test_mmq8_q8_0_config3(mm):
     got = run_mul_mat(mm, a, b, [N, M_, 1, 1])
     want = G.oracle_mul_mat(a, b, [N, M_, 1, 1], threads=16)
     assert qref.nmse(got, want) <= 5e-4
+
+
+# ------------------------------------------------------------------------------------------
+# MUL_MAT_ID on the int8 tile (>= 64 (slot, token) pairs; mmq8_id_launch): experts grouped on
+# the device, activation columns gathered per 64-pair tile, rows scattered to dst[slot][token]
+# ------------------------------------------------------------------------------------------
+def run_mul_mat_id(mm, t, w, x, ids, K, N, E, b_ne1):
+    from test_gpu_parity import check_guard, dev_bytes, guarded_out
+    U, T = ids.shape[1], ids.shape[0]
+    a = G.Operand(t, w, [K, N, E, 1], qref.contiguous_nb(t, [K, N, E, 1]))
+    b = G.Operand(qref.F32, x, [K, b_ne1, T, 1], qref.contiguous_nb(qref.F32, [K, b_ne1, T, 1]))
+    iop = G.Operand(qref.I32, ids, [U, T, 1, 1], [4, 4 * U, 4 * U * T, 4 * U * T])
+    out_ne = [N, U, T, 1]
+    da, db, di = dev_bytes(w), dev_bytes(x), dev_bytes(ids)
+    nel = int(np.prod(out_ne))
+    dout = guarded_out(nel)
+    A = mm.tensor(t, da.data_ptr(), a.ne, a.nb)
+    B = mm.tensor(qref.F32, db.data_ptr(), b.ne, b.nb)
+    I = mm.tensor(qref.I32, di.data_ptr(), iop.ne, iop.nb)
+    D = mm.tensor(qref.F32, dout.data_ptr() + 4 * 1024, out_ne, qref.contiguous_nb(qref.F32, out_ne))
+    mm.mul_mat_id(A, B, I, D)
+    torch.cuda.synchronize()
+    return check_guard(dout, nel), G.oracle_mul_mat_id(a, b, iop, out_ne)
+
+
+@pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])
+@pytest.mark.parametrize("case_", ["skewed", "empty_experts", "one_expert", "b_shared"])
+def test_mmq8_mul_mat_id(mm, t, case_):
+    """expert counts that are not multiples of the 64-pair tile, a hot expert, experts with no
+    pair (their tiles do not exist), all pairs on one expert, src1 shared by the slots"""
+    K, N, E, U, T = 512, 200, 8, 2, 150
+    rng = np.random.default_rng(61)
+    ids = np.stack([rng.permutation(E)[:U] for _ in range(T)]).astype(np.int32)
+    if case_ == "skewed":
+        ids[: T // 2, 0] = 3
+        ids[: T // 2, 1] = np.where(ids[: T // 2, 1] == 3, 5, ids[: T // 2, 1])
+    elif case_ == "empty_experts":
+        ids = np.stack([rng.choice([1, 4, 6], U, replace=False) for _ in range(T)]).astype(np.int32)
+    elif case_ == "one_expert":
+        U = 1
+        ids = np.full((T, 1), 7, np.int32)
+    b_ne1 = 1 if case_ == "b_shared" else U
+    w = qref.quantize(t, qref.fill_uniform(N * K * E, 62), n_per_row=K)
+    x = qref.fill_uniform(K * b_ne1 * T, 63)
+    got, want = run_mul_mat_id(mm, t, w, x, ids, K, N, E, b_ne1)
+    assert np.all(np.isfinite(got))
+    assert qref.nmse(got, want) <= TIGHT[t]
+
+
+@pytest.mark.parametrize("t,big", [(qref.Q8_0, 7.0e4), (qref.Q4_K, 2.0e3), (qref.Q6_K, 3.0e3)])
+def test_mmq8_mul_mat_id_huge_scales(mm, t, big):
+    """scales far beyond real weights on the grouped path: exact int32 block sums, f32 scales"""
+    K, N, E, U, T = 512, 96, 4, 2, 100
+    f = qref.fill_uniform(N * K * E, 71).reshape(N * E, K)
+    f[3::5] *= big
+    w = qref.quantize(t, f.reshape(-1), n_per_row=K)
+    x = qref.fill_uniform(K * U * T, 72)
+    ids = np.stack([np.random.default_rng(73 + i).permutation(E)[:U] for i in range(T)]).astype(np.int32)
+    got, want = run_mul_mat_id(mm, t, w, x, ids, K, N, E, U)
+    assert np.all(np.isfinite(got))
+    assert qref.nmse(got, want) <= TIGHT[t]
