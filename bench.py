@@ -369,7 +369,8 @@ def sched_plugin_gpt2(threads: int, tokens: int = 64, devices: int = 1) -> dict 
     gpt2_synth.write_model(path, gpt2_synth.GPT2_117M, qref.Q4_0, 1234)
     try:
         r = subprocess.run([exe, path, "--tokens", "40", "--threads", str(threads), "--plugin", M.LIB_PATH, "--devices",
-                            str(devices), "--time-tokens", str(tokens)], capture_output=True, text=True, timeout=300)
+                            str(devices), "--time-tokens", str(tokens)], capture_output=True, text=True,
+                           timeout=300 if devices == 1 else 150)   # (the N > 1 ranks wait on it)
         if r.returncode != 0:
             return None
         j = json.loads(r.stdout.strip().splitlines()[-1])
