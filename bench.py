@@ -368,9 +368,12 @@ def sched_plugin_gpt2(threads: int, tokens: int = 64, devices: int = 1) -> dict 
     path = os.path.join(tempfile.gettempdir(), f"bench_gpt2_sched_{os.getpid()}.bin")
     gpt2_synth.write_model(path, gpt2_synth.GPT2_117M, qref.Q4_0, 1234)
     try:
+        env = dict(os.environ)
+        if REHEARSAL and devices > 1:
+            env["GGML_MI355X_VIRTUAL_DEVICES"] = str(devices)   # plugin devices over GPU 0
         r = subprocess.run([exe, path, "--tokens", "40", "--threads", str(threads), "--plugin", M.LIB_PATH, "--devices",
                             str(devices), "--time-tokens", str(tokens)], capture_output=True, text=True,
-                           timeout=300 if devices == 1 else 150)   # (the N > 1 ranks wait on it)
+                           timeout=300 if devices == 1 else 150, env=env)   # (the N > 1 ranks wait on it)
         if r.returncode != 0:
             return None
         j = json.loads(r.stdout.strip().splitlines()[-1])
@@ -623,7 +626,7 @@ def main() -> None:
         if rank == 0:
             # configs[4]'s scheduler form: the reference's scheduler over all `world` devices
             gpt2["reference_scheduler_with_plugin"] = sched_plugin_gpt2(cpu["cores"] if cpu else cpu_threads(),
-                                                                        devices=1 if REHEARSAL else world)
+                                                                        devices=world)
         if world > 1:
             dist.barrier(group=cpu_group)   # host wait: rank 0's scheduler run uses the other GPUs
 

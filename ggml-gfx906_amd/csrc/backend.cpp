@@ -1472,7 +1472,9 @@ bool dv_supports_op(ggml_backend_dev_t d, const struct ggml_tensor *op) {
 
 bool dv_supports_buft(ggml_backend_dev_t d, ggml_backend_buffer_type_t bt) {
     if (is_split_buft(bt)) return bt->device == d;
-    return is_our_buft(bt) && static_cast<DeviceCtx *>(bt->context)->device == dev_ctx(d)->device;
+    // a device's own buffer type only (as ggml_backend_cuda_device_supports_buft): with virtual
+    // devices two plugin devices share one GPU, and the scheduler must still see two places
+    return is_our_buft(bt) && static_cast<DeviceCtx *>(bt->context) == dev_ctx(d);
 }
 
 // like the CUDA backend: batched matmuls are worth moving weights across for
@@ -1556,13 +1558,11 @@ Registry &registry() {
             (void)hipGetLastError();
             n = 0;
         }
-        for (int i = 0; i < n; ++i) {
-            hipDeviceProp_t p;
-            if (hipGetDeviceProperties(&p, i) != hipSuccess || strncmp(p.gcnArchName, "gfx950", 6) != 0) continue;
+        auto add = [&](int hip_dev, const char *desc) {
             auto dc = std::make_unique<DeviceCtx>();
-            dc->device = i;
+            dc->device = hip_dev;
             dc->name = std::string("MI355X") + std::to_string(R->ctxs.size());
-            dc->desc = p.name;
+            dc->desc = desc;
             dc->buft_name = std::string(BUFT_TAG) + std::to_string(R->ctxs.size());
             auto dev = std::make_unique<ggml_backend_device>();
             dev->iface = DEVICE_IFACE;
@@ -1573,6 +1573,21 @@ Registry &registry() {
             dc->buft.context = dc.get();
             R->ctxs.push_back(std::move(dc));
             R->devs.push_back(std::move(dev));
+        };
+        for (int i = 0; i < n; ++i) {
+            hipDeviceProp_t p;
+            if (hipGetDeviceProperties(&p, i) != hipSuccess || strncmp(p.gcnArchName, "gfx950", 6) != 0) continue;
+            add(i, p.name);
+        }
+        // GGML_MI355X_VIRTUAL_DEVICES=k (testing): k plugin devices over the GPUs present, device
+        // i on GPU i % n — on a one-GPU box the scheduler's multi-device split (graph splits,
+        // cross-device tensor copies, stream / event hand-offs) runs with every device on GPU 0
+        // (same-GPU copies instead of peer copies)
+        const int n_real = (int)R->ctxs.size();
+        const char *vd = getenv("GGML_MI355X_VIRTUAL_DEVICES");
+        for (int i = n_real; n_real > 0 && vd && i < atoi(vd); ++i) {
+            const DeviceCtx &src = *R->ctxs[i % n_real];
+            add(src.device, (src.desc + " (virtual)").c_str());
         }
         // peer access between every pair of our devices, once, at registry init: the scheduler's
         // cross-device hand-off (be_cpy_async) and the split buffer's row shards then move over

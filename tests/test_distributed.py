@@ -101,3 +101,5 @@ def test_bench_two_ranks_one_gpu_rehearsal():
         assert line["configs"][k]["shards"] == 2 and line["configs"][k]["us"] > 0
     assert line["gpt2"]["value"] > 0 and line["gpt2"]["batched_n_seq8_tokens_per_s"] > 0
     assert line["gpt2"]["parallelism"].startswith("pp2")
+    sched = line["gpt2"]["reference_scheduler_with_plugin"]   # 2 plugin devices (virtual, GPU 0)
+    assert sched is not None and sched["devices"] == 2 and sched["splits"] >= 2 and sched["value"] > 0

@@ -107,10 +107,13 @@ def test_pipeline_two_stages_match_single_stage():
 @pytest.mark.skipif(not os.path.exists(REF_BIN), reason="oracle/_ref not built")
 def test_reference_scheduler_splits_over_two_devices():
     """the reference's ggml_backend_sched places layers on two plugin devices and moves
-    activations with our cross-device cpy_tensor_async (hipMemcpyPeerAsync over xGMI)"""
+    activations with our cross-device cpy_tensor_async (hipMemcpyPeerAsync over xGMI). On a
+    one-GPU box both plugin devices are GPU 0 (GGML_MI355X_VIRTUAL_DEVICES=2): the graph split,
+    the hand-off copies and the stream / event ordering run, with a same-GPU copy for the peer
+    copy."""
+    env = dict(os.environ)
     if _n_gpus() < 2:
-        pytest.skip("needs 2 gfx950 devices (the driver's multi-GPU node); the 1-GPU box covers the "
-                    "single-device scheduler path in test_gpt2.py::test_reference_scheduler_drives_plugin")
+        env["GGML_MI355X_VIRTUAL_DEVICES"] = "2"
     import json
     man = json.load(open(os.path.join(ROOT, "tests", "golden", "gpt2_manifest.json")))
     c = man["cases"]["q4_0"]
@@ -118,8 +121,11 @@ def test_reference_scheduler_splits_over_two_devices():
     out = os.path.join(tempfile.gettempdir(), f"gpt2_plugin2_{os.getpid()}.f32")
     lib = os.path.join(ROOT, "ggml-gfx906_amd", "libggml-hip-mi355x.so")
     r = subprocess.run([REF_BIN, path, "--tokens", ",".join(map(str, c["tokens"][:24])), "--out", out, "--plugin", lib,
-                        "--devices", "2"], capture_output=True, text=True, timeout=180)
+                        "--devices", "2"], capture_output=True, text=True, timeout=180, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
+    import re
+    m = re.search(r"(\d+) backends, (\d+) splits", r.stderr)
+    assert m and int(m.group(1)) == 3 and int(m.group(2)) >= 2, r.stderr[-500:]   # 2 plugin devices + CPU
     got = np.fromfile(out, np.float32).reshape(24, -1)
     want = np.fromfile(os.path.join(ROOT, "tests", "golden", c["logits"]), np.float32).reshape(len(c["tokens"]), -1)[:24]
     for i in range(24):
