@@ -141,14 +141,21 @@ __device__ __forceinline__ void q8_dma16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_
 // ------------------------------------------------------------------------------------------
 // MOE: token index = position in the tile-padded pair list (tile tok / 64 of moe), its column
 // gathered from src1 (slot % ne11, token) as mmq_convert_x does; padding positions are zeros.
+// zero_dst: also clear dst (the 2-way split-K kernel adds both halves into it): workgroup
+// (16 tokens, super-block sb) clears columns [sb * ceil(N / n_sb), ...) of its tokens' rows.
 template <int T, bool MOE = false>
 __global__ __launch_bounds__(256) void mmq8_quant_x(const MmArgs a, uint8_t *__restrict__ ximg, int n_tt, int n_sb,
-                                                    const Moe8 moe) {
+                                                    const Moe8 moe, int zero_dst) {
     constexpr int XB = ximg_bytes<T>();
     const int tid = threadIdx.x, p = tid & 15;
     const int tok = (blockIdx.x / n_sb) * 16 + (tid >> 4), sb = blockIdx.x % n_sb;
     const int slice = blockIdx.y;
     const int i12 = slice % a.ne12, i13 = slice / a.ne12;
+    if (!MOE && zero_dst && tok < a.M) {
+        const int chunk = (a.N + n_sb - 1) / n_sb, c1 = min(a.N, (sb + 1) * chunk);
+        float *drow = reinterpret_cast<float *>(a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3 + (int64_t)tok * a.nb1);
+        for (int c = sb * chunk + p; c < c1; c += 16) drow[c] = 0.f;
+    }
     const uint8_t *row = nullptr;
     if constexpr (MOE) {
         int e, q0, cnt;
@@ -643,7 +650,7 @@ __global__ __launch_bounds__(4 * TR) void mmq8_kernel(const MmArgs a, const uint
     uint8_t *const Xs = lds + 2 * WB;
     const int n_sb = a.K / Q8_QK;
     int v = blockIdx.x;
-    if (xcd_remap) v = (v & 7) * (int)(gridDim.x >> 3) + (v >> 3);
+    if (xcd_remap & 1) v = (v & 7) * (int)(gridDim.x >> 3) + (v >> 3);
     const int tt = v % n_tt;
     v /= n_tt;
     const int ks = v % ksplit, rt = v / ksplit;
@@ -743,7 +750,8 @@ __global__ __launch_bounds__(4 * TR) void mmq8_kernel(const MmArgs a, const uint
     const int rowA = rt * TR + 64 * rg + r, rowB = rowA + 32;
     uint8_t *dbase;
     int64_t ldd;
-    if (ksplit > 1) {   // part[ks][slice][token][row]
+    const bool atomic = (xcd_remap & 4) != 0;   // 2-way split-K: both halves add into dst (zeroed)
+    if (ksplit > 1 && !atomic) {   // part[ks][slice][token][row]
         dbase = reinterpret_cast<uint8_t *>(part + ((int64_t)ks * gridDim.y + slice) * a.M * a.N);
         ldd = (int64_t)a.N * 4;
     } else {
@@ -761,6 +769,11 @@ __global__ __launch_bounds__(4 * TR) void mmq8_kernel(const MmArgs a, const uint
                                                  (int64_t)(pair / moe.n_used) * a.nb2);
             } else {
                 drow = reinterpret_cast<float *>(dbase + (int64_t)tok * ldd);
+            }
+            if (atomic) {   // 0 + a + b == 0 + b + a: deterministic for exactly two halves
+                if (rowA < a.N) unsafeAtomicAdd(drow + rowA, acc0[i]);
+                if (rowB < a.N) unsafeAtomicAdd(drow + rowB, acc1[i]);
+                continue;
             }
             if (rowA < a.N) drow[rowA] = acc0[i];
             if (rowB < a.N) drow[rowB] = acc1[i];
@@ -814,17 +827,17 @@ bool mmq8_supported(int type, const MmArgs &a) {
 
 template <int T>
 static void launch8(const MmArgs &a, uint8_t *ximg, int tr_rows, int tt_tok, int n_tt, int slices, int ksplit,
-                    int sb_per, float *part, hipStream_t st) {
+                    int sb_per, float *part, bool atomic, hipStream_t st) {
     const int n_sb = a.K / Q8_QK;
     const int n_img = n_tt * (tt_tok / Q8_TOK);   // 64-token images per slice (tokens past M: zeros)
     hipLaunchKernelGGL(mmq8_quant_x<T>, dim3((unsigned)(n_img * (Q8_TOK / 16) * n_sb), slices), dim3(256), 0, st, a, ximg,
-                       n_img, n_sb, Moe8{});
+                       n_img, n_sb, Moe8{}, atomic ? 1 : 0);
     const int64_t row_b = (int64_t)a.K / QT<T>::blck * QT<T>::bytes;
     // windows of the last super-block may reach 2 bytes past the row: round the range up to a dword
     const uint32_t w_extent = (uint32_t)(((int64_t)(a.N - 1) * a.nb01 + row_b + 3) & ~(int64_t)3);
     const int n_rt = (a.N + tr_rows - 1) / tr_rows;
     const unsigned gx = (unsigned)(n_rt * ksplit * n_tt);
-    const int remap = (gx % 8 == 0) ? 1 : 0;
+    const int remap = ((gx % 8 == 0) ? 1 : 0) | (atomic ? 4 : 0);
     const dim3 grid(gx, slices);
 #define Q8_LAUNCH(TTv, TRv)                                                                                          \
     hipLaunchKernelGGL((mmq8_kernel<T, TTv, TRv>), grid, dim3(4 * TRv), 0, st, a, (const uint8_t *)ximg, n_tt, ksplit, \
@@ -833,7 +846,7 @@ static void launch8(const MmArgs &a, uint8_t *ximg, int tr_rows, int tt_tok, int
     else if (tr_rows == 128) Q8_LAUNCH(64, 128);
     else Q8_LAUNCH(64, 64);   // measured slower than 128 rows at every shape; kept for A/B
 #undef Q8_LAUNCH
-    if (ksplit > 1) {
+    if (ksplit > 1 && !atomic) {
         const int64_t n = (int64_t)slices * a.M * a.N;
         hipLaunchKernelGGL(mmq8_split_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, (const float *)part,
                            ksplit, slices);
@@ -846,6 +859,8 @@ hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scrat
     // rows x tokens per workgroup: 128-token tiles once they alone give every CU a workgroup
     // (the weight stage then serves twice the tokens); GGML_MI355X_MMQ8_TT / _TR override
     // (measurements; 128 tokens always run 128 rows)
+    // (128-token tiles on half the chip with 2-way split-K measured slower at 4096 x 4096 x 512:
+    // 44.9-45.1 vs 41.3 us, profiles/r03_mmq8_split2_atomic.txt)
     int tt_tok = (int64_t)((a.N + 127) / 128) * ((a.M + 127) / 128) * slices >= 256 ? 128 : 64;
     if (const char *e = getenv("GGML_MI355X_MMQ8_TT")) tt_tok = atoi(e) == 128 ? 128 : 64;
     int tr_rows = 128;
@@ -861,16 +876,19 @@ hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scrat
     const int sb_per = (n_sb + ksplit - 1) / ksplit;
     ksplit = (n_sb + sb_per - 1) / sb_per;
     const size_t img_bytes = ((size_t)slices * n_tt * (tt_tok / Q8_TOK) * n_sb * ximg_bytes_rt(type) + 255) & ~(size_t)255;
-    const size_t part_bytes = ksplit > 1 ? (size_t)ksplit * slices * a.M * a.N * sizeof(float) : 0;
+    // exactly two halves add into dst atomically (order-independent); more go through part[]
+    static const bool no_atomic = getenv("GGML_MI355X_MMQ8_ATOMIC") && atoi(getenv("GGML_MI355X_MMQ8_ATOMIC")) == 0;
+    const bool atomic = ksplit == 2 && !no_atomic;
+    const size_t part_bytes = ksplit > 1 && !atomic ? (size_t)ksplit * slices * a.M * a.N * sizeof(float) : 0;
     uint8_t *buf = static_cast<uint8_t *>(scratch.get(img_bytes + part_bytes, st));
     if (!buf) return hipErrorOutOfMemory;
     float *part = reinterpret_cast<float *>(buf + img_bytes);
     switch (type) {
-        case T_Q4_0: launch8<T_Q4_0>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, st); break;
-        case T_Q8_0: launch8<T_Q8_0>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, st); break;
-        case T_Q4_K: launch8<T_Q4_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, st); break;
-        case T_Q5_K: launch8<T_Q5_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, st); break;
-        case T_Q6_K: launch8<T_Q6_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, st); break;
+        case T_Q4_0: launch8<T_Q4_0>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, atomic, st); break;
+        case T_Q8_0: launch8<T_Q8_0>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, atomic, st); break;
+        case T_Q4_K: launch8<T_Q4_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, atomic, st); break;
+        case T_Q5_K: launch8<T_Q5_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, atomic, st); break;
+        case T_Q6_K: launch8<T_Q6_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, atomic, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -902,7 +920,7 @@ template <int T>
 static void launch8_id(const MmArgs &a, uint8_t *ximg, int n_tiles, const Moe8 &moe, hipStream_t st) {
     const int n_sb = a.K / Q8_QK;
     hipLaunchKernelGGL((mmq8_quant_x<T, true>), dim3((unsigned)(n_tiles * (Q8_TOK / 16) * n_sb), 1), dim3(256), 0, st, a,
-                       ximg, n_tiles, n_sb, moe);
+                       ximg, n_tiles, n_sb, moe, 0);
     const int64_t row_b = (int64_t)a.K / QT<T>::blck * QT<T>::bytes;
     const uint32_t w_extent = (uint32_t)(((int64_t)(a.N - 1) * a.nb01 + row_b + 3) & ~(int64_t)3);
     const unsigned gx = (unsigned)((a.N + 127) / 128);

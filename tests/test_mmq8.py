@@ -226,3 +226,18 @@ def test_mmq8_mul_mat_id_huge_scales(mm, t, big):
     got, want = run_mul_mat_id(mm, t, w, x, ids, K, N, E, U)
     assert np.all(np.isfinite(got))
     assert qref.nmse(got, want) <= TIGHT[t]
+
+
+@pytest.mark.parametrize("t", [qref.Q8_0, qref.Q4_K], ids=lambda t: qref.NAMES[t])
+def test_mmq8_two_halves_bitwise_repeatable(mm, t):
+    """the 2-way split-K adds both K-halves into the zeroed dst with float atomics: with exactly
+    two addends the sum is order-independent, so repeated calls agree bit for bit (N = 1024,
+    M = 512, K = 1024: 64 tiles of 128 x 64, four super-blocks, two K-halves)"""
+    N, M_, K = 1024, 512, 1024
+    w = qref.quantize(t, qref.fill_uniform(N * K, 91), n_per_row=K)
+    x = qref.fill_uniform(M_ * K, 92)
+    a = G.Operand(t, w, [K, N, 1, 1], qref.contiguous_nb(t, [K, N, 1, 1]))
+    b = G.Operand(qref.F32, x, [K, M_, 1, 1], qref.contiguous_nb(qref.F32, [K, M_, 1, 1]))
+    outs = [run_mul_mat(mm, a, b, [N, M_, 1, 1]) for _ in range(3)]
+    assert all(np.array_equal(outs[0].view(np.uint32), o.view(np.uint32)) for o in outs[1:])
+    assert qref.nmse(outs[0], G.oracle_mul_mat(a, b, [N, M_, 1, 1])) <= TIGHT[t]
