@@ -4,6 +4,7 @@
 //   hipcc --offload-arch=gfx950 -O3 scripts/hbm_probe.hip -o scripts/hbm_probe && scripts/hbm_probe
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -30,6 +31,56 @@ __global__ void stream_read(const uint4 *__restrict__ p, size_t per_wg_vec, uint
         for (int u = 0; u < UNROLL; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
     }
     if (acc == 0x12345678u) out[blockIdx.x] = acc;   // keep the loads alive
+}
+
+// the same stream with the non-temporal policy (global_load_dwordx4 ... nt): whole lines per
+// wave instruction
+template <int UNROLL>
+__global__ void stream_read_nt(const uint4 *__restrict__ p, size_t per_wg_vec, uint32_t *out) {
+    const uint4 *base = p + (size_t)blockIdx.x * per_wg_vec;
+    uint32_t acc = 0;
+    for (size_t i = threadIdx.x; i < per_wg_vec; i += (size_t)blockDim.x * UNROLL) {
+        uint4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const size_t j = i + (size_t)u * blockDim.x;
+            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+            const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(base + (j < per_wg_vec ? j : 0)));
+            v[u] = make_uint4(t[0], t[1], t[2], t[3]);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    if (acc == 0x12345678u) out[blockIdx.x] = acc;
+}
+
+// LDS-DMA stream: every wave moves 1-KiB pieces (16 B per lane) into its own LDS ring of RING
+// pieces, keeping RING - 1 in flight, and touches one dword of each landed piece. AUX: cache
+// policy of the DMA (0 default, 2 nt).
+typedef __attribute__((address_space(3))) void *lds_ptr_t;
+template <int RING, int AUX>
+__global__ __launch_bounds__(256) void stream_lds_dma(const uint8_t *__restrict__ p, size_t per_wg, uint32_t *out) {
+    __shared__ __align__(16) uint8_t ring[4][RING][1024];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint8_t *base = p + (size_t)blockIdx.x * per_wg;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, (uint32_t)per_wg, 0x00020000);
+    const int n_pieces = (int)(per_wg / 1024);
+    uint32_t acc = 0;
+    int issued = 0;
+    for (int k = wave; k < n_pieces && issued < RING - 1; k += 4, ++issued)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)ring[wave][issued % RING], 16, (uint32_t)(k * 1024 + lane * 16), 0, 0, AUX);
+    int done = 0;
+    for (int k = wave; k < n_pieces; k += 4, ++done) {
+        const int kn = k + 4 * (RING - 1);
+        if (kn < n_pieces) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)ring[wave][(done + RING - 1) % RING], 16, (uint32_t)(kn * 1024 + lane * 16), 0, 0, AUX);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RING - 1) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        acc ^= reinterpret_cast<const uint32_t *>(ring[wave][done % RING])[lane];
+    }
+    if (acc == 0x12345678u) out[blockIdx.x] = acc;
 }
 
 struct __attribute__((packed, aligned(2))) u4a2 { uint32_t v[4]; };
@@ -77,6 +128,48 @@ int main(int argc, char **argv) {
             }
         }
         if (argc > 1 && argv[1][0] == 'e') return 0;
+    }
+    if (argc > 1 && argv[1][0] == 'n') {   // 576 MiB, two buffers alternating: plain vs nt vs LDS-DMA
+        const size_t bytes = 603979776;
+        uint8_t *bufs[2];
+        uint32_t *o;
+        for (auto &b : bufs) { CK(hipMalloc(&b, bytes)); CK(hipMemset(b, 1, bytes)); }
+        CK(hipMalloc(&o, 1 << 20));
+        hipEvent_t a, b;
+        CK(hipEventCreate(&a));
+        CK(hipEventCreate(&b));
+        auto run = [&](const char *name, auto launch) {
+            for (int i = 0; i < 4; ++i) launch(bufs[i & 1]);
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(a, 0));
+            for (int i = 0; i < 20; ++i) launch(bufs[i & 1]);
+            CK(hipEventRecord(b, 0));
+            CK(hipEventSynchronize(b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            printf("%-40s %7.0f GB/s\n", name, bytes * 20 / (ms * 1e-3) / 1e9);
+        };
+        for (int rep = 0; rep < 2; ++rep) {
+            for (int wgs : {2048, 4096}) {
+                const size_t per = bytes / 16 / wgs;
+                char nm[64];
+                snprintf(nm, sizeof nm, "plain dwordx4 x4, 512 thr, %d wgs", wgs);
+                run(nm, [&](uint8_t *p) { hipLaunchKernelGGL(stream_read<4>, dim3(wgs), dim3(512), 0, 0, (const uint4 *)p, per, o); });
+                snprintf(nm, sizeof nm, "nt    dwordx4 x4, 512 thr, %d wgs", wgs);
+                run(nm, [&](uint8_t *p) { hipLaunchKernelGGL(stream_read_nt<4>, dim3(wgs), dim3(512), 0, 0, (const uint4 *)p, per, o); });
+            }
+            for (int wgs : {512, 1024, 2048}) {
+                const size_t per = bytes / wgs;
+                char nm[64];
+                snprintf(nm, sizeof nm, "lds-dma ring 8 default, %d wgs", wgs);
+                run(nm, [&](uint8_t *p) { hipLaunchKernelGGL((stream_lds_dma<8, 0>), dim3(wgs), dim3(256), 0, 0, p, per, o); });
+                snprintf(nm, sizeof nm, "lds-dma ring 8 nt, %d wgs", wgs);
+                run(nm, [&](uint8_t *p) { hipLaunchKernelGGL((stream_lds_dma<8, 2>), dim3(wgs), dim3(256), 0, 0, p, per, o); });
+                snprintf(nm, sizeof nm, "lds-dma ring 16 nt, %d wgs", wgs);
+                run(nm, [&](uint8_t *p) { hipLaunchKernelGGL((stream_lds_dma<16, 2>), dim3(wgs), dim3(256), 0, 0, p, per, o); });
+            }
+        }
+        return 0;
     }
     if (argc > 1 && argv[1][0] == 'a') {
         const size_t bytes = 603979776;   // 576 MiB
