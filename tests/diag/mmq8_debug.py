@@ -5,7 +5,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "ggml-gfx906_amd"), os.path.join(ROOT, "tests")):
     sys.path.insert(0, p)
 os.environ["GGML_MI355X_MMQ"] = "i8"

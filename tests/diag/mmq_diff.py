@@ -1,10 +1,10 @@
 """Test-side diagnostic (imports the oracle as the checker). Error map of one golden MUL_MAT record on the current mat-mat tile (GGML_MI355X_MMQ_TILE):
 per-token and per-row error against the threaded oracle, to localize a tile bug.
-Usage: python scripts/mmq_diff.py record_name"""
+Usage: python tests/diag/mmq_diff.py record_name"""
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "tests"), ROOT, os.path.join(ROOT, "ggml-gfx906_amd"), os.path.join(ROOT, "oracle")]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
