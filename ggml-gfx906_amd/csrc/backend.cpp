@@ -837,6 +837,22 @@ int absorb_copies(BackendCtx *c, const struct ggml_cgraph *g, int last, int n, c
 }
 
 // nodes consumed by a fused mat-vec run at node i (0: no fusion); rc receives the launch status
+// GET_ROWS(a), GET_ROWS(b), ADD(first, second) with both row results used only by the ADD ->
+// one launch (the GPT-2 embedding, main-sched.cpp:589-595); returns the nodes consumed
+int fuse_embed(BackendCtx *c, const struct ggml_cgraph *g, int i, int n, int &rc) {
+    if (i + 2 >= n) return 0;
+    struct ggml_tensor *ga = g->nodes[i], *gb2 = g->nodes[i + 1], *add = g->nodes[i + 2];
+    if (ga->op != GGMLABI_OP_GET_ROWS || gb2->op != GGMLABI_OP_GET_ROWS || add->op != GGMLABI_OP_ADD) return 0;
+    if (add->src[0] != ga || add->src[1] != gb2 || !skippable(g, ga) || !skippable(g, gb2)) return 0;
+    if (ga->type != GGMLABI_TYPE_F32 || gb2->type != GGMLABI_TYPE_F32 || add->type != GGMLABI_TYPE_F32) return 0;
+    if (!same_shape_t(ga, gb2) || !same_shape_t(ga, add) || ga->ne[2] != 1 || ga->ne[3] != 1) return 0;
+    if (gb2->src[0]->type != GGMLABI_TYPE_F32) return 0;
+    rc = get_rows_add(tv(ga->src[0]), tv(ga->src[1]), tv(gb2->src[0]), tv(gb2->src[1]), tv(add), c->stream);
+    if (rc == GGML_MI355X_EINVAL) { rc = GGML_MI355X_OK; return 0; }   // shapes the fused kernel does not take
+    logf("fused embedding (3 nodes) at %s\n", add->name);
+    return 3;
+}
+
 int fuse_matvec(BackendCtx *c, const struct ggml_cgraph *g, int i, int n, int &rc) {
     auto at = [&](int k) -> struct ggml_tensor * { return i + k < n ? g->nodes[i + k] : nullptr; };
     const struct ggml_tensor *x = nullptr, *ln_g = nullptr, *ln_b = nullptr;
@@ -1220,6 +1236,7 @@ enum ggml_status run_nodes(BackendCtx *c, struct ggml_cgraph *g, bool quiet) {
             if (node->op == GGMLABI_OP_NORM || node->op == GGMLABI_OP_MUL_MAT) fused = fuse_matvec(c, g, i, n, rc);
             else if (node->op == GGMLABI_OP_SCALE || node->op == GGMLABI_OP_DIAG_MASK_INF) fused = fuse_softmax(c, g, i, n, rc);
             else if (is_plain_copy(node)) fused = pair_copies(c, g, i, n, rc);
+            else if (node->op == GGMLABI_OP_GET_ROWS) fused = fuse_embed(c, g, i, n, rc);
         }
         if (fused > 0) {
             i += fused - 1;

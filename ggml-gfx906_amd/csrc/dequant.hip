@@ -64,6 +64,46 @@ __global__ __launch_bounds__(256) void get_rows_kernel(const RowsArgs a) {
     }
 }
 
+// GET_ROWS(a) + GET_ROWS(b) -> ADD in one launch (the GPT-2 embedding, main-sched.cpp:589-595:
+// wte rows + wpe rows): each output element is the same dequantized values and the same single
+// fp32 addition as the three nodes, so the result is bit-identical. b is f32; both index one
+// 2-D matrix with a 1-D row list (the host checks).
+template <int T>
+__global__ __launch_bounds__(256) void get_rows_add_kernel(const RowsArgs a, const RowsArgs b) {
+    const int64_t row = blockIdx.y;
+    int64_t ia = *reinterpret_cast<const int32_t *>(a.idx + row * a.nb10);
+    int64_t ib = *reinterpret_cast<const int32_t *>(b.idx + row * b.nb10);
+    ia = ia < 0 ? 0 : (ia >= a.ne01 ? a.ne01 - 1 : ia);
+    ib = ib < 0 ? 0 : (ib >= b.ne01 ? b.ne01 - 1 : ib);
+    const uint8_t *sa = a.src + ia * a.nb01;
+    const float *sb = reinterpret_cast<const float *>(b.src + ib * b.nb01);
+    float *drow = reinterpret_cast<float *>(a.dst + row * a.nb1);
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.ne00) return;
+    float va;
+    if constexpr (T == T_F32) {
+        va = reinterpret_cast<const float *>(sa)[i];
+    } else {
+        const int64_t bl = i / QT<T>::blck;
+        va = deq_one<T>(sa + bl * QT<T>::bytes, (int)(i - bl * QT<T>::blck));
+    }
+    drow[i] = __fadd_rn(va, sb[i]);
+}
+
+hipError_t get_rows_add_launch(int type, const RowsArgs &a, const RowsArgs &b, int64_t nrows, hipStream_t st) {
+    const dim3 grid((unsigned)((a.ne00 + 255) / 256), (unsigned)nrows);
+    switch (type) {
+        case T_F32: hipLaunchKernelGGL(get_rows_add_kernel<T_F32>, grid, dim3(256), 0, st, a, b); break;
+        case T_Q4_0: hipLaunchKernelGGL(get_rows_add_kernel<T_Q4_0>, grid, dim3(256), 0, st, a, b); break;
+        case T_Q8_0: hipLaunchKernelGGL(get_rows_add_kernel<T_Q8_0>, grid, dim3(256), 0, st, a, b); break;
+        case T_Q4_K: hipLaunchKernelGGL(get_rows_add_kernel<T_Q4_K>, grid, dim3(256), 0, st, a, b); break;
+        case T_Q5_K: hipLaunchKernelGGL(get_rows_add_kernel<T_Q5_K>, grid, dim3(256), 0, st, a, b); break;
+        case T_Q6_K: hipLaunchKernelGGL(get_rows_add_kernel<T_Q6_K>, grid, dim3(256), 0, st, a, b); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t get_rows_launch(int type, const RowsArgs &a, int64_t nrows, hipStream_t st) {
     const dim3 grid((unsigned)((a.ne00 + 255) / 256), (unsigned)nrows);
     switch (type) {

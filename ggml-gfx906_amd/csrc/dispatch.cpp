@@ -36,6 +36,7 @@ struct RowsArgs {
     int64_t ne00;
 };
 hipError_t get_rows_launch(int type, const RowsArgs &a, int64_t nrows, hipStream_t st);
+hipError_t get_rows_add_launch(int type, const RowsArgs &a, const RowsArgs &b, int64_t nrows, hipStream_t st);
 struct QuantArgs {
     const uint8_t *src; int64_t nb01, nb02, nb03;
     uint8_t *dst; int64_t nb1, nb2, nb3;
@@ -271,6 +272,32 @@ int get_rows(const TensorView &a, const TensorView &r, const TensorView &d, hipS
     g.nb1 = (int64_t)d.nb[1]; g.nb2 = (int64_t)d.nb[2]; g.nb3 = (int64_t)d.nb[3];
     g.ne00 = a.ne[0];
     return get_rows_launch(a.type, g, nrows, st) == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
+}
+
+// GET_ROWS(a, ra) + GET_ROWS(b, rb) -> d in one launch (graph fusion of the GPT-2 embedding):
+// a hot type or f32, b f32, both 2-D with a 1-D row list of the same length, d [ne00, rows] f32
+int get_rows_add(const TensorView &a, const TensorView &ra, const TensorView &b, const TensorView &rb, const TensorView &d,
+                 hipStream_t st) {
+    int rc = check_get_rows(a, ra, d);
+    if (rc == GGML_MI355X_OK) rc = check_get_rows(b, rb, d);
+    if (rc != GGML_MI355X_OK) return rc;
+    if (b.type != T_F32 || a.ne[2] != 1 || a.ne[3] != 1 || b.ne[2] != 1 || b.ne[3] != 1) return GGML_MI355X_EINVAL;
+    if (ra.ne[1] != 1 || ra.ne[2] != 1 || rb.ne[0] != ra.ne[0] || rb.ne[1] != 1 || rb.ne[2] != 1) return GGML_MI355X_EINVAL;
+    const int64_t nrows = ra.ne[0];
+    if (nrows == 0 || a.ne[0] == 0) return GGML_MI355X_OK;
+    auto args = [&](const TensorView &s, const TensorView &r) {
+        RowsArgs g{};
+        g.src = static_cast<const uint8_t *>(s.data);
+        g.nb01 = (int64_t)s.nb[1]; g.nb02 = (int64_t)s.nb[2]; g.nb03 = (int64_t)s.nb[3]; g.ne01 = s.ne[1];
+        g.idx = static_cast<const uint8_t *>(r.data);
+        g.nb10 = (int64_t)r.nb[0]; g.nb11 = (int64_t)r.nb[1]; g.nb12 = (int64_t)r.nb[2];
+        g.ne10 = r.ne[0]; g.ne11 = r.ne[1];
+        g.dst = static_cast<uint8_t *>(d.data);
+        g.nb1 = (int64_t)d.nb[1]; g.nb2 = (int64_t)d.nb[2]; g.nb3 = (int64_t)d.nb[3];
+        g.ne00 = s.ne[0];
+        return g;
+    };
+    return get_rows_add_launch(a.type, args(a, ra), args(b, rb), nrows, st) == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
 }
 
 // f32 -> Q4_0 / Q8_0 (GGML_OP_CPY into a quantized tensor)

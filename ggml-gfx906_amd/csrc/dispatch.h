@@ -55,6 +55,8 @@ int mul_mat_id(const TensorView &as, const TensorView &b, const TensorView &ids,
 int dequantize(int type, const void *src, float *dst, int64_t n, hipStream_t st);
 int check_get_rows(const TensorView &a, const TensorView &rows, const TensorView &d);
 int get_rows(const TensorView &a, const TensorView &rows, const TensorView &d, hipStream_t st);
+int get_rows_add(const TensorView &a, const TensorView &ra, const TensorView &b, const TensorView &rb, const TensorView &d,
+                 hipStream_t st);
 int check_quantize(const TensorView &src, const TensorView &d);
 int quantize(const TensorView &src, const TensorView &d, hipStream_t st);
 

@@ -132,7 +132,7 @@ int main(int argc, char **argv) {
     const float eps = 1e-5f;
     int fails = 0;
 
-    auto check = [&](const std::string &name, const Builder &b, const Inputs &in) {
+    auto check = [&](const std::string &name, const Builder &b, const Inputs &in, bool exact = false) {
         fprintf(stderr, "CASE %s\n", name.c_str());   // the plugin's debug log follows on stderr
         const auto got = run(gpu, b, in);
         const auto want = run(cpu, b, in);
@@ -142,6 +142,7 @@ int main(int argc, char **argv) {
             bool finite = true;
             const double e = nmse(got[j], want[j], &finite);
             ok = ok && finite && e <= 5e-4;
+            if (exact) ok = ok && got[j].size() == want[j].size() && memcmp(got[j].data(), want[j].data(), 4 * got[j].size()) == 0;
             char buf[64];
             snprintf(buf, sizeof buf, " out%zu=%.3e%s", j, e, finite ? "" : "(nonfinite)");
             detail += buf;
@@ -204,6 +205,27 @@ int main(int argc, char **argv) {
                 ggml_build_forward_expand(gf, ggml_cpy(c, Vcur, v));
                 return std::vector<ggml_tensor *>{cur, memk, memv};
             }, in);
+
+            // token + position embedding (main-sched.cpp:589-595): GET_ROWS(wte) + GET_ROWS(wpe)
+            if (M > 1) {
+                const int V = 64, n_ctx = 32;
+                in.bytes["wte"] = q_bytes(t, E, V);
+                in.bytes["wpe"] = f32_bytes((size_t)E * n_ctx, -1.f, 1.f);
+                std::vector<uint8_t> tok(4 * M), pos(4 * M);
+                for (int j = 0; j < M; ++j) {
+                    const int32_t tv = (int32_t)(rng() % V), pv = 3 + j;
+                    memcpy(&tok[4 * j], &tv, 4);
+                    memcpy(&pos[4 * j], &pv, 4);
+                }
+                in.bytes["tok"] = tok;
+                in.bytes["pos"] = pos;
+                check("embed " + tag, [&](ggml_context *c, ggml_cgraph *) {
+                    ggml_tensor *wte = input(c, "wte", t, E, V), *wpe = input(c, "wpe", GGML_TYPE_F32, E, n_ctx);
+                    ggml_tensor *y = ggml_add(c, ggml_get_rows(c, wte, input(c, "tok", GGML_TYPE_I32, M)),
+                                              ggml_get_rows(c, wpe, input(c, "pos", GGML_TYPE_I32, M)));
+                    return std::vector<ggml_tensor *>{y};
+                }, in, true);
+            }
 
             // final layer-norm -> lm_head without bias (main-sched.cpp:826-847)
             check("ln_matvec " + tag, [&](ggml_context *c, ggml_cgraph *) {

@@ -21,6 +21,7 @@ pytestmark = pytest.mark.gpu
 
 
 folds = {}   # copies folded into a fused mat-vec, by case (filled by _run)
+embeds = {}  # fused embedding launches, by case
 
 
 def _run(fusion: bool, **extra):
@@ -32,6 +33,7 @@ def _run(fusion: bool, **extra):
     assert r.returncode == 0 and "FUSION_CHECK_OK" in r.stdout, (fails, r.stdout[-1500:], r.stderr[-1500:])
     fused, attn, pairs = {}, {}, {}
     folds.clear()
+    embeds.clear()
     case = None
     for line in r.stderr.splitlines():
         if line.startswith("CASE "):
@@ -40,6 +42,9 @@ def _run(fusion: bool, **extra):
             attn[case] = 0
             pairs[case] = 0
             folds[case] = 0
+            embeds[case] = 0
+        if "fused embedding" in line and case is not None:
+            embeds[case] += 1
         if "folded into the mat-vec's epilogue" in line and case is not None:
             folds[case] += 1
         m = re.search(r"fused (\d+) nodes", line)
@@ -64,6 +69,8 @@ def test_fused_chains_match_cpu_and_fuse(attn_kernel):
             assert fused[f"ln_matvec {tag}"] == [4], tag
             # c_attn + bias fuses and both cache writes ride in its epilogue (caches read back whole)
             assert fused[f"qkv_cache {tag}"] == [2] and folds[f"qkv_cache {tag}"] == 2, (tag, fused[f"qkv_cache {tag}"])
+            if m > 1:   # wte rows + wpe rows in one launch, bit-identical to ggml-cpu (checked by fusion_check)
+                assert embeds[f"embed {tag}"] == 1, tag
     # the norm is an output: at most MUL_MAT + bias fuses ([]: its result landed on the freed input)
     assert fused["neg_output_flag"] in ([2], [])
     assert fused["neg_second_use"] == []        # the mat-vec result has two consumers
@@ -86,3 +93,4 @@ def test_unfused_graph_matches_cpu():
     fused, attn, pairs = _run(False)
     assert all(v == [] for v in fused.values()), fused
     assert not any(attn.values()) and not any(pairs.values()) and not any(folds.values()), (attn, pairs, folds)
+    assert not any(embeds.values()), embeds
