@@ -128,17 +128,26 @@ struct FusePlan {
 
 // hipGraph of the last graph_compute (cf. the reference's CUDA graphs, ggml-cuda.cu:2757-2998):
 // the node properties it was captured from, and how many calls in a row needed a new capture
+// (the sources' types and layouts are part of it: weights are leafs, not nodes, and the kernel a
+// node launches depends on its weight's type and strides)
 struct NodeProps {
     const void *node, *data;
-    int32_t op, flags;
+    int32_t op, flags, type;
     int64_t ne[4];
     size_t nb[4];
     int32_t op_params[16];
     const void *src[GGMLABI_MAX_SRC], *src_data[GGMLABI_MAX_SRC];
+    int32_t src_type[GGMLABI_MAX_SRC];
+    int64_t src_ne[GGMLABI_MAX_SRC][4];
+    size_t src_nb[GGMLABI_MAX_SRC][4];
 };
+// scratch_gen: the backend scratch's generation when `exec` was captured; a later eager run that
+// grew (reallocated) the scratch invalidates the executable, whose mat-mat launches hold the old
+// buffer's address
 struct GraphCache {
     hipGraphExec_t exec = nullptr;
     std::vector<NodeProps> props;
+    uint64_t scratch_gen = 0;
     int updates = 0;
     bool disabled = false;
 };
@@ -642,6 +651,10 @@ void be_sync(ggml_backend_t b) {
     BackendCtx *c = be_ctx(b);
     HIP_OK(hipSetDevice(c->device));
     HIP_OK(hipStreamSynchronize(c->stream));
+    if (take_device_error()) {   // as the reference's GGML_ASSERT in get_rows (src/ggml-cpu/ops.cpp:5157)
+        fprintf(stderr, "[ggml-mi355x] %s: GET_ROWS row index out of range\n", c->name.c_str());
+        abort();
+    }
 }
 
 // MUL_MAT whose src0 lives in a split buffer (reference ggml_cuda_op_mul_mat's split branch,
@@ -1285,6 +1298,7 @@ void node_props(const struct ggml_tensor *t, NodeProps &p) {
     p.data = t->data;
     p.op = t->op;
     p.flags = t->flags;
+    p.type = t->type;
     for (int i = 0; i < 4; ++i) {
         p.ne[i] = t->ne[i];
         p.nb[i] = t->nb[i];
@@ -1293,6 +1307,13 @@ void node_props(const struct ggml_tensor *t, NodeProps &p) {
     for (int i = 0; i < GGMLABI_MAX_SRC; ++i) {
         p.src[i] = t->src[i];
         p.src_data[i] = t->src[i] ? t->src[i]->data : nullptr;
+        if (t->src[i]) {
+            p.src_type[i] = t->src[i]->type;
+            for (int d = 0; d < 4; ++d) {
+                p.src_ne[i][d] = t->src[i]->ne[d];
+                p.src_nb[i][d] = t->src[i]->nb[d];
+            }
+        }
     }
 }
 
@@ -1326,8 +1347,12 @@ enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
     if (!ggml_base().ok) return GGML_STATUS_FAILED;
     HIP_OK(hipSetDevice(c->device));
     GraphCache &hg = c->hg;
-    if (!graphs_on() || hg.disabled || has_split_weights(g)) return run_nodes(c, g, false);
-    const bool same = graph_unchanged(hg, g);
+    if (!graphs_on() || hg.disabled || has_split_weights(g)) {
+        // an eager run may grow (reallocate) the scratch a cached executable points into; the
+        // generation check below then refuses to replay it
+        return run_nodes(c, g, false);
+    }
+    const bool same = graph_unchanged(hg, g) && hg.scratch_gen == c->scratch.gen;
     if (same && hg.exec) {
         hg.updates = 0;
         HIP_OK(hipGraphLaunch(hg.exec, c->stream));
@@ -1361,6 +1386,7 @@ enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
         }
     }
     if (!hg.exec) HIP_OK(hipGraphInstantiate(&hg.exec, graph, nullptr, nullptr, 0));
+    hg.scratch_gen = c->scratch.gen;
     HIP_OK(hipGraphDestroy(graph));
     HIP_OK(hipGraphLaunch(hg.exec, c->stream));
     return GGML_STATUS_SUCCESS;

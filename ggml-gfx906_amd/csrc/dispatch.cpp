@@ -34,6 +34,7 @@ struct RowsArgs {
     const uint8_t *idx; int64_t nb10, nb11, nb12, ne10, ne11;
     uint8_t *dst; int64_t nb1, nb2, nb3;
     int64_t ne00;
+    int *err;
 };
 hipError_t get_rows_launch(int type, const RowsArgs &a, int64_t nrows, hipStream_t st);
 hipError_t get_rows_add_launch(int type, const RowsArgs &a, const RowsArgs &b, int64_t nrows, hipStream_t st);
@@ -43,6 +44,12 @@ struct QuantArgs {
     int64_t ne0, ne1, ne2, ne3;
 };
 hipError_t quantize_launch(int type, const QuantArgs &a, hipStream_t st);
+struct CpyQArgs {
+    const uint8_t *src; int64_t ne00, ne01, ne02; int64_t nb00, nb01, nb02, nb03;
+    uint8_t *dst; int64_t ne0, ne1, ne2; int64_t nb0, nb1, nb2, nb3;
+    int64_t n;
+};
+hipError_t cpy_q_launch(int type, bool to_f32, const CpyQArgs &a, hipStream_t st);
 bool mmq_supported(int type, const MmArgs &a);
 bool mmq_id_supported(int type, const MmArgs &a);
 hipError_t mmq_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
@@ -51,20 +58,19 @@ hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scrat
 bool mmq8_id_supported(int type, const MmArgs &a);
 hipError_t mmq8_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
 
-// mat-mat kernel family: the int8 MFMA tile (csrc/mmq8.hip) wherever it applies (K a multiple
-// of 256, aligned rows): it is exact in the block scales (no f16 range to overflow) and measured
-// as fast or faster than the f16 tiles for Q4_0 / Q8_0 / Q4_K / Q5_K from 9 to 2048 tokens
-// (scripts/mmq8_sweep.sh, profiles/r03_mmq_sweep.txt); Q6_K costs two MFMAs per 32-k block there
-// and runs ~1.4x slower than its f16 tile but stays on the exact path. GGML_MI355X_MMQ = f16
-// selects the f16 kernels (csrc/mmq.hip) for A/B measurements.
-static bool use_mmq8(int type, const MmArgs &m) {
-    if (!mmq8_supported(type, m)) return false;
-    const char *env = getenv("GGML_MI355X_MMQ");
-    if (env && !strcmp(env, "f16")) return false;
-    return true;
+// mat-mat kernel family: the int8 MFMA tile (csrc/mmq8.hip). It takes every K and every
+// 2-byte-aligned Q4_0 / Q8_0 / Q6_K layout (16-B aligned Q4_K / Q5_K), is exact in the block
+// scales (no f16 range to overflow) and measured as fast or faster than the f16 tiles for Q4_0 /
+// Q8_0 / Q4_K / Q5_K from 9 to 2048 tokens (scripts/mmq8_sweep.sh, profiles/r03_mmq_sweep.txt).
+// What it refuses (a K-quant view at an offset finer than 16 B, > 4 GiB spans) takes the
+// mat-vec, which is exact too. The f16 kernels (csrc/mmq.hip) run only when GGML_MI355X_MMQ = f16
+// asks for them (A/B measurements): their LDS-staged tiles overflow f16 past d > 511 (Q8_0).
+static bool mmq_f16_forced() {
+    const char *env = getenv("GGML_MI355X_MMQ");   // read per call: tests switch it
+    return env && !strcmp(env, "f16");
 }
 
-static constexpr size_t LDS_LIMIT = 160 * 1024;
+static constexpr size_t LDS_LIMIT = 159 * 1024;   // 160 KB per CU, less the kernels' static arrays
 
 int type_blck(int t) {
     switch (t) {
@@ -180,8 +186,9 @@ int mul_mat(const TensorView &a, const TensorView &b, const TensorView &d, hipSt
     MmArgs m = base_args(a, b, d);
     std::lock_guard<std::mutex> hold(scratch.mu);   // until the scratch users are queued
     hipError_t e;
-    if (m.M > 8 && use_mmq8(a.type, m)) e = mmq8_launch(a.type, m, st, scratch);
-    else if (m.M > 8 && mmq_supported(a.type, m)) e = mmq_launch(a.type, m, st, scratch);
+    const bool f16 = mmq_f16_forced();
+    if (m.M > 8 && !f16 && mmq8_supported(a.type, m)) e = mmq8_launch(a.type, m, st, scratch);
+    else if (m.M > 8 && f16 && mmq_supported(a.type, m)) e = mmq_launch(a.type, m, st, scratch);
     else e = run_mmvq(a.type, m, 0, m.M, st);
     if (e == hipErrorOutOfMemory) return GGML_MI355X_ENOMEM;
     return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
@@ -227,15 +234,49 @@ int mul_mat_id(const TensorView &as, const TensorView &b, const TensorView &ids,
     m.x_aligned16 = aligned16(b.data, m.nb11, m.nb12, m.nb13);
     static const int min_pairs = getenv("GGML_MI355X_MMQ_ID_MIN") ? atoi(getenv("GGML_MI355X_MMQ_ID_MIN")) : MMQ_ID_MIN_PAIRS;
     const bool grouped = m.n_used * m.n_tok >= min_pairs;
-    // the grouped int8 tile unless GGML_MI355X_MMQ=f16 (as for MUL_MAT)
-    const char *mq = getenv("GGML_MI355X_MMQ");
-    const bool i8 = grouped && !(mq && !strcmp(mq, "f16")) && mmq8_id_supported(as.type, m);
+    // the grouped int8 tile; the f16 one only when GGML_MI355X_MMQ=f16 asks (as for MUL_MAT)
+    const bool f16 = mmq_f16_forced();
+    const bool i8 = grouped && !f16 && mmq8_id_supported(as.type, m);
     std::lock_guard<std::mutex> hold(scratch.mu);
     const hipError_t e = i8 ? mmq8_id_launch(as.type, m, st, scratch)
-                         : grouped && mmq_id_supported(as.type, m) ? mmq_id_launch(as.type, m, st, scratch)
-                                                                   : mmvq_id_launch(as.type, m, 1, st);
+                         : grouped && f16 && mmq_id_supported(as.type, m) ? mmq_id_launch(as.type, m, st, scratch)
+                                                                          : mmvq_id_launch(as.type, m, 1, st);
     if (e == hipErrorOutOfMemory) return GGML_MI355X_ENOMEM;
     return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
+}
+
+// ------------------------------------------------------------------------------------------
+// device error word: one int in host-mapped pinned memory that kernels raise on a failed
+// precondition they can only see on the device (a GET_ROWS index out of range; the reference
+// GGML_ASSERTs, src/ggml-cpu/ops.cpp:5157). Read after the stream has synchronized.
+// ------------------------------------------------------------------------------------------
+static int *g_err_host = nullptr, *g_err_dev = nullptr;
+static std::once_flag g_err_once;
+
+int *device_error_word() {
+    std::call_once(g_err_once, [] {
+        void *h = nullptr;
+        if (hipHostMalloc(&h, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+            (void)hipGetLastError();
+            return;
+        }
+        void *d = nullptr;
+        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipHostFree(h);
+            return;
+        }
+        g_err_host = static_cast<int *>(h);
+        *g_err_host = 0;
+        g_err_dev = static_cast<int *>(d);
+    });
+    return g_err_dev;
+}
+
+int take_device_error() {
+    if (!g_err_host) return 0;
+    const int v = __atomic_exchange_n(g_err_host, 0, __ATOMIC_ACQ_REL);
+    return v;
 }
 
 int dequantize(int type, const void *src, float *dst, int64_t n, hipStream_t st) {
@@ -271,6 +312,8 @@ int get_rows(const TensorView &a, const TensorView &r, const TensorView &d, hipS
     g.dst = static_cast<uint8_t *>(d.data);
     g.nb1 = (int64_t)d.nb[1]; g.nb2 = (int64_t)d.nb[2]; g.nb3 = (int64_t)d.nb[3];
     g.ne00 = a.ne[0];
+    g.err = device_error_word();
+    if (!g.err) return GGML_MI355X_EHIP;
     return get_rows_launch(a.type, g, nrows, st) == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
 }
 
@@ -295,8 +338,10 @@ int get_rows_add(const TensorView &a, const TensorView &ra, const TensorView &b,
         g.dst = static_cast<uint8_t *>(d.data);
         g.nb1 = (int64_t)d.nb[1]; g.nb2 = (int64_t)d.nb[2]; g.nb3 = (int64_t)d.nb[3];
         g.ne00 = s.ne[0];
+        g.err = device_error_word();
         return g;
     };
+    if (!device_error_word()) return GGML_MI355X_EHIP;
     return get_rows_add_launch(a.type, args(a, ra), args(b, rb), nrows, st) == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
 }
 
@@ -307,6 +352,55 @@ int check_quantize(const TensorView &s, const TensorView &d) {
         if (s.ne[i] != d.ne[i]) return GGML_MI355X_EINVAL;
     if (s.ne[0] % 32 != 0 || s.nb[0] != 4 || (int64_t)d.nb[0] != type_bytes(d.type)) return GGML_MI355X_EINVAL;
     return GGML_MI355X_OK;
+}
+
+static int64_t nelements(const TensorView &t) { return t.ne[0] * t.ne[1] * t.ne[2] * t.ne[3]; }
+
+static bool is_contiguous(const TensorView &t) {
+    const int blck = t.type == T_F32 ? 1 : type_blck(t.type);
+    if ((int64_t)t.nb[0] != type_bytes(t.type) || t.ne[0] % blck != 0) return false;
+    const int64_t nb1 = (int64_t)t.nb[0] * (t.ne[0] / blck);
+    return (t.ne[1] <= 1 || (int64_t)t.nb[1] == nb1) && (t.ne[2] <= 1 || (int64_t)t.nb[2] == nb1 * t.ne[1]) &&
+           (t.ne[3] <= 1 || (int64_t)t.nb[3] == nb1 * t.ne[1] * t.ne[2]);
+}
+
+// GGML_OP_CPY (ggml_cpy, reference src/ggml.c; ggml_cuda_cpy src/ggml-cuda/cpy.cu) between the
+// types of this path:
+//   f32 -> Q4_0 / Q8_0   quantize_row_*_ref (check_quantize: same shape)
+//   hot -> f32           dup_q (src/ggml-cpu/ops.cpp:1105-1154): same element count, src blocks
+//                        along dim 0, dst rows holding whole blocks or dst contiguous (:1121-1123)
+//   hot -> same hot      dup_bytes (ops.cpp:956-1103): same element count, whole blocks per row
+int check_cpy(const TensorView &s, const TensorView &d) {
+    if (s.type == T_F32 && is_hot_quant(d.type)) return check_quantize(s, d);
+    if (!is_hot_quant(s.type) || !(d.type == T_F32 || d.type == s.type)) return GGML_MI355X_EINVAL;
+    const int blck = type_blck(s.type);
+    for (int i = 0; i < 4; ++i)
+        if (s.ne[i] < 0 || d.ne[i] < 0) return GGML_MI355X_EINVAL;
+    if (nelements(s) != nelements(d) || s.ne[0] % blck != 0 || (int64_t)s.nb[0] != type_bytes(s.type)) return GGML_MI355X_EINVAL;
+    if (d.type == T_F32) {
+        if (d.nb[0] != 4 || !(d.ne[0] % blck == 0 || is_contiguous(d))) return GGML_MI355X_EINVAL;
+    } else if (d.ne[0] % blck != 0 || (int64_t)d.nb[0] != type_bytes(d.type)) {
+        return GGML_MI355X_EINVAL;
+    }
+    if (nelements(s) > (1LL << 40)) return GGML_MI355X_EINVAL;   // 1-D grid
+    return GGML_MI355X_OK;
+}
+
+int cpy(const TensorView &s, const TensorView &d, hipStream_t st) {
+    if (s.type == T_F32) return quantize(s, d, st);
+    const int rc = check_cpy(s, d);
+    if (rc != GGML_MI355X_OK) return rc;
+    if (nelements(s) == 0) return GGML_MI355X_OK;
+    CpyQArgs q{};
+    q.src = static_cast<const uint8_t *>(s.data);
+    q.ne00 = s.ne[0]; q.ne01 = s.ne[1]; q.ne02 = s.ne[2];
+    q.nb00 = (int64_t)s.nb[0]; q.nb01 = (int64_t)s.nb[1]; q.nb02 = (int64_t)s.nb[2]; q.nb03 = (int64_t)s.nb[3];
+    q.dst = static_cast<uint8_t *>(d.data);
+    q.ne0 = d.ne[0]; q.ne1 = d.ne[1]; q.ne2 = d.ne[2];
+    q.nb0 = (int64_t)d.nb[0]; q.nb1 = (int64_t)d.nb[1]; q.nb2 = (int64_t)d.nb[2]; q.nb3 = (int64_t)d.nb[3];
+    const bool to_f32 = d.type == T_F32;
+    q.n = to_f32 ? nelements(s) : nelements(s) / type_blck(s.type);
+    return cpy_q_launch(s.type, to_f32, q, st) == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
 }
 
 int quantize(const TensorView &s, const TensorView &d, hipStream_t st) {
@@ -352,6 +446,7 @@ void *Scratch::get(size_t bytes, hipStream_t st) {
     }
     (void)hipGetDevice(&device);
     cap = want;
+    ++gen;
     return ptr;
 }
 
@@ -359,6 +454,7 @@ void Scratch::release() {
     if (ptr) (void)hipFree(ptr);
     ptr = nullptr;
     cap = 0;
+    ++gen;
 }
 
 Scratch::~Scratch() { release(); }
@@ -417,6 +513,13 @@ int ggml_mi355x_get_rows(const ggml_mi355x_tensor *src0, const ggml_mi355x_tenso
                          void *stream) {
     if (!src0 || !rows || !dst) return GGML_MI355X_EINVAL;
     return get_rows(view_of(src0), view_of(rows), view_of(dst), static_cast<hipStream_t>(stream));
+}
+
+int ggml_mi355x_device_error(void) { return take_device_error(); }
+
+int ggml_mi355x_cpy(const ggml_mi355x_tensor *src, ggml_mi355x_tensor *dst, void *stream) {
+    if (!src || !dst) return GGML_MI355X_EINVAL;
+    return cpy(view_of(src), view_of(dst), static_cast<hipStream_t>(stream));
 }
 
 int ggml_mi355x_quantize(const ggml_mi355x_tensor *src, ggml_mi355x_tensor *dst, void *stream) {

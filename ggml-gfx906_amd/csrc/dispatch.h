@@ -29,11 +29,15 @@ struct TensorView {
 // thread, and ctypes releases the GIL during a call), so mul_mat / mul_mat_id hold `mu` from
 // get() until every kernel that uses the buffer is queued: a second thread that must grow the
 // buffer then synchronizes the stream behind those kernels before it frees the old one.
+//
+// `gen` counts reallocations: a hipGraph captured while the buffer had generation g holds its
+// address, so the graph may be replayed only while gen is still g (backend.cpp checks it).
 struct Scratch {
     std::mutex mu;
     void *ptr = nullptr;
     size_t cap = 0;
     int device = -1;
+    uint64_t gen = 0;
     void *get(size_t bytes, hipStream_t st);
     void release();                   // free now (on the current device)
     ~Scratch();
@@ -57,7 +61,14 @@ int check_get_rows(const TensorView &a, const TensorView &rows, const TensorView
 int get_rows(const TensorView &a, const TensorView &rows, const TensorView &d, hipStream_t st);
 int get_rows_add(const TensorView &a, const TensorView &ra, const TensorView &b, const TensorView &rb, const TensorView &d,
                  hipStream_t st);
+// device error word (host-mapped): raised by kernels on a failed device-side precondition;
+// take_device_error() returns and clears it (call after the stream synchronized)
+int *device_error_word();
+int take_device_error();
 int check_quantize(const TensorView &src, const TensorView &d);
+// GGML_OP_CPY between this path's types: f32 -> Q4_0 / Q8_0, hot -> f32, hot -> same hot
+int check_cpy(const TensorView &src, const TensorView &d);
+int cpy(const TensorView &src, const TensorView &d, hipStream_t st);
 int quantize(const TensorView &src, const TensorView &d, hipStream_t st);
 
 // the f32 graph ops around the matmuls (graph_ops.hip)

@@ -170,7 +170,7 @@ __global__ __launch_bounds__(256) void mmq8_quant_x(const MmArgs a, uint8_t *__r
     float v[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = 0.f;
-    if (row != nullptr) {
+    if (row != nullptr && sb * Q8_QK + p * 16 < a.K) {   // (K % 32 == 0: a 16-piece is all in or all out)
         const float *src = reinterpret_cast<const float *>(row) + sb * Q8_QK + p * 16;
         if (a.x_aligned16) {
 #pragma unroll
@@ -228,9 +228,14 @@ __global__ __launch_bounds__(256) void mmq8_quant_x(const MmArgs a, uint8_t *__r
 // rows (consecutive lanes = consecutive blocks / chunks of one row), so a wave's 16-B loads
 // cover a few whole rows (coalesced) instead of one window of many rows.
 // ------------------------------------------------------------------------------------------
-struct RowTile {   // first row of the tile, rows of the matrix, row pitch, super-block offset
+// first row of the tile, rows of the matrix, row pitch, super-block offset (plus the matrix's
+// misalignment below a dword: the buffer base is the dword floor of the matrix), and the 32-blocks
+// of a row left from this super-block on (Q4_0 / Q8_0: K need not be a multiple of 256; blocks
+// past the row's end get a zero scale)
+struct RowTile {
     int row0, N;
     uint32_t nb01, sboff;
+    int blk_left;
     __device__ __forceinline__ uint32_t rb(int row) const {
         return (uint32_t)min(row0 + row, N - 1) * nb01 + sboff;
     }
@@ -238,9 +243,10 @@ struct RowTile {   // first row of the tile, rows of the matrix, row pitch, supe
 
 template <int T> struct WStage8;
 
-// Q8_0: task (row, block) = (t >> 3, t & 7), t = tid + 512 e. Rows and super-blocks are
-// dword-aligned (host check), so even blocks start dword-aligned (codes at +2) and odd blocks at
-// +2 (codes dword-aligned): one v_perm per dword realigns either.
+// Q8_0: task (row, block) = (t >> 3, t & 7), t = tid + 512 e. Blocks are 2-byte aligned (34-B
+// blocks, rows and matrices at any even offset): a block starting at 0 mod 4 has its codes at +2,
+// one starting at 2 mod 4 has them dword-aligned; one v_perm per dword realigns either, chosen
+// per lane from the block's own offset.
 template <> struct WStage8<T_Q8_0> {
     static constexpr int VMEM = 6;   // vector-memory instructions of one load()
     uint32_t w[2][9];
@@ -255,15 +261,16 @@ template <> struct WStage8<T_Q8_0> {
             w[e][8] = bl32(rs, o4 + 32);
         }
     }
-    template <int TR> __device__ __forceinline__ void store(uint8_t *W, const RowTile &, int tid) const {
+    template <int TR> __device__ __forceinline__ void store(uint8_t *W, const RowTile &R, int tid) const {
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-            const int t = tid + 4 * TR * e, row = t >> 3, blk = t & 7, odd = blk & 1;
+            const int t = tid + 4 * TR * e, row = t >> 3, blk = t & 7;
+            const int odd = ((R.rb(row) >> 1) ^ blk) & 1;   // the block starts at 2 mod 4
             const uint32_t sel = odd ? 0x07060504u : 0x05040302u;
             uint32_t c[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) c[i] = __builtin_amdgcn_perm(w[e][i + 1], w[e][i], sel);
-            const float d = h2f((uint16_t)(odd ? w[e][0] >> 16 : w[e][0] & 0xffffu));
+            const float d = blk < R.blk_left ? h2f((uint16_t)(odd ? w[e][0] >> 16 : w[e][0] & 0xffffu)) : 0.f;
             st128(W + wslot16<T_Q8_0, TR>(blk, 0, row), u32x4v{c[0], c[1], c[2], c[3]});
             st128(W + wslot16<T_Q8_0, TR>(blk, 1, row), u32x4v{c[4], c[5], c[6], c[7]});
             *reinterpret_cast<float *>(W + wi_meta<TR>() + (blk >> 2) * 16 * TR + row * 16 + 4 * (blk & 3)) = d;
@@ -285,10 +292,11 @@ template <> struct WStage8<T_Q4_0> {
             w[e][4] = bl32(rs, o4 + 16);
         }
     }
-    template <int TR> __device__ __forceinline__ void store(uint8_t *W, const RowTile &, int tid) const {
+    template <int TR> __device__ __forceinline__ void store(uint8_t *W, const RowTile &R, int tid) const {
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-            const int t = tid + 4 * TR * e, row = t >> 3, blk = t & 7, odd = blk & 1;
+            const int t = tid + 4 * TR * e, row = t >> 3, blk = t & 7;
+            const int odd = ((R.rb(row) >> 1) ^ blk) & 1;
             const uint32_t sel = odd ? 0x07060504u : 0x05040302u;
             uint32_t lo[4], hi[4];
 #pragma unroll
@@ -297,7 +305,7 @@ template <> struct WStage8<T_Q4_0> {
                 lo[i] = sub8_bytes(n & 0x0F0F0F0Fu);          // k 0..15
                 hi[i] = sub8_bytes((n >> 4) & 0x0F0F0F0Fu);   // k 16..31
             }
-            const float d = h2f((uint16_t)(odd ? w[e][0] >> 16 : w[e][0] & 0xffffu));
+            const float d = blk < R.blk_left ? h2f((uint16_t)(odd ? w[e][0] >> 16 : w[e][0] & 0xffffu)) : 0.f;
             st128(W + wslot16<T_Q4_0, TR>(blk, 0, row), u32x4v{lo[0], lo[1], lo[2], lo[3]});
             st128(W + wslot16<T_Q4_0, TR>(blk, 1, row), u32x4v{hi[0], hi[1], hi[2], hi[3]});
             *reinterpret_cast<float *>(W + wi_meta<TR>() + (blk >> 2) * 16 * TR + row * 16 + 4 * (blk & 3)) = d;
@@ -648,7 +656,7 @@ __global__ __launch_bounds__(4 * TR) void mmq8_kernel(const MmArgs a, const uint
     // the activation ring (LDS-DMA DX super-blocks ahead)
     __shared__ __align__(16) uint8_t lds[2 * WB + N_XS * NI * XB];
     uint8_t *const Xs = lds + 2 * WB;
-    const int n_sb = a.K / Q8_QK;
+    const int n_sb = (a.K + Q8_QK - 1) / Q8_QK;
     int v = blockIdx.x;
     if (xcd_remap & 1) v = (v & 7) * (int)(gridDim.x >> 3) + (v >> 3);
     const int tt = v % n_tt;
@@ -662,7 +670,12 @@ __global__ __launch_bounds__(4 * TR) void mmq8_kernel(const MmArgs a, const uint
         if (!moe8_tile(moe, slice, ex, q0, n_tok)) return;   // (uniform, before any barrier)
     const uint8_t *wmat = MOE ? a.w + (int64_t)ex * a.nb02
                               : a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03;
-    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void *)wmat, 0, w_extent, Q8_RSRC_W3);
+    // buffer base = the dword floor of the matrix, so that every window below is dword-aligned
+    const uint32_t wmis = (uint32_t)(reinterpret_cast<uintptr_t>(wmat) & 3);
+    // (w_extent: bytes from the matrix start to its last row's end; rounded up to the dword
+    // holding that end, so no window reaches into a later dword)
+    const __amdgpu_buffer_rsrc_t wr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(wmat - wmis), 0, (w_extent + wmis + 3) & ~3u, Q8_RSRC_W3);
     // the NI consecutive 64-token images of this tile: [slice][64-token tile][sb][image]
     const uint8_t *xbase = ximg + ((int64_t)slice * n_tt * NI + (int64_t)tt * NI) * n_sb * XB;
     const __amdgpu_buffer_rsrc_t xr =
@@ -676,7 +689,9 @@ __global__ __launch_bounds__(4 * TR) void mmq8_kernel(const MmArgs a, const uint
     const int rg = wave % NRG, tg = (wave / NRG) % NTG, kg = wave / (NRG * NTG);
     constexpr uint32_t SBB = (uint32_t)QT<T>::bytes * (Q8_QK / QT<T>::blck);   // bytes of one row's super-block
     constexpr int NXV = NI * q8_x_vmem<T, NW>();   // vector-memory instructions of one activation stage
-    auto rowtile = [&](int sb) { return RowTile{rt * TR, a.N, (uint32_t)a.nb01, (uint32_t)sb * SBB}; };
+    auto rowtile = [&](int sb) {
+        return RowTile{rt * TR, a.N, (uint32_t)a.nb01, (uint32_t)sb * SBB + wmis, a.K / 32 - 8 * sb};
+    };
 
     f32x16 acc0, acc1;
 #pragma unroll
@@ -806,35 +821,37 @@ static int ximg_bytes_rt(int type) {
     }
 }
 
+// Every K the block size divides (Q4_0 / Q8_0: a partial last super-block, its missing blocks
+// with zero activation codes and zero weight scales) and every 2-byte-aligned layout of Q4_0 /
+// Q8_0 / Q6_K (windows realigned per lane from the block's own offset, the buffer based at the
+// matrix's dword floor). Q4_K / Q5_K rows are 144 / 176 B, so their super-blocks are 16-B aligned
+// whenever the tensor is; a K-quant view at a finer offset takes the mat-vec.
 bool mmq8_supported(int type, const MmArgs &a) {
     if (!(type == T_Q4_0 || type == T_Q8_0 || type == T_Q4_K || type == T_Q5_K || type == T_Q6_K)) return false;
-    if (a.K % Q8_QK != 0 || a.M <= 0) return false;
-    // Q4_K / Q5_K: 16-B aligned row super-blocks; Q4_0 / Q8_0: dword-aligned (the block parity
-    // pattern of WStage8 relies on it)
-    // (Q6_K: matrices dword-aligned, rows 2-byte aligned: realigned per lane)
-    const uintptr_t al = (type == T_Q4_K || type == T_Q5_K) ? 15 : 3;
-    const uintptr_t al1 = type == T_Q6_K ? 1 : al;
+    if (a.K <= 0 || a.K % type_blck(type) != 0 || a.M <= 0) return false;
+    const uintptr_t al = (type == T_Q4_K || type == T_Q5_K) ? 15 : 1;
     // (the matrix strides matter only where there is more than one matrix)
     const bool many2 = a.ne12 / a.r2 > 1, many3 = a.ne13 / a.r3 > 1;
-    if ((reinterpret_cast<uintptr_t>(a.w) & al) || (a.nb01 & al1) || (many2 && (a.nb02 & al)) || (many3 && (a.nb03 & al)))
+    if ((reinterpret_cast<uintptr_t>(a.w) & al) || (a.nb01 & al) || (many2 && (a.nb02 & al)) || (many3 && (a.nb03 & al)))
         return false;
     const int64_t row_b = (int64_t)a.K / type_blck(type) * type_bytes(type);
-    const int64_t w_span = (int64_t)a.N * a.nb01 + row_b + 4;
+    const int64_t n_sb = (a.K + Q8_QK - 1) / Q8_QK;
+    // the last super-block's windows reach past a short row by up to one super-block
+    const int64_t w_span = (int64_t)a.N * a.nb01 + n_sb * Q8_QK / type_blck(type) * type_bytes(type) + 8;
     const int64_t n_tt = (a.M + Q8_TOK - 1) / Q8_TOK;
-    const int64_t img_slice = n_tt * (a.K / Q8_QK) * ximg_bytes_rt(type);
+    const int64_t img_slice = n_tt * n_sb * ximg_bytes_rt(type);
     return a.nb01 >= row_b && w_span < (1LL << 32) && img_slice < (1LL << 31);
 }
 
 template <int T>
 static void launch8(const MmArgs &a, uint8_t *ximg, int tr_rows, int tt_tok, int n_tt, int slices, int ksplit,
                     int sb_per, float *part, bool atomic, hipStream_t st) {
-    const int n_sb = a.K / Q8_QK;
+    const int n_sb = (a.K + Q8_QK - 1) / Q8_QK;
     const int n_img = n_tt * (tt_tok / Q8_TOK);   // 64-token images per slice (tokens past M: zeros)
     hipLaunchKernelGGL(mmq8_quant_x<T>, dim3((unsigned)(n_img * (Q8_TOK / 16) * n_sb), slices), dim3(256), 0, st, a, ximg,
                        n_img, n_sb, Moe8{}, atomic ? 1 : 0);
     const int64_t row_b = (int64_t)a.K / QT<T>::blck * QT<T>::bytes;
-    // windows of the last super-block may reach 2 bytes past the row: round the range up to a dword
-    const uint32_t w_extent = (uint32_t)(((int64_t)(a.N - 1) * a.nb01 + row_b + 3) & ~(int64_t)3);
+    const uint32_t w_extent = (uint32_t)((int64_t)(a.N - 1) * a.nb01 + row_b);   // (the kernel rounds it up)
     const int n_rt = (a.N + tr_rows - 1) / tr_rows;
     const unsigned gx = (unsigned)(n_rt * ksplit * n_tt);
     const int remap = ((gx % 8 == 0) ? 1 : 0) | (atomic ? 4 : 0);
@@ -855,7 +872,7 @@ static void launch8(const MmArgs &a, uint8_t *ximg, int tr_rows, int tt_tok, int
 
 hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch) {
     const int slices = a.ne12 * a.ne13;
-    const int n_sb = a.K / Q8_QK;
+    const int n_sb = (a.K + Q8_QK - 1) / Q8_QK;
     // rows x tokens per workgroup: 128-token tiles once they alone give every CU a workgroup
     // (the weight stage then serves twice the tokens); GGML_MI355X_MMQ8_TT / _TR override
     // (measurements; 128 tokens always run 128 rows)
@@ -913,16 +930,16 @@ bool mmq8_id_supported(int type, const MmArgs &a) {
     b.M = a.n_used * a.n_tok;
     b.ne12 = a.n_expert; b.ne13 = 1; b.r2 = 1; b.r3 = 1;   // every expert matrix: alignment of nb02
     if (!mmq8_supported(type, b)) return false;
-    return moe8_tiles(a) <= 65535 && moe8_tiles(a) * (a.K / Q8_QK) * ximg_bytes_rt(type) < (1LL << 31);
+    return moe8_tiles(a) <= 65535 && moe8_tiles(a) * ((a.K + Q8_QK - 1) / Q8_QK) * ximg_bytes_rt(type) < (1LL << 31);
 }
 
 template <int T>
 static void launch8_id(const MmArgs &a, uint8_t *ximg, int n_tiles, const Moe8 &moe, hipStream_t st) {
-    const int n_sb = a.K / Q8_QK;
+    const int n_sb = (a.K + Q8_QK - 1) / Q8_QK;
     hipLaunchKernelGGL((mmq8_quant_x<T, true>), dim3((unsigned)(n_tiles * (Q8_TOK / 16) * n_sb), 1), dim3(256), 0, st, a,
                        ximg, n_tiles, n_sb, moe, 0);
     const int64_t row_b = (int64_t)a.K / QT<T>::blck * QT<T>::bytes;
-    const uint32_t w_extent = (uint32_t)(((int64_t)(a.N - 1) * a.nb01 + row_b + 3) & ~(int64_t)3);
+    const uint32_t w_extent = (uint32_t)((int64_t)(a.N - 1) * a.nb01 + row_b);
     const unsigned gx = (unsigned)((a.N + 127) / 128);
     const int remap = (gx % 8 == 0) ? 1 : 0;
     hipLaunchKernelGGL((mmq8_kernel<T, 64, 128, true>), dim3(gx, (unsigned)n_tiles), dim3(512), 0, st, a,
@@ -930,7 +947,7 @@ static void launch8_id(const MmArgs &a, uint8_t *ximg, int n_tiles, const Moe8 &
 }
 
 hipError_t mmq8_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch) {
-    const int P = a.n_used * a.n_tok, E = a.n_expert, n_sb = a.K / Q8_QK;
+    const int P = a.n_used * a.n_tok, E = a.n_expert, n_sb = (a.K + Q8_QK - 1) / Q8_QK;
     const int n_tiles = (int)moe8_tiles(a);
     const size_t img_bytes = ((size_t)n_tiles * n_sb * ximg_bytes_rt(type) + 255) & ~(size_t)255;
     const size_t map_bytes = sizeof(int) * (2 * (size_t)(E + 1) + P);

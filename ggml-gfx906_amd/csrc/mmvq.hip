@@ -32,9 +32,21 @@ static hipError_t launch_one(const MmArgs &a0, int grid_y, int grid_z, hipStream
     auto kern = mmvq_kernel<T, NC, LPR, RPW, IDS, RAG, XA, BIGK>;
     MmArgs a = a0;
     a.n_it = ((a.K + 63) / 64 + LPR - 1) / LPR;
+    // more than 64 KB of dynamic LDS needs the attribute, once per instantiation. The call fails
+    // inside a stream capture: the error is returned (the capture then fails and the caller runs
+    // the graph eagerly once), and the flag is set only when the call succeeded.
     static bool attr_set = false;   // per-instantiation
-    if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (lds > 64 * 1024 && !attr_set) {
+        // 160 KB of LDS per CU minus the kernel's static arrays
+        hipFuncAttributes fa{};
+        hipError_t e = hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kern));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)(160 * 1024 - fa.sharedSizeBytes));
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return e;
+        }
         attr_set = true;
     }
     const int rows_per_group = MMVQ_WAVES * (WAVE / LPR) * RPW;

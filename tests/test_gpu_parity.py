@@ -156,8 +156,8 @@ def test_rejects_bad_shapes(mm):
 
 
 # ------------------------------------------------------------------------------------------
-# mat-mat (ne11 > 8) path: the int8 MFMA tile (default) and the f16 kernels (GGML_MI355X_MMQ=f16;
-# they also take K % 256 != 0, misaligned rows and MUL_MAT_ID)
+# mat-mat (ne11 > 8) path: the int8 MFMA tile (default, every K) and the f16 kernels (GGML_MI355X_MMQ=f16)
+# on the same shapes, K % 256 != 0 included
 # ------------------------------------------------------------------------------------------
 MMQ_SHAPES = [  # (N, M, K-multiplier) around the tile edges
     (37, 9, 1), (64, 127, 2), (65, 128, 1), (200, 129, 2), (128, 300, 3),
@@ -171,8 +171,8 @@ def test_mmq_tile_edges(mm, t, shape, path, monkeypatch):
     if path == "f16":
         monkeypatch.setenv("GGML_MI355X_MMQ", "f16")
     N, M_, km = shape
-    # 32-block types: K % 64 == 32 for odd multipliers (f16 tiles), K % 256 == 0 for even ones
-    # (the int8 tile); K-quants: any multiple of 256
+    # 32-block types: K % 64 == 32 for odd multipliers (a partial last super-block on the int8
+    # tile), K % 256 == 0 for even ones; K-quants: any multiple of 256
     K = (96 if qref.BLCK[t] == 32 and km % 2 else 256) * km
     w = qref.quantize(t, qref.fill_uniform(N * K, 21), n_per_row=K)
     x = qref.fill_uniform(M_ * K, 22)

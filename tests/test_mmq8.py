@@ -155,6 +155,76 @@ def test_mmq8_activation_range(mm, t):
         assert np.all(got[9 * N:10 * N] == 0.0)
 
 
+@pytest.mark.parametrize("t", [qref.Q4_0, qref.Q8_0], ids=lambda t: qref.NAMES[t])
+@pytest.mark.parametrize("shape", [(64, 16, 32), (37, 9, 96), (200, 129, 288), (130, 200, 96 * 11), (128, 512, 4096 + 96),
+                                   (256, 300, 2048 - 32)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_mmq8_partial_superblock(mm, t, shape):
+    """K not a multiple of 256: the last super-block is partial; its missing
+    32-blocks carry zero activation codes and a zero weight scale. Rows of an odd number of
+    blocks (K = 32, 96, ...) are 2-byte aligned every other row."""
+    N, M_, K = shape
+    case(mm, t, N, M_, K, seed=13)
+
+
+@pytest.mark.parametrize("t", [qref.Q4_0, qref.Q8_0], ids=lambda t: qref.NAMES[t])
+@pytest.mark.parametrize("ksplit", [2, 3])
+def test_mmq8_partial_superblock_ksplit(mm, t, ksplit):
+    """split-K whose last split ends in the partial super-block"""
+    case(mm, t, 192, 96, 256 * 4 + 160, seed=17, ksplit=ksplit)
+
+
+@pytest.mark.parametrize("t", [qref.Q4_0, qref.Q8_0, qref.Q6_K], ids=lambda t: qref.NAMES[t])
+@pytest.mark.parametrize("K", [256, 96 * 5], ids=lambda k: f"k{k}")
+def test_mmq8_matrix_at_2_mod_4(mm, t, K):
+    """the weight matrix itself starts at 2 mod 4 (a view at an odd block offset): the buffer is
+    based at its dword floor and every window realigned from its own offset"""
+    if qref.BLCK[t] == 256 and K % 256:
+        pytest.skip("K-quants: K is a multiple of 256")
+    from test_gpu_parity import check_guard, guarded_out
+    N, M_ = 150, 70
+    w = qref.quantize(t, qref.fill_uniform(N * K, 19), n_per_row=K)
+    x = qref.fill_uniform(M_ * K, 20)
+    raw = np.zeros(w.nbytes + 2, np.uint8)
+    raw[2:] = w.view(np.uint8)
+    dw = torch.from_numpy(raw).cuda()
+    dx = torch.from_numpy(x.copy()).cuda()
+    nel = N * M_
+    dout = guarded_out(nel)
+    A = mm.tensor(t, dw.data_ptr() + 2, [K, N, 1, 1], qref.contiguous_nb(t, [K, N, 1, 1]))
+    B = mm.tensor(qref.F32, dx.data_ptr(), [K, M_, 1, 1], qref.contiguous_nb(qref.F32, [K, M_, 1, 1]))
+    D = mm.tensor(qref.F32, dout.data_ptr() + 4 * 1024, [N, M_, 1, 1], qref.contiguous_nb(qref.F32, [N, M_, 1, 1]))
+    mm.mul_mat(A, B, D)
+    torch.cuda.synchronize()
+    got = check_guard(dout, nel)
+    a = G.Operand(t, w, [K, N, 1, 1], qref.contiguous_nb(t, [K, N, 1, 1]))
+    b = G.Operand(qref.F32, x, [K, M_, 1, 1], qref.contiguous_nb(qref.F32, [K, M_, 1, 1]))
+    assert np.all(np.isfinite(got))
+    assert qref.nmse(got, G.oracle_mul_mat(a, b, [N, M_, 1, 1])) <= TIGHT[t]
+
+
+@pytest.mark.parametrize("t,big", [(qref.Q8_0, 7.0e4), (qref.Q4_0, 1.0e5)])
+@pytest.mark.parametrize("M_", [200, 512])
+@pytest.mark.parametrize("K", [96, 96 * 7])
+def test_mmq8_huge_scales_ragged_k(mm, t, big, M_, K):
+    """block scales far past the f16 tile's range (d > 511) with K = 96 k, the
+    shapes that used to fall to the f16 LDS-staged tiles; now on the exact int8 tile"""
+    N = 160
+    f = qref.fill_uniform(N * K, 79).reshape(N, K)
+    f[5::7] *= big
+    w = qref.quantize(t, f.reshape(-1), n_per_row=K)
+    x = qref.fill_uniform(M_ * K, 80)
+    a = G.Operand(t, w, [K, N, 1, 1], qref.contiguous_nb(t, [K, N, 1, 1]))
+    b = G.Operand(qref.F32, x, [K, M_, 1, 1], qref.contiguous_nb(qref.F32, [K, M_, 1, 1]))
+    got = run_mul_mat(mm, a, b, [N, M_, 1, 1])
+    want = G.oracle_mul_mat(a, b, [N, M_, 1, 1])
+    assert np.all(np.isfinite(got))
+    assert qref.nmse(got, want) <= TIGHT[t]
+    keep = np.ones(N, bool)
+    keep[5::7] = False
+    assert qref.nmse(got.reshape(M_, N)[:, keep], want.reshape(M_, N)[:, keep]) <= TIGHT[t]
+
+
 def test_mmq8_q8_0_config3(mm):
     """BASELINE configs[3]: Q8_0 4096 x 4096 x 512, every element against the threaded oracle"""
     t, N, M_, K = qref.Q8_0, 4096, 512, 4096
