@@ -195,6 +195,13 @@ TensorView tv(const struct ggml_tensor *t) {
     return v;
 }
 
+bool is_copy_op(int op) { return op == GGMLABI_OP_CPY || op == GGMLABI_OP_CONT || op == GGMLABI_OP_DUP; }
+
+// a copy into or out of a quantized tensor (mi355x::cpy: quantize, dequantize, block copy)
+bool is_quant_copy(const struct ggml_tensor *t) {
+    return is_copy_op(t->op) && (is_hot_quant(t->type) || is_hot_quant(t->src[0]->type));
+}
+
 bool graph_op_of(const struct ggml_tensor *node, GraphOp &g) {
     g = GraphOp{};
     switch (node->op) {
@@ -1041,7 +1048,7 @@ int next_compute(const struct ggml_cgraph *g, int i, int n) {
 }
 
 bool is_plain_copy(const struct ggml_tensor *t) {
-    return (t->op == GGMLABI_OP_CPY || t->op == GGMLABI_OP_CONT || t->op == GGMLABI_OP_DUP) && !is_hot_quant(t->type);
+    return is_copy_op(t->op) && !is_hot_quant(t->type) && !is_hot_quant(t->src[0]->type);
 }
 
 // two independent copies with only view nodes between them (GPT-2's K and V cache writes,
@@ -1261,8 +1268,8 @@ enum ggml_status run_nodes(BackendCtx *c, struct ggml_cgraph *g, bool quiet) {
             rc = mul_mat_id(tv(node->src[0]), tv(node->src[1]), tv(node->src[2]), tv(node), c->stream, c->scratch);
         } else if (node->op == GGMLABI_OP_GET_ROWS) {
             rc = get_rows(tv(node->src[0]), tv(node->src[1]), tv(node), c->stream);
-        } else if (node->op == GGMLABI_OP_CPY && is_hot_quant(node->type)) {
-            rc = quantize(tv(node->src[0]), tv(node), c->stream);   // node is the view of src[1]
+        } else if (is_quant_copy(node)) {
+            rc = cpy(tv(node->src[0]), tv(node), c->stream);   // for CPY node is the view of src[1]
         } else if (graph_op_of(node, gop)) {
             rc = run_graph_op(gop, c->stream);
         } else {
@@ -1501,9 +1508,12 @@ bool dv_supports_op(ggml_backend_dev_t d, const struct ggml_tensor *op) {
         // GET_ROWS of the hot quant types / f32 (dequantized rows, bit-exact), like get_rows_cuda
         case GGMLABI_OP_GET_ROWS:
             return check_get_rows(tv(op->src[0]), tv(op->src[1]), tv(op)) == GGML_MI355X_OK;
-        // f32 -> Q4_0 / Q8_0 copies (the reference GPU's cpy_f32_q subset of these types)
+        // copies into / out of the hot types: f32 -> Q4_0 / Q8_0 (cpy_f32_q), Q* -> f32 (cpy_q_f32,
+        // cpy.cu:94) and same-type block copies
         case GGMLABI_OP_CPY:
-            if (is_hot_quant(op->type)) return check_quantize(tv(op->src[0]), tv(op)) == GGML_MI355X_OK;
+        case GGMLABI_OP_CONT:
+        case GGMLABI_OP_DUP:
+            if (is_quant_copy(op)) return check_cpy(tv(op->src[0]), tv(op)) == GGML_MI355X_OK;
             break;
         default:
             break;

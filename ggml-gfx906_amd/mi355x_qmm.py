@@ -70,6 +70,8 @@ def lib():
         L.ggml_mi355x_supports_mul_mat.argtypes = [P, P]
         L.ggml_mi355x_get_rows.argtypes = [P, P, P, C.c_void_p]
         L.ggml_mi355x_quantize.argtypes = [P, P, C.c_void_p]
+        L.ggml_mi355x_cpy.argtypes = [P, P, C.c_void_p]
+        L.ggml_mi355x_device_error.restype = C.c_int
         L.ggml_mi355x_strerror.restype = C.c_char_p
         L.ggml_mi355x_strerror.argtypes = [C.c_int]
         L.ggml_backend_init.restype = C.c_void_p
@@ -136,6 +138,16 @@ def get_rows(a: MmTensor, rows: MmTensor, d: MmTensor, stream=None) -> None:
 def quantize(src: MmTensor, dst: MmTensor, stream=None) -> None:
     """dst (Q4_0 / Q8_0) = quantize_row_*_ref(src f32) on the device (GGML_OP_CPY f32 -> q)"""
     _check(lib().ggml_mi355x_quantize(C.byref(src), C.byref(dst), _stream_ptr(stream)), "quantize")
+
+
+def cpy(src: MmTensor, dst: MmTensor, stream=None) -> None:
+    """dst = src (GGML_OP_CPY): f32 -> Q4_0/Q8_0, hot quant -> f32 (dup_q), hot -> same type"""
+    _check(lib().ggml_mi355x_cpy(C.byref(src), C.byref(dst), _stream_ptr(stream)), "cpy")
+
+
+def device_error() -> int:
+    """returns and clears the device error word (call after synchronizing the stream)"""
+    return lib().ggml_mi355x_device_error()
 
 
 def mul_mat_id(a: MmTensor, b: MmTensor, ids: MmTensor, d: MmTensor, stream=None) -> None:

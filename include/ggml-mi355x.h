@@ -99,9 +99,25 @@ GGML_MI355X_API int ggml_mi355x_dequantize(int32_t type, const void *src, float 
  * src/ggml.c:3617-3637; CPU src/ggml-cpu/ops.cpp:5121-5163): src0 [ne00, ne01, ne02, ne03] of a
  * hot quant type or f32, rows [r, ne02, ne03] i32, dst [ne00, r, ne02, ne03] f32, each row the
  * bit-exact dequantize_row_* of the selected src0 row. Replaces get_rows_cuda
- * (src/ggml-cuda/getrows.cu). Indices outside [0, ne01) are clamped (the reference asserts). */
+ * (src/ggml-cuda/getrows.cu). An index outside [0, ne01) (the reference GGML_ASSERTs,
+ * src/ggml-cpu/ops.cpp:5157) writes nothing for that row and raises the device error word that
+ * ggml_mi355x_device_error() returns once the stream has synchronized. */
 GGML_MI355X_API int ggml_mi355x_get_rows(const ggml_mi355x_tensor *src0, const ggml_mi355x_tensor *rows,
                                          ggml_mi355x_tensor *dst, void *stream);
+
+/* Returns and clears the device error word (nonzero: a kernel met a precondition the reference
+ * asserts on, e.g. a GET_ROWS index out of range). Call after the stream synchronized. */
+GGML_MI355X_API int ggml_mi355x_device_error(void);
+
+/* dst = src with GGML_OP_CPY semantics (ggml_cpy, reference src/ggml.c; CPU dup_q
+ * src/ggml-cpu/ops.cpp:1105-1154 and dup_bytes :956-1103) between this path's types:
+ *   f32 -> Q4_0 / Q8_0     as ggml_mi355x_quantize (same shapes);
+ *   Q4_0/Q8_0/Q4_K/Q5_K/Q6_K -> f32   bit-exact dequantize_row_* of every block, placed where
+ *                          dup_q places it (same element count; dst rows hold whole blocks or
+ *                          dst is contiguous);
+ *   hot type -> same type  block copy (same element count, whole blocks per row).
+ * Replaces ggml_cpy_q4_0_f32_cuda / ggml_cpy_q8_0_f32_cuda (src/ggml-cuda/cpy.cu:94, :362-366). */
+GGML_MI355X_API int ggml_mi355x_cpy(const ggml_mi355x_tensor *src, ggml_mi355x_tensor *dst, void *stream);
 
 /* dst = src converted f32 -> Q4_0 or Q8_0 (GGML_OP_CPY into a quantized tensor), bit-exact with
  * quantize_row_q4_0_ref / quantize_row_q8_0_ref (reference src/ggml-quants.c:36-71, 199-222).

@@ -64,9 +64,30 @@ def test_backend_ops_mul_mat_id():
     assert _executed_hot_f32(out, "MUL_MAT_ID") >= 114
 
 
-@pytest.mark.parametrize("op", ["GET_ROWS", "CPY"])
-def test_backend_ops_rows_and_quantize(op):
-    _tbo(op)
+def test_backend_ops_get_rows():
+    _tbo("GET_ROWS")
+
+
+def _executed_cpy(out: str) -> dict:
+    """executed (OK) CPY cases per (type_src, type_dst)"""
+    n = {}
+    for line in out.splitlines():
+        line = line.strip()
+        m = re.match(r"CPY\(type_src=(\w+),type_dst=(\w+),", line)
+        if m and line.endswith("OK"):
+            n[m.groups()] = n.get(m.groups(), 0) + 1
+    return n
+
+
+def test_backend_ops_cpy():
+    """CPY (tests/test-backend-ops.cpp:5576-5602): f32 -> Q4_0/Q8_0, every hot type -> f32
+    (cpy_q_f32) and every hot type -> itself must execute on MI355X0, not fall back"""
+    n = _executed_cpy(_tbo("CPY"))
+    for t in HOT:
+        assert n.get((t, "f32"), 0) >= 2, (t, n)        # contiguous + cpy by rows
+        assert n.get((t, t), 0) >= 9, (t, n)            # k = 1..3 x three permutes
+    for t in ("q4_0", "q8_0"):
+        assert n.get(("f32", t), 0) >= 2, (t, n)
 
 
 @pytest.mark.parametrize("shards,fractions", [(1, None), (2, None), (2, "1,3"), (3, None)])

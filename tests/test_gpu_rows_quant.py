@@ -114,3 +114,116 @@ def test_rejects_unsupported(mm):
     Q = mm.tensor(qref.Q4_K, q.data_ptr(), [64, 1, 1, 1], [144, 144, 144, 144])
     with pytest.raises(mm.Mi355xError):
         mm.quantize(S, Q)            # K-quant device quantization is not implemented
+
+
+# ---- GGML_OP_CPY out of a quantized tensor (cpy_q_f32, reference src/ggml-cuda/cpy.cu:94;
+# ggml-cpu dup_q src/ggml-cpu/ops.cpp:1105-1154, dup_bytes :956-1103) ----------------------
+
+def _logical_rows(src: np.ndarray, t: int, ne, nb) -> list:
+    """the quantized rows of a 4-d view in row-major logical order (bytes of each row)"""
+    rb = qref.row_size(t, ne[0])
+    out = []
+    for i3 in range(ne[3]):
+        for i2 in range(ne[2]):
+            for i1 in range(ne[1]):
+                o = i1 * nb[1] + i2 * nb[2] + i3 * nb[3]
+                out.append(src[o:o + rb])
+    return out
+
+
+def _permuted_view(t, ne):
+    """a [ne0, ne2, ne1, ne3] view of a contiguous [ne0, ne1, ne2, ne3] tensor (dims 1, 2 swapped)"""
+    nb = qref.contiguous_nb(t, ne)
+    return [ne[0], ne[2], ne[1], ne[3]], [nb[0], nb[2], nb[1], nb[3]]
+
+
+@pytest.mark.parametrize("t", list(qref.HOT_TYPES), ids=lambda t: qref.NAMES[t])
+@pytest.mark.parametrize("layout", ["contig", "permuted", "reshaped_dst", "padded_dst"])
+def test_cpy_q_to_f32_bit_exact(mm, t, layout):
+    """CPY Q* -> f32 (test-backend-ops test_cpy, tests/test-backend-ops.cpp:5560-5600, with the
+    src permutes it runs): every element the bit-exact dequantize_row_* value at dup_q's place."""
+    blck = qref.BLCK[t]
+    ne = [2 * blck, 3, 2, 2]
+    src = G.weights_bytes(t, ne, 4242 + t)
+    if layout == "permuted":
+        lne, lnb = _permuted_view(t, ne)
+    else:
+        lne, lnb = ne, qref.contiguous_nb(t, ne)
+    rows = _logical_rows(src, t, lne, lnb)
+    want = np.concatenate([qref.dequantize(t, r, lne[0]) for r in rows])
+    nel = int(np.prod(lne))
+    ds = dev(src)
+    if layout == "padded_dst":        # dst rows hold whole blocks, 64 floats of padding after each
+        pad = 64
+        out = torch.full((nel // lne[0], lne[0] + pad), -7.0, dtype=torch.float32, device="cuda")
+        dne = [lne[0], lne[1], lne[2], lne[3]]
+        row = 4 * (lne[0] + pad)
+        dnb = [4, row, row * lne[1], row * lne[1] * lne[2]]
+    else:
+        out = torch.full((nel,), -7.0, dtype=torch.float32, device="cuda")
+        dne = [nel // 4, 2, 2, 1] if layout == "reshaped_dst" else lne   # contiguous: any shape
+        dnb = qref.contiguous_nb(qref.F32, dne)
+    S = mm.tensor(t, ds.data_ptr(), lne, lnb)
+    D = mm.tensor(qref.F32, out.data_ptr(), dne, dnb)
+    mm.cpy(S, D)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    if layout == "padded_dst":
+        assert (got[:, lne[0]:] == -7.0).all(), "padding written"
+        got = got[:, :lne[0]]
+    np.testing.assert_array_equal(got.reshape(-1).view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("t", list(qref.HOT_TYPES), ids=lambda t: qref.NAMES[t])
+def test_cpy_q_same_type_blocks(mm, t):
+    """CPY of a permuted quantized view into a contiguous tensor of the same type: the blocks in
+    logical order, byte for byte (dup_bytes)."""
+    blck = qref.BLCK[t]
+    ne = [3 * blck, 2, 3, 1]
+    src = G.weights_bytes(t, ne, 99 + t)
+    lne, lnb = _permuted_view(t, ne)
+    want = np.concatenate(_logical_rows(src, t, lne, lnb))
+    ds = dev(src)
+    out = torch.zeros(want.size, dtype=torch.uint8, device="cuda")
+    mm.cpy(mm.tensor(t, ds.data_ptr(), lne, lnb), mm.tensor(t, out.data_ptr(), lne, qref.contiguous_nb(t, lne)))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), want)
+
+
+def test_cpy_q_rejects(mm):
+    t = qref.Q4_0
+    q = torch.zeros(18 * 4, dtype=torch.uint8, device="cuda")
+    f = torch.zeros(128, dtype=torch.float32, device="cuda")
+    S = mm.tensor(t, q.data_ptr(), [64, 2], qref.contiguous_nb(t, [64, 2]))
+    with pytest.raises(mm.Mi355xError):     # element counts differ
+        mm.cpy(S, mm.tensor(qref.F32, f.data_ptr(), [64, 1], qref.contiguous_nb(qref.F32, [64, 1])))
+    with pytest.raises(mm.Mi355xError):     # dst rows of 16 floats split blocks and dst is not contiguous
+        mm.cpy(S, mm.tensor(qref.F32, f.data_ptr(), [16, 8, 1, 1], [4, 128, 1024, 1024]))
+    with pytest.raises(mm.Mi355xError):     # Q4_0 -> Q8_0 is not a copy this path does
+        mm.cpy(S, mm.tensor(qref.Q8_0, q.data_ptr(), [64, 2], qref.contiguous_nb(qref.Q8_0, [64, 2])))
+
+
+@pytest.mark.parametrize("t", [qref.F32, qref.Q4_0], ids=["f32", "q4_0"])
+def test_get_rows_out_of_range_raises(mm, t):
+    """an index outside [0, ne01) is the reference's GGML_ASSERT (ops.cpp:5157): the device error
+    word is raised and that row is not written; in-range rows are still right"""
+    n, m = 64, 5
+    src = G.weights_bytes(t, [n, m, 1, 1], 7)
+    rows = np.array([1, m, -1, 3], dtype=np.int32)
+    ds, di = dev(src), dev(rows)
+    out = torch.full((4, n), -3.0, dtype=torch.float32, device="cuda")
+    assert mm.device_error() in (0, 1)      # clear anything a previous test left
+    A = mm.tensor(t, ds.data_ptr(), [n, m], qref.contiguous_nb(t, [n, m]) if t != qref.F32 else [4, 4 * n, 4 * n * m, 4 * n * m])
+    R = mm.tensor(qref.I32, di.data_ptr(), [4, 1, 1, 1], [4, 16, 16, 16])
+    D = mm.tensor(qref.F32, out.data_ptr(), [n, 4], qref.contiguous_nb(qref.F32, [n, 4]))
+    mm.get_rows(A, R, D)
+    torch.cuda.synchronize()
+    assert mm.device_error() == 1
+    assert mm.device_error() == 0          # reading clears it
+    got = out.cpu().numpy()
+    assert (got[1] == -3.0).all() and (got[2] == -3.0).all()
+    rb = qref.row_size(t, n) if t != qref.F32 else 4 * n
+    for k, r in ((0, 1), (3, 3)):
+        row = src[r * rb:(r + 1) * rb]
+        want = row.view(np.float32) if t == qref.F32 else qref.dequantize(t, row, n)
+        np.testing.assert_array_equal(got[k].view(np.uint32), want.view(np.uint32))
