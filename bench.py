@@ -93,7 +93,8 @@ class MatVecSet:
     activations [K, M, batch] and outputs [N, M, batch]: one launch = one MUL_MAT over the
     whole stack (ne02 = ne12 = batch), rotating over the copies."""
 
-    def __init__(self, torch, t: int, K: int, N: int, Mc: int, batch: int, copies: int, seed: int = 1234):
+    def __init__(self, torch, t: int, K: int, N: int, Mc: int, batch: int, copies: int, seed: int = 1234,
+                 repacked: bool = False):
         self.torch, self.t, self.K, self.N, self.Mc, self.batch, self.copies = torch, t, K, N, Mc, batch, copies
         host = synthetic_weights(t, N, K, seed)                       # one matrix, replicated on device
         one = torch.from_numpy(host.reshape(-1)).cuda()
@@ -107,9 +108,21 @@ class MatVecSet:
         self.D = M.tensor(M.F32, self.y.data_ptr(), [N, Mc, batch, 1], M.contiguous_nb(M.F32, [N, Mc, batch]))
         self.bytes = alg_bytes(t, K, N, Mc) * batch
         self.flops = 2.0 * K * N * Mc * batch
+        # repacked: each weight copy also held in the int8 tile's fragment layout (made once, as a
+        # repacked weight buffer does at upload), and the launches use it
+        self.rp = None
+        if repacked:
+            n = M.repack_size(self.A[0])
+            self.rp = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(copies)]
+            for a, r in zip(self.A, self.rp):
+                M.repack(a, r.data_ptr(), n)
+            torch.cuda.synchronize()
 
     def launch(self, i: int, stream=None) -> None:
-        M.mul_mat(self.A[i % self.copies], self.B, self.D, stream)
+        if self.rp is not None:
+            M.mul_mat_repacked(self.A[i % self.copies], self.rp[i % self.copies].data_ptr(), self.B, self.D, stream)
+        else:
+            M.mul_mat(self.A[i % self.copies], self.B, self.D, stream)
 
     def launch_us(self, reps: int) -> float:
         """mean device time per launch: HIP events on the launch stream around `reps` back-to-back

@@ -104,6 +104,10 @@ struct DeviceCtx {
     std::string name, desc;
     struct ggml_backend_buffer_type buft {};
     std::string buft_name;
+    // repacked-weight buffer type (an "extra" buffer type, ggml_backend_dev_get_extra_bufts)
+    struct ggml_backend_buffer_type rp_buft {};
+    std::string rp_buft_name;
+    ggml_backend_buffer_type_t extra_bufts[2] = {nullptr, nullptr};
 };
 
 struct BufferCtx {
@@ -298,6 +302,61 @@ const struct ggml_backend_buffer_i BUFFER_IFACE = {
 };
 
 // ------------------------------------------------------------------------------------------
+// repacked-weight buffer ("MI355X<i>_Repack", offered through ggml_backend_dev_get_extra_bufts as
+// the reference CPU backend offers its repack buffer, src/ggml-cpu/repack.cpp:1967 and
+// ggml-cpu.cpp:619): a quantized tensor keeps its ggml bytes at `data` (so GET_ROWS, CPY, the
+// mat-vec and get_tensor read it as usual) and gets, right behind them, the int8 tile's repacked
+// copy (mmq8.hip: int8 codes in MFMA-fragment order + f32 block scales), pointed to by
+// tensor->extra and remade by every write to the tensor. MUL_MAT with more than 8 tokens on such
+// a weight runs the tile on the copy: no per-call weight decode.
+// ------------------------------------------------------------------------------------------
+size_t rp_extra_bytes(const struct ggml_tensor *t) {
+    if (t->view_src != nullptr) return 0;
+    TensorView v = tv(t);
+    v.data = nullptr;
+    const size_t n = repack_size(v);
+    return n ? n + 256 : 0;   // + alignment slack of the copy
+}
+
+uint8_t *rp_extra_ptr(const struct ggml_tensor *t) {
+    const uintptr_t end = reinterpret_cast<uintptr_t>(t->data) + ggml_base().nbytes(t);
+    return reinterpret_cast<uint8_t *>((end + 255) & ~(uintptr_t)255);
+}
+
+void rp_refresh(BufferCtx *c, struct ggml_tensor *t) {
+    if (t->extra == nullptr) return;
+    const size_t n = rp_extra_bytes(t) - 256;
+    HIP_OK(hipSetDevice(c->device));
+    if (repack(tv(t), t->extra, n, nullptr) != GGML_MI355X_OK) fatal("repack", hipErrorInvalidValue);
+    HIP_OK(hipStreamSynchronize(nullptr));
+}
+
+enum ggml_status rp_init_tensor(ggml_backend_buffer_t, struct ggml_tensor *t) {
+    t->extra = rp_extra_bytes(t) ? rp_extra_ptr(t) : nullptr;
+    return GGML_STATUS_SUCCESS;
+}
+
+void rp_memset(ggml_backend_buffer_t b, struct ggml_tensor *t, uint8_t v, size_t off, size_t n) {
+    buf_memset(b, t, v, off, n);
+    rp_refresh(static_cast<BufferCtx *>(b->context), t);
+}
+
+void rp_set(ggml_backend_buffer_t b, struct ggml_tensor *t, const void *data, size_t off, size_t n) {
+    buf_set(b, t, data, off, n);
+    rp_refresh(static_cast<BufferCtx *>(b->context), t);
+}
+
+bool rp_cpy(ggml_backend_buffer_t b, const struct ggml_tensor *src, struct ggml_tensor *dst) {
+    if (!buf_cpy(b, src, dst)) return false;
+    rp_refresh(static_cast<BufferCtx *>(b->context), dst);
+    return true;
+}
+
+const struct ggml_backend_buffer_i RP_BUFFER_IFACE = {
+    buf_free, buf_base, rp_init_tensor, rp_memset, rp_set, buf_get, rp_cpy, buf_clear, nullptr,
+};
+
+// ------------------------------------------------------------------------------------------
 // buffer type
 // ------------------------------------------------------------------------------------------
 const char *buft_name(ggml_backend_buffer_type_t bt) { return static_cast<DeviceCtx *>(bt->context)->buft_name.c_str(); }
@@ -317,7 +376,8 @@ ggml_backend_buffer_t buft_alloc(ggml_backend_buffer_type_t bt, size_t size) {
         return nullptr;
     }
     logf("alloc %zu bytes on device %d -> %p\n", size, d->device, p);
-    return ggml_base().buffer_init(bt, BUFFER_IFACE, new BufferCtx{d->device, p}, size);
+    const bool rp = bt == &d->rp_buft;
+    return ggml_base().buffer_init(bt, rp ? RP_BUFFER_IFACE : BUFFER_IFACE, new BufferCtx{d->device, p}, size);
 }
 
 size_t buft_align(ggml_backend_buffer_type_t) { return 128; }
@@ -329,7 +389,23 @@ const struct ggml_backend_buffer_type_i BUFT_IFACE = {
     buft_name, buft_alloc, buft_align, buft_max, buft_alloc_size, buft_is_host,
 };
 
-bool is_our_buft(ggml_backend_buffer_type_t buft) { return buft && buft->iface.get_name == buft_name; }
+const char *rp_buft_name(ggml_backend_buffer_type_t bt) { return static_cast<DeviceCtx *>(bt->context)->rp_buft_name.c_str(); }
+size_t rp_buft_alloc_size(ggml_backend_buffer_type_t, const struct ggml_tensor *t) {
+    return ggml_base().nbytes(t) + rp_extra_bytes(t);
+}
+
+const struct ggml_backend_buffer_type_i RP_BUFT_IFACE = {
+    rp_buft_name, buft_alloc, buft_align, buft_max, rp_buft_alloc_size, buft_is_host,
+};
+
+bool is_rp_buft(ggml_backend_buffer_type_t buft) { return buft && buft->iface.get_name == rp_buft_name; }
+// device memory of one of our devices (plain or repacked-weight buffer: both hold BufferCtx)
+bool is_our_buft(ggml_backend_buffer_type_t buft) { return buft && (buft->iface.get_name == buft_name || is_rp_buft(buft)); }
+
+// src0's repacked copy, when it lives in a repacked-weight buffer (else nullptr)
+const void *repacked_of(const struct ggml_tensor *a) {
+    return a->buffer && is_rp_buft(a->buffer->buft) && a->view_src == nullptr ? a->extra : nullptr;
+}
 
 // ------------------------------------------------------------------------------------------
 // row-split ("tensor parallel") buffer type: ggml_backend_split_buffer_type(main, tensor_split)
@@ -1263,7 +1339,7 @@ enum ggml_status run_nodes(BackendCtx *c, struct ggml_cgraph *g, bool quiet) {
         } else if (node->op == GGMLABI_OP_MUL_MAT && node->src[0]->buffer && is_split_buft(node->src[0]->buffer->buft)) {
             rc = be_split_mul_mat(c, node);
         } else if (node->op == GGMLABI_OP_MUL_MAT && is_hot_quant(node->src[0]->type)) {
-            rc = mul_mat(tv(node->src[0]), tv(node->src[1]), tv(node), c->stream, c->scratch);
+            rc = mul_mat_rp(tv(node->src[0]), repacked_of(node->src[0]), tv(node->src[1]), tv(node), c->stream, c->scratch);
         } else if (node->op == GGMLABI_OP_MUL_MAT_ID) {
             rc = mul_mat_id(tv(node->src[0]), tv(node->src[1]), tv(node->src[2]), tv(node), c->stream, c->scratch);
         } else if (node->op == GGMLABI_OP_GET_ROWS) {
@@ -1592,9 +1668,13 @@ struct ggml_backend_feature FEATURES[] = {
 
 struct ggml_backend_feature *rg_features(ggml_backend_reg_t) { return FEATURES; }
 
+// ggml_backend_dev_get_extra_bufts (reference include/ggml-backend.h:192): NULL-terminated
+ggml_backend_buffer_type_t *dv_extra_bufts(ggml_backend_dev_t d) { return dev_ctx(d)->extra_bufts; }
+
 void *rg_proc(ggml_backend_reg_t, const char *name) {
     if (strcmp(name, "ggml_backend_get_features") == 0) return reinterpret_cast<void *>(rg_features);
     if (strcmp(name, "ggml_backend_split_buffer_type") == 0) return reinterpret_cast<void *>(mi355x_split_buffer_type);
+    if (strcmp(name, "ggml_backend_dev_get_extra_bufts") == 0) return reinterpret_cast<void *>(dv_extra_bufts);
     if (strcmp(name, "ggml_backend_register_host_buffer") == 0) return reinterpret_cast<void *>(mi355x_register_host_buffer);
     if (strcmp(name, "ggml_backend_unregister_host_buffer") == 0) return reinterpret_cast<void *>(mi355x_unregister_host_buffer);
     if (strcmp(name, "ggml_mi355x_mul_mat") == 0) return reinterpret_cast<void *>(ggml_mi355x_mul_mat);
@@ -1624,6 +1704,11 @@ Registry &registry() {
             dc->buft.iface = BUFT_IFACE;
             dc->buft.device = dev.get();
             dc->buft.context = dc.get();
+            dc->rp_buft_name = dc->buft_name + "_Repack";
+            dc->rp_buft.iface = RP_BUFT_IFACE;
+            dc->rp_buft.device = dev.get();
+            dc->rp_buft.context = dc.get();
+            dc->extra_bufts[0] = &dc->rp_buft;
             R->ctxs.push_back(std::move(dc));
             R->devs.push_back(std::move(dev));
         };

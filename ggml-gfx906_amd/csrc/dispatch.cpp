@@ -55,6 +55,7 @@ bool mmq_id_supported(int type, const MmArgs &a);
 hipError_t mmq_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
 bool mmq8_supported(int type, const MmArgs &a);
 hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
+hipError_t mmq8r_launch(int type, const MmArgs &a, const void *rp, int ne02, int n_mat, hipStream_t st, Scratch &scratch);
 bool mmq8_id_supported(int type, const MmArgs &a);
 hipError_t mmq8_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
 
@@ -179,7 +180,40 @@ static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st
     return hipSuccess;
 }
 
+static RpSrcView rp_view(const TensorView &w) {
+    return RpSrcView{w.data, (int64_t)w.nb[1], (int64_t)w.nb[2], (int64_t)w.nb[3], (int)w.ne[0], (int)w.ne[1], (int)w.ne[2],
+                     (int)(w.ne[2] * w.ne[3])};
+}
+
+size_t repack_size(const TensorView &w) {
+    if (!is_hot_quant(w.type) || (int64_t)w.nb[0] != type_bytes(w.type) || w.ne[0] <= 0 || w.ne[1] <= 0) return 0;
+    if (w.ne[0] > (1 << 24) || w.ne[1] > (1LL << 31) - 1 || w.ne[2] * w.ne[3] > (1LL << 31) - 1) return 0;
+    const RpSrcView v = rp_view(w);
+    return repack_supported(w.type, v) ? rp_layout(w.type, v.K, v.N, v.n_mat).bytes : 0;
+}
+
+int repack(const TensorView &w, void *dst, size_t bytes, hipStream_t st) {
+    const size_t need = repack_size(w);
+    if (need == 0) return GGML_MI355X_EINVAL;
+    if (bytes < need || dst == nullptr) return GGML_MI355X_EINVAL;
+    return repack_launch(w.type, rp_view(w), dst, st) == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
+}
+
+// mat-mat on repacked weights, per call: from this many tokens the int8 tile reads a repacked
+// copy of src0 (made in scratch by one extra launch when the caller has none); below it, and for
+// layouts the repack does not take, the in-place int8 tile. GGML_MI355X_MMQ_REPACK_MIN overrides
+// (measurements: 0 = never repack per call).
+static int repack_min_tokens() {
+    const char *e = getenv("GGML_MI355X_MMQ_REPACK_MIN");   // per call: tests switch it
+    return e ? atoi(e) : 1 << 30;
+}
+
 int mul_mat(const TensorView &a, const TensorView &b, const TensorView &d, hipStream_t st, Scratch &scratch) {
+    return mul_mat_rp(a, nullptr, b, d, st, scratch);
+}
+
+int mul_mat_rp(const TensorView &a, const void *rp, const TensorView &b, const TensorView &d, hipStream_t st,
+               Scratch &scratch) {
     const int rc = check_mul_mat(a, b, d);
     if (rc != GGML_MI355X_OK) return rc;
     if (a.ne[1] == 0 || b.ne[1] == 0 || b.ne[2] == 0 || b.ne[3] == 0) return GGML_MI355X_OK;
@@ -187,7 +221,11 @@ int mul_mat(const TensorView &a, const TensorView &b, const TensorView &d, hipSt
     std::lock_guard<std::mutex> hold(scratch.mu);   // until the scratch users are queued
     hipError_t e;
     const bool f16 = mmq_f16_forced();
-    if (m.M > 8 && !f16 && mmq8_supported(a.type, m)) e = mmq8_launch(a.type, m, st, scratch);
+    const int n_mat = (int)(a.ne[2] * a.ne[3]);
+    const int rmin = repack_min_tokens();
+    const bool use_rp = m.M > 8 && !f16 && (rp != nullptr || (rmin > 0 && m.M >= rmin)) && repack_size(a) != 0;
+    if (use_rp) e = mmq8r_launch(a.type, m, rp, (int)a.ne[2], n_mat, st, scratch);
+    else if (m.M > 8 && !f16 && mmq8_supported(a.type, m)) e = mmq8_launch(a.type, m, st, scratch);
     else if (m.M > 8 && f16 && mmq_supported(a.type, m)) e = mmq_launch(a.type, m, st, scratch);
     else e = run_mmvq(a.type, m, 0, m.M, st);
     if (e == hipErrorOutOfMemory) return GGML_MI355X_ENOMEM;
@@ -496,6 +534,25 @@ int ggml_mi355x_mul_mat(const ggml_mi355x_tensor *src0, const ggml_mi355x_tensor
     if (!src0 || !src1 || !dst) return GGML_MI355X_EINVAL;
     return mul_mat(view_of(src0), view_of(src1), view_of(dst), static_cast<hipStream_t>(stream),
                   scratch_for(static_cast<hipStream_t>(stream)));
+}
+
+int ggml_mi355x_repack_size(const ggml_mi355x_tensor *src0, size_t *bytes) {
+    if (!src0 || !bytes) return GGML_MI355X_EINVAL;
+    *bytes = repack_size(view_of(src0));
+    return *bytes ? GGML_MI355X_OK : GGML_MI355X_EINVAL;
+}
+
+int ggml_mi355x_repack(const ggml_mi355x_tensor *src0, void *dst, size_t bytes, void *stream) {
+    if (!src0) return GGML_MI355X_EINVAL;
+    return repack(view_of(src0), dst, bytes, static_cast<hipStream_t>(stream));
+}
+
+int ggml_mi355x_mul_mat_repacked(const ggml_mi355x_tensor *src0, const void *repacked, const ggml_mi355x_tensor *src1,
+                                 ggml_mi355x_tensor *dst, void *stream) {
+    if (!src0 || !src1 || !dst || !repacked) return GGML_MI355X_EINVAL;
+    if (repack_size(view_of(src0)) == 0) return GGML_MI355X_EINVAL;
+    return mul_mat_rp(view_of(src0), repacked, view_of(src1), view_of(dst), static_cast<hipStream_t>(stream),
+                      scratch_for(static_cast<hipStream_t>(stream)));
 }
 
 int ggml_mi355x_mul_mat_id(const ggml_mi355x_tensor *as, const ggml_mi355x_tensor *b, const ggml_mi355x_tensor *ids,

@@ -50,6 +50,26 @@ int type_blck(int t);
 int type_bytes(int t);
 bool is_hot_quant(int t);
 
+// repacked weights for the int8 mat-mat tile (mmq8.hip): int8 codes in MFMA-fragment order +
+// f32 block scales (+ K-quant mins), laid out per matrix by rp_layout
+struct RpLayout {
+    int n_rt, n_sb;          // 32-row tiles, super-blocks per row
+    size_t off_meta, bytes;
+};
+struct RpSrcView {           // a ggml weight tensor: n_mat = ne02 * ne03 matrices of N rows x K
+    const void *w;
+    int64_t nb01, nb02, nb03;
+    int K, N, ne02, n_mat;
+};
+RpLayout rp_layout(int type, int K, int N, int n_mat);
+bool repack_supported(int type, const RpSrcView &s);
+hipError_t repack_launch(int type, const RpSrcView &s, void *dst, hipStream_t st);
+int repack(const TensorView &w, void *dst, size_t bytes, hipStream_t st);
+size_t repack_size(const TensorView &w);
+// MUL_MAT with src0 also available repacked at `rp` (nullptr: plain mul_mat)
+int mul_mat_rp(const TensorView &a, const void *rp, const TensorView &b, const TensorView &d, hipStream_t st,
+               Scratch &scratch);
+
 int check_mul_mat(const TensorView &a, const TensorView &b, const TensorView &d);
 int check_mul_mat_id(const TensorView &as, const TensorView &b, const TensorView &ids, const TensorView &d);
 

@@ -811,6 +811,388 @@ __global__ __launch_bounds__(256) void mmq8_split_reduce(const MmArgs a, const f
     reinterpret_cast<float *>(a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3 + (int64_t)tok * a.nb1)[row] = v;
 }
 
+// ==========================================================================================
+// Repacked weights (the optional repacked weight layout): the int8 tile's B
+// operands stored once in MFMA-fragment order, so the tile kernel moves them into LDS by
+// LDS-DMA, 1 KiB per wave instruction, with no VGPR round trip, no decode and no realignment.
+// (Reference analogue: the CPU backend's repack extra buffer type, src/ggml-cpu/repack.cpp:1967,
+// which re-lays Q4_0 / Q4_K blocks for its SIMD kernels at set_tensor time.)
+//   codes [mat][rt32][sb][blk 8][1 KiB]  the int8 codes of 32 rows x one 32-block, in the order a
+//         v_mfma_i32_32x32x32_i8 B operand reads them: lane l holds row l&31, k 16(l>>5)..+15 at
+//         bytes 16l..16l+15. Q6_K: two 512-B v_mfma_i32_32x32x16_i8 operands per block, group g
+//         of 16 k: lane l holds row l&31, k 16g+8(l>>5)..+7 at bytes 512g+8l..
+//         Codes: Q4_0 q-8, Q8_0 q, Q4_K q, Q5_K q | qh<<4, Q6_K q-32.
+//   meta  [mat][rt32][sb][row 32][K-half 2][16 B]  what one lane needs for its row and its half
+//         (blocks 4h..4h+3) of a super-block, in one 16-B load:
+//           Q4_0 / Q8_0: f32 d of the four blocks;
+//           Q4_K / Q5_K: f32 d, f32 dmin, u8 sc[4], u8 m[4] (get_scale_min_k4, ggml-quants.c:703-710);
+//           Q6_K:        f32 d, i8 sc[8] (the 16-groups of the four blocks), 4 B zero.
+// Rows are padded to 32 and K to whole super-blocks with zero codes and zero scales, so the tile
+// kernel never tests a bound inside its loop.
+// ==========================================================================================
+template <int T> constexpr bool rp_has_mins() { return T == T_Q4_K || T == T_Q5_K; }
+
+struct RpArgs {
+    const uint8_t *codes;
+    const uint8_t *meta;
+    int n_rt, n_sb;          // 32-row tiles and super-blocks per matrix
+    int ne02;                // matrix index = i03 * ne02 + i02
+};
+
+struct RpSrc {               // the ggml tensor being repacked
+    const uint8_t *w;
+    int64_t nb01, nb02, nb03;
+    int K, N, ne02, n_mat;
+};
+
+__device__ __forceinline__ uint32_t ld_u16(const uint8_t *p) { return *reinterpret_cast<const uint16_t *>(p); }
+// 4 bytes at a 2-byte-aligned address
+__device__ __forceinline__ uint32_t ld_u32a2(const uint8_t *p) { return ld_u16(p) | (ld_u16(p + 2) << 16); }
+
+// one thread per (matrix, row, 32-block), the row fastest: consecutive threads write consecutive
+// 16-B pieces of one fragment; the thread of a K-half's first block writes that half's meta
+template <int T>
+__global__ __launch_bounds__(256) void repack_kernel(const RpSrc s, const RpArgs r) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int rr = (int)(t & 31);
+    int64_t q = t >> 5;
+    const int blk = (int)(q & 7);
+    q >>= 3;
+    const int sb = (int)(q % r.n_sb);
+    q /= r.n_sb;
+    const int rt = (int)(q % r.n_rt);
+    const int mat = (int)(q / r.n_rt);
+    if (mat >= s.n_mat) return;
+    const int row = rt * 32 + rr, b = sb * 8 + blk;   // 32-block index in the row
+    const bool live = row < s.N && b * 32 < s.K;
+    const uint8_t *wrow = s.w + (int64_t)(mat % s.ne02) * s.nb02 + (int64_t)(mat / s.ne02) * s.nb03 + (int64_t)row * s.nb01;
+    uint32_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};        // 32 codes, little-endian bytes
+    u32x4v meta = u32x4v{0u, 0u, 0u, 0u};           // (the K-half's, written by blk % 4 == 0)
+    float d = 0.f;                                  // Q4_0 / Q8_0 block scale
+    if (live) {
+        if constexpr (T == T_Q8_0) {
+            const uint8_t *p = wrow + (int64_t)b * 34;
+            d = h2f((uint16_t)ld_u16(p));
+#pragma unroll
+            for (int i = 0; i < 8; ++i) c[i] = ld_u32a2(p + 2 + 4 * i);
+        } else if constexpr (T == T_Q4_0) {
+            const uint8_t *p = wrow + (int64_t)b * 18;
+            d = h2f((uint16_t)ld_u16(p));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t n = ld_u32a2(p + 2 + 4 * i);
+                c[i] = sub8_bytes(n & 0x0F0F0F0Fu);            // k 4i..4i+3
+                c[4 + i] = sub8_bytes((n >> 4) & 0x0F0F0F0Fu); // k 16+4i..
+            }
+        } else if constexpr (T == T_Q4_K || T == T_Q5_K) {
+            constexpr int BB = T == T_Q4_K ? 144 : 176, QS = T == T_Q4_K ? 16 : 48;
+            const uint8_t *p = wrow + (int64_t)sb * BB;      // 16-B aligned rows (checked on the host)
+            const int cc = blk >> 1, hi = blk & 1;           // 64-chunk, nibble
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t n = *reinterpret_cast<const uint32_t *>(p + QS + 32 * cc + 4 * i);
+                uint32_t v = hi ? (n >> 4) & 0x0F0F0F0Fu : n & 0x0F0F0F0Fu;
+                if constexpr (T == T_Q5_K) {
+                    const uint32_t h = *reinterpret_cast<const uint32_t *>(p + 16 + 4 * i);
+                    v |= ((h >> blk) & 0x01010101u) << 4;
+                }
+                c[i] = v;
+            }
+            if ((blk & 3) == 0) {   // get_scale_min_k4 (src/ggml-quants.c:703-710) for blocks blk..blk+3
+                const uint32_t h0 = *reinterpret_cast<const uint32_t *>(p);
+                const uint8_t *scs = p + 4;
+                uint32_t sc = 0, m = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int jj = blk + j;
+                    const uint32_t scv = jj < 4 ? scs[jj] & 63 : (scs[jj + 4] & 0xF) | ((scs[jj - 4] >> 6) << 4);
+                    const uint32_t mv = jj < 4 ? scs[jj + 4] & 63 : (scs[jj + 4] >> 4) | ((scs[jj] >> 6) << 4);
+                    sc |= scv << (8 * j);
+                    m |= mv << (8 * j);
+                }
+                meta = u32x4v{fu(h2f((uint16_t)(h0 & 0xffffu))), fu(h2f((uint16_t)(h0 >> 16))), sc, m};
+            }
+        } else {   // Q6_K: 32-block blk = 4h + k of the super-block (dequantize_row_q6_K, src/ggml-quants.c:1762-1791)
+            const uint8_t *p = wrow + (int64_t)sb * 210;     // 2-byte aligned
+            const int h = blk >> 2, k = blk & 3;
+            const uint8_t *ql = p + 64 * h + (k & 1) * 32, *qh = p + 128 + 32 * h;
+            const int sh = 2 * k;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t l = ld_u32a2(ql + 4 * i), hb = ld_u32a2(qh + 4 * i);
+                const uint32_t lo = (k >> 1) ? (l >> 4) & 0x0F0F0F0Fu : l & 0x0F0F0F0Fu;
+                c[i] = sub32_bytes(lo | (((hb >> sh) & 0x03030303u) << 4));
+            }
+            if (k == 0) {   // groups of blocks 4h..4h+3: scale of block 4h + k, group g is sc[8h + g + 2k]
+                const float dd = h2f((uint16_t)ld_u16(p + 208));
+                uint32_t s0 = 0, s1 = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    s0 |= (uint32_t)p[192 + 8 * h + j] << (8 * j);
+                    s1 |= (uint32_t)p[192 + 8 * h + 4 + j] << (8 * j);
+                }
+                meta = u32x4v{fu(dd), s0, s1, 0u};   // sc bytes in (block, group) order = 2k + g
+            }
+        }
+    }
+    const int64_t tile = ((int64_t)mat * r.n_rt + rt) * r.n_sb + sb;
+    uint8_t *cb = const_cast<uint8_t *>(r.codes) + (tile * 8 + blk) * 1024;
+    uint8_t *mb = const_cast<uint8_t *>(r.meta) + ((tile * 32 + rr) * 2 + (blk >> 2)) * 16;
+    if constexpr (T == T_Q6_K) {   // group g = k/16, k-half kg = (k/8)&1: 8 B at 512g + 256kg + 8rr
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+            for (int kg = 0; kg < 2; ++kg)
+                *reinterpret_cast<u32x2v *>(cb + 512 * g + 256 * kg + 8 * rr) = u32x2v{c[4 * g + 2 * kg], c[4 * g + 2 * kg + 1]};
+    } else {
+        st128(cb + 16 * rr, u32x4v{c[0], c[1], c[2], c[3]});
+        st128(cb + 512 + 16 * rr, u32x4v{c[4], c[5], c[6], c[7]});
+    }
+    if constexpr (T == T_Q4_0 || T == T_Q8_0) *reinterpret_cast<float *>(mb + 4 * (blk & 3)) = d;
+    else if ((blk & 3) == 0) st128(mb, meta);
+}
+
+// ------------------------------------------------------------------------------------------
+// the tile kernel on repacked weights: 128 rows x 64 tokens per workgroup, 8 waves = 4 row
+// groups of 32 x 2 K-halves (blocks 0-3 / 4-7 of each super-block); a wave owns 32 rows x 64
+// tokens, i.e. two 32x32 MFMA tiles sharing the weight (B) fragment. Per super-block step the
+// workgroup's 32 KiB of weight fragments and the activation image go to a 3-slot LDS ring by
+// LDS-DMA two steps ahead (every wave issues the same instruction count, so one counted
+// s_waitcnt vmcnt + one s_barrier per step), and each lane's meta (its row, its K-half) comes in
+// registers from a 3-deep ring loaded with the same step.
+// Scale arithmetic as mmq8_kernel:
+//   Q4_0 / Q8_0: the MFMA's C input 0x4B400000 makes the int32 result the f32 12582912 + R, one
+//     fma per output and block applies d; -12582912 * sum(d) starts the sums;
+//   K-quants: exact int32 sums p_i += sc * R (v_mad_i32_i24), then d * p_i, and for Q4_K / Q5_K
+//     minus dmin * sum_j m_j * bsum_j as one f16 MFMA per tile on exact integers;
+// then acc += dx[token] * p per super-block.
+// ------------------------------------------------------------------------------------------
+constexpr int RP_WB = 32768;   // weight bytes of one ring slot: 4 row groups x 8 blocks x 1 KiB
+
+template <int T> constexpr int rp_slot_bytes() { return RP_WB + ximg_bytes<T>(); }
+// vector-memory instructions one wave issues per step (identical in every wave)
+template <int T> constexpr int rp_vmem() { return 4 + q8_x_vmem<T, 8>() + 1; }
+
+template <int T>
+__global__ __launch_bounds__(512) void mmq8r_kernel(const MmArgs a, const RpArgs r, const uint8_t *__restrict__ ximg,
+                                                    int n_tt, int ksplit, int sb_per, float *__restrict__ part, int flags) {
+    constexpr int XB = ximg_bytes<T>();
+    constexpr int SLOT = rp_slot_bytes<T>();
+    constexpr bool F32S = T == T_Q4_0 || T == T_Q8_0;   // float block scales (else integer sub-block scales)
+    __shared__ __align__(16) uint8_t lds[3 * SLOT];
+    const int n_sb = r.n_sb;
+    int v = blockIdx.x;
+    if (flags & 1) v = (v & 7) * (int)(gridDim.x >> 3) + (v >> 3);
+    const int tt = v % n_tt;
+    v /= n_tt;
+    const int ks = v % ksplit, rt128 = v / ksplit;
+    const int sb0 = ks * sb_per, sb1 = min(n_sb, sb0 + sb_per);
+    const int n_steps = sb1 - sb0;
+    if (n_steps <= 0) return;   // (uniform)
+    const int slice = blockIdx.y;
+    const int i12 = slice % a.ne12, i13 = slice / a.ne12;
+    const int mat = (i13 / a.r3) * r.ne02 + (i12 / a.r2);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int rg = wave & 3, kh = wave >> 2;
+    const int rr = lane & 31, hl = lane >> 5;
+    const int64_t mat_tiles = (int64_t)mat * r.n_rt;
+    // the weight codes of this matrix (rows past N read the last row tile: valid memory, never stored)
+    const uint32_t codes_bytes = (uint32_t)r.n_rt * (uint32_t)n_sb * 8192u;
+    const __amdgpu_buffer_rsrc_t wr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(r.codes + mat_tiles * n_sb * 8192), 0, codes_bytes, Q8_RSRC_W3);
+    const uint8_t *xbase = ximg + ((int64_t)slice * n_tt + tt) * n_sb * XB;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void *)xbase, 0, (uint32_t)(n_sb * XB), Q8_RSRC_W3);
+    // this wave's DMA pieces: p = wave + 8i (row group p >> 3, block p & 7)
+    uint32_t woff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int p = wave + 8 * i;
+        const int rt = min(4 * rt128 + (p >> 3), r.n_rt - 1);
+        woff[i] = (uint32_t)rt * (uint32_t)n_sb * 8192u + (uint32_t)(p & 7) * 1024u + (uint32_t)lane * 16u;
+    }
+    const int my_rt = min(4 * rt128 + rg, r.n_rt - 1);
+    const uint8_t *mrow = r.meta + (((mat_tiles + my_rt) * n_sb * 32 + rr) * 2 + kh) * 16;
+
+    auto issue = [&](int slot, int sb, u32x4v &g) {
+        uint8_t *dst = lds + slot * SLOT;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            q8_dma16(wr, dst + (wave + 8 * i) * 1024, woff[i] + (uint32_t)sb * 8192u);
+        q8_x_dma<T, 8>(xr, (uint32_t)(sb * XB), dst + RP_WB, wave, lane);
+        g = *reinterpret_cast<const u32x4v *>(mrow + (int64_t)sb * 32 * 2 * 16);
+    };
+
+    f32x16 acc0, acc1;
+    i32x16 cin;   // MFMA C input: the magic constant (float scales) or zero (integer scales)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { acc0[i] = 0.f; acc1[i] = 0.f; cin[i] = F32S ? (int)Q8_MAGIC_I : 0; }
+
+    auto compute = [&](int slot, const u32x4v &g) {
+        const uint8_t *W = lds + slot * SLOT + rg * 8192;
+        const uint8_t *X = lds + slot * SLOT + RP_WB;
+        // step q: (block, group) of this K-half; A fragments of both token tiles, one B fragment
+        constexpr int NQ = T == T_Q6_K ? 8 : 4;
+        auto mfma2 = [&](int q, i32x16 &R0, i32x16 &R1) {
+            if constexpr (T == T_Q6_K) {
+                const int blk = 4 * kh + (q >> 1), gq = q & 1;
+                const uint8_t *xa = X + blk * 2048 + gq * 1024 + hl * 512 + rr * 8;
+                const u32x2v A0 = ld64(xa), A1 = ld64(xa + 256);
+                const u32x2v B = ld64(W + blk * 1024 + gq * 512 + lane * 8);
+                R0 = __builtin_amdgcn_mfma_i32_32x32x16_i8(as_l(A0), as_l(B), cin, 0, 0, 0);
+                R1 = __builtin_amdgcn_mfma_i32_32x32x16_i8(as_l(A1), as_l(B), cin, 0, 0, 0);
+            } else {
+                const int blk = 4 * kh + q;
+                const uint8_t *xa = X + blk * 2048 + hl * 1024 + rr * 16;
+                const u32x4v A0 = ld128(xa), A1 = ld128(xa + 512);
+                const u32x4v B = ld128(W + blk * 1024 + lane * 16);
+                R0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i4(A0), as_i4(B), cin, 0, 0, 0);
+                R1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i4(A1), as_i4(B), cin, 0, 0, 0);
+            }
+        };
+        f32x16 p0, p1;
+        i32x16 pi0, pi1;
+        float c0 = 0.f;
+        if constexpr (F32S) c0 = -Q8_MAGIC_F * ((uf(g[0]) + uf(g[1])) + (uf(g[2]) + uf(g[3])));
+        auto consume = [&](int q, const i32x16 &R0, const i32x16 &R1) {
+            if constexpr (F32S) {
+                const float sq = uf(g[q]);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    p0[i] = __builtin_fmaf(uf((uint32_t)R0[i]), sq, q == 0 ? c0 : p0[i]);
+                    p1[i] = __builtin_fmaf(uf((uint32_t)R1[i]), sq, q == 0 ? c0 : p1[i]);
+                }
+                asm volatile("" : "+v"(p0), "+v"(p1));
+            } else {
+                // Q4_K / Q5_K: sc[q] (unsigned 6-bit) in byte q of g[2]; Q6_K: sc of step q (signed)
+                // in byte q of g[1..2]
+                const int sc = T == T_Q6_K ? (int)(int8_t)(uint8_t)(g[1 + (q >> 2)] >> (8 * (q & 3)))
+                                           : (int)((g[2] >> (8 * q)) & 0xffu);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    pi0[i] = q == 0 ? __mul24(R0[i], sc) : pi0[i] + __mul24(R0[i], sc);
+                    pi1[i] = q == 0 ? __mul24(R1[i], sc) : pi1[i] + __mul24(R1[i], sc);
+                }
+                asm volatile("" : "+v"(pi0), "+v"(pi1));
+            }
+        };
+        i32x16 Ra0, Ra1, Rb0, Rb1;
+        mfma2(0, Ra0, Ra1);
+#pragma unroll
+        for (int q = 1; q < NQ; ++q) {
+            if (q & 1) mfma2(q, Rb0, Rb1);
+            else mfma2(q, Ra0, Ra1);
+            if (q & 1) consume(q - 1, Ra0, Ra1);
+            else consume(q - 1, Rb0, Rb1);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        consume(NQ - 1, Rb0, Rb1);
+        if constexpr (!F32S) {
+            const float dd = uf(g[0]);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { p0[i] = dd * (float)pi0[i]; p1[i] = dd * (float)pi1[i]; }
+        }
+        if constexpr (rp_has_mins<T>()) {
+            // sum over this K-half's sub-blocks j of m_j * bsum_j: k16-sums 8kh..8kh+7 of the image
+            // (half kh of its bsums), lane k-group (l>>5) takes four of them; m_j for k16-sum e is
+            // m_(e>>1). Exact integers in f16, f32 sums.
+            typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+            const u32x2v bs0 = ld64(X + XI_BS + kh * 1024 + rr * 16 + hl * 8);
+            const u32x2v bs1 = ld64(X + XI_BS + kh * 1024 + (32 + rr) * 16 + hl * 8);
+            const uint32_t m0 = (g[3] >> (16 * hl)) & 0xffu, m1 = (g[3] >> (16 * hl + 8)) & 0xffu;
+            const uint32_t h0 = __builtin_bit_cast(uint16_t, (_Float16)(float)m0);
+            const uint32_t h1 = __builtin_bit_cast(uint16_t, (_Float16)(float)m1);
+            const f16x4 Bm = __builtin_bit_cast(f16x4, u32x2v{h0 | (h0 << 16), h1 | (h1 << 16)});
+            f32x16 zf;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) zf[i] = 0.f;
+            const f32x16 mn0 = __builtin_amdgcn_mfma_f32_32x32x8f16(__builtin_bit_cast(f16x4, bs0), Bm, zf, 0, 0, 0);
+            const f32x16 mn1 = __builtin_amdgcn_mfma_f32_32x32x8f16(__builtin_bit_cast(f16x4, bs1), Bm, zf, 0, 0, 0);
+            const float ndmin = -uf(g[1]);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                p0[i] = __builtin_fmaf(ndmin, mn0[i], p0[i]);
+                p1[i] = __builtin_fmaf(ndmin, mn1[i], p1[i]);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const u32x4v d0 = ld128(X + XI_DX + 4 * (8 * q + 4 * hl));
+            const u32x4v d1 = ld128(X + XI_DX + 4 * (32 + 8 * q + 4 * hl));
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                acc0[4 * q + c] = __builtin_fmaf(p0[4 * q + c], uf(d0[c]), acc0[4 * q + c]);
+                acc1[4 * q + c] = __builtin_fmaf(p1[4 * q + c], uf(d1[c]), acc1[4 * q + c]);
+            }
+        }
+    };
+
+    auto sbc = [&](int it) { return sb0 + min(it, n_steps - 1); };
+    u32x4v g0, g1, g2;
+    issue(0, sbc(0), g0);
+    issue(1, sbc(1), g1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(rp_vmem<T>()) : "memory");   // step 0 landed
+    lds_barrier();
+    // step it: DMA + meta of it+2 into slot (it+2)%3, compute it, wait for it+1, barrier
+    auto step = [&](int it, int slot, const u32x4v &gc, u32x4v &gi) {
+        issue((slot + 2) % 3, sbc(it + 2), gi);
+        compute(slot, gc);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(rp_vmem<T>()) : "memory");
+        lds_barrier();
+    };
+    for (int it = 0; it < n_steps; it += 3) {
+        step(it, 0, g0, g2);
+        if (it + 1 < n_steps) step(it + 1, 1, g1, g0);
+        if (it + 2 < n_steps) step(it + 2, 2, g2, g1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // K-half reduction through LDS (kh = 1 waves hand over; the ring is free after the last barrier)
+    {
+        float *red = reinterpret_cast<float *>(lds);
+        if (kh == 1) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                red[((rg * 2 + 0) * 16 + i) * 64 + lane] = acc0[i];
+                red[((rg * 2 + 1) * 16 + i) * 64 + lane] = acc1[i];
+            }
+        }
+        lds_barrier();
+        if (kh == 1) return;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            acc0[i] += red[((rg * 2 + 0) * 16 + i) * 64 + lane];
+            acc1[i] += red[((rg * 2 + 1) * 16 + i) * 64 + lane];
+        }
+    }
+    const int row = rt128 * 128 + rg * 32 + rr;
+    if (row >= a.N) return;
+    const bool atomic = (flags & 4) != 0;
+    uint8_t *dbase;
+    int64_t ldd;
+    if (ksplit > 1 && !atomic) {
+        dbase = reinterpret_cast<uint8_t *>(part + ((int64_t)ks * gridDim.y + slice) * a.M * a.N);
+        ldd = (int64_t)a.N * 4;
+    } else {
+        dbase = a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3;
+        ldd = a.nb1;
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int tok = tt * 64 + 32 * t + 8 * (i >> 2) + 4 * hl + (i & 3);
+            if (tok < a.M) {
+                float *drow = reinterpret_cast<float *>(dbase + (int64_t)tok * ldd);
+                const float val = t ? acc1[i] : acc0[i];
+                if (atomic) unsafeAtomicAdd(drow + row, val);
+                else drow[row] = val;
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
@@ -965,6 +1347,117 @@ hipError_t mmq8_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &sc
         case T_Q4_K: launch8_id<T_Q4_K>(a, buf, n_tiles, moe, st); break;
         case T_Q5_K: launch8_id<T_Q5_K>(a, buf, n_tiles, moe, st); break;
         case T_Q6_K: launch8_id<T_Q6_K>(a, buf, n_tiles, moe, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// repacked operand: geometry, the repack launch and the tile launch
+// ------------------------------------------------------------------------------------------
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+RpLayout rp_layout(int type, int K, int N, int n_mat) {
+    RpLayout L{};
+    L.n_rt = (N + 31) / 32;
+    L.n_sb = (K + Q8_QK - 1) / Q8_QK;
+    const size_t tiles = (size_t)n_mat * L.n_rt * L.n_sb;
+    L.off_meta = al256(tiles * 8192);
+    L.bytes = L.off_meta + al256(tiles * 32 * 2 * 16);
+    return L;
+}
+
+bool repack_supported(int type, const RpSrcView &s) {
+    if (!(type == T_Q4_0 || type == T_Q8_0 || type == T_Q4_K || type == T_Q5_K || type == T_Q6_K)) return false;
+    if (s.K <= 0 || s.N <= 0 || s.n_mat <= 0 || s.K % type_blck(type) != 0) return false;
+    // K-quant headers and qs are read as dwords: 16-B aligned super-blocks (144 / 176 B)
+    const uintptr_t al = (type == T_Q4_K || type == T_Q5_K) ? 15 : 1;
+    if ((reinterpret_cast<uintptr_t>(s.w) & al) || (s.nb01 & al) || (s.n_mat > s.ne02 && (s.nb03 & al)) || (s.ne02 > 1 && (s.nb02 & al)))
+        return false;
+    const RpLayout L = rp_layout(type, s.K, s.N, s.n_mat);
+    return L.bytes < (1ull << 40) && (int64_t)L.n_rt * L.n_sb * 8192 < (1ll << 32);
+}
+
+static RpArgs rp_args(const RpLayout &L, const void *base, int ne02) {
+    RpArgs r{};
+    r.codes = static_cast<const uint8_t *>(base);
+    r.meta = static_cast<const uint8_t *>(base) + L.off_meta;
+    r.n_rt = L.n_rt;
+    r.n_sb = L.n_sb;
+    r.ne02 = ne02;
+    return r;
+}
+
+hipError_t repack_launch(int type, const RpSrcView &v, void *dst, hipStream_t st) {
+    const RpLayout L = rp_layout(type, v.K, v.N, v.n_mat);
+    const RpArgs r = rp_args(L, dst, v.ne02);
+    const RpSrc s{static_cast<const uint8_t *>(v.w), v.nb01, v.nb02, v.nb03, v.K, v.N, v.ne02, v.n_mat};
+    const int64_t threads = (int64_t)v.n_mat * L.n_rt * L.n_sb * 8 * 32;
+    const dim3 grid((unsigned)((threads + 255) / 256));
+    switch (type) {
+        case T_Q4_0: hipLaunchKernelGGL(repack_kernel<T_Q4_0>, grid, dim3(256), 0, st, s, r); break;
+        case T_Q8_0: hipLaunchKernelGGL(repack_kernel<T_Q8_0>, grid, dim3(256), 0, st, s, r); break;
+        case T_Q4_K: hipLaunchKernelGGL(repack_kernel<T_Q4_K>, grid, dim3(256), 0, st, s, r); break;
+        case T_Q5_K: hipLaunchKernelGGL(repack_kernel<T_Q5_K>, grid, dim3(256), 0, st, s, r); break;
+        case T_Q6_K: hipLaunchKernelGGL(repack_kernel<T_Q6_K>, grid, dim3(256), 0, st, s, r); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <int T>
+static void launch8r(const MmArgs &a, const RpArgs &r, uint8_t *ximg, int n_tt, int slices, int ksplit, int sb_per,
+                     float *part, bool atomic, hipStream_t st) {
+    const int n_sb = r.n_sb;
+    hipLaunchKernelGGL(mmq8_quant_x<T>, dim3((unsigned)(n_tt * (Q8_TOK / 16) * n_sb), slices), dim3(256), 0, st, a, ximg,
+                       n_tt, n_sb, Moe8{}, atomic ? 1 : 0);
+    const int n_rt128 = (a.N + 127) / 128;
+    const unsigned gx = (unsigned)(n_rt128 * ksplit * n_tt);
+    const int flags = ((gx % 8 == 0) ? 1 : 0) | (atomic ? 4 : 0);
+    hipLaunchKernelGGL(mmq8r_kernel<T>, dim3(gx, slices), dim3(512), 0, st, a, r, (const uint8_t *)ximg, n_tt, ksplit,
+                       sb_per, part, flags);
+    if (ksplit > 1 && !atomic) {
+        const int64_t n = (int64_t)slices * a.M * a.N;
+        hipLaunchKernelGGL(mmq8_split_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, (const float *)part,
+                           ksplit, slices);
+    }
+}
+
+// the tile on a repacked operand (rp = its base, laid out by rp_layout for the matrices of a);
+// repack_first: repack a.w into scratch first (the per-call form)
+hipError_t mmq8r_launch(int type, const MmArgs &a, const void *rp, int ne02, int n_mat, hipStream_t st, Scratch &scratch) {
+    const int slices = a.ne12 * a.ne13;
+    const RpLayout L = rp_layout(type, a.K, a.N, n_mat);
+    const int n_sb = L.n_sb;
+    const int n_tt = (a.M + Q8_TOK - 1) / Q8_TOK;
+    const int n_rt128 = (a.N + 127) / 128;
+    const int64_t tiles = (int64_t)n_rt128 * n_tt * slices;
+    int ksplit = 1;
+    while (tiles * ksplit * 2 <= 256 && n_sb >= 4 * ksplit) ksplit *= 2;
+    if (const char *env = getenv("GGML_MI355X_MMQ8_KSPLIT")) ksplit = std::max(1, std::min(atoi(env), n_sb));
+    const int sb_per = (n_sb + ksplit - 1) / ksplit;
+    ksplit = (n_sb + sb_per - 1) / sb_per;
+    static const bool no_atomic = getenv("GGML_MI355X_MMQ8_ATOMIC") && atoi(getenv("GGML_MI355X_MMQ8_ATOMIC")) == 0;
+    const bool atomic = ksplit == 2 && !no_atomic;
+    const size_t img_bytes = al256((size_t)slices * n_tt * n_sb * ximg_bytes_rt(type));
+    const size_t part_bytes = ksplit > 1 && !atomic ? al256((size_t)ksplit * slices * a.M * a.N * sizeof(float)) : 0;
+    const size_t rp_bytes = rp ? 0 : L.bytes;
+    uint8_t *buf = static_cast<uint8_t *>(scratch.get(img_bytes + part_bytes + rp_bytes, st));
+    if (!buf) return hipErrorOutOfMemory;
+    float *part = reinterpret_cast<float *>(buf + img_bytes);
+    if (!rp) {
+        RpSrcView v{a.w, a.nb01, a.nb02, a.nb03, a.K, a.N, ne02, n_mat};
+        const hipError_t e = repack_launch(type, v, buf + img_bytes + part_bytes, st);
+        if (e != hipSuccess) return e;
+        rp = buf + img_bytes + part_bytes;
+    }
+    const RpArgs r = rp_args(L, rp, ne02);
+    switch (type) {
+        case T_Q4_0: launch8r<T_Q4_0>(a, r, buf, n_tt, slices, ksplit, sb_per, part, atomic, st); break;
+        case T_Q8_0: launch8r<T_Q8_0>(a, r, buf, n_tt, slices, ksplit, sb_per, part, atomic, st); break;
+        case T_Q4_K: launch8r<T_Q4_K>(a, r, buf, n_tt, slices, ksplit, sb_per, part, atomic, st); break;
+        case T_Q5_K: launch8r<T_Q5_K>(a, r, buf, n_tt, slices, ksplit, sb_per, part, atomic, st); break;
+        case T_Q6_K: launch8r<T_Q6_K>(a, r, buf, n_tt, slices, ksplit, sb_per, part, atomic, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

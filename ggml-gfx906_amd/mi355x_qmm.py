@@ -71,6 +71,9 @@ def lib():
         L.ggml_mi355x_get_rows.argtypes = [P, P, P, C.c_void_p]
         L.ggml_mi355x_quantize.argtypes = [P, P, C.c_void_p]
         L.ggml_mi355x_cpy.argtypes = [P, P, C.c_void_p]
+        L.ggml_mi355x_repack_size.argtypes = [P, C.POINTER(C.c_size_t)]
+        L.ggml_mi355x_repack.argtypes = [P, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.ggml_mi355x_mul_mat_repacked.argtypes = [P, C.c_void_p, P, P, C.c_void_p]
         L.ggml_mi355x_device_error.restype = C.c_int
         L.ggml_mi355x_strerror.restype = C.c_char_p
         L.ggml_mi355x_strerror.argtypes = [C.c_int]
@@ -138,6 +141,22 @@ def get_rows(a: MmTensor, rows: MmTensor, d: MmTensor, stream=None) -> None:
 def quantize(src: MmTensor, dst: MmTensor, stream=None) -> None:
     """dst (Q4_0 / Q8_0) = quantize_row_*_ref(src f32) on the device (GGML_OP_CPY f32 -> q)"""
     _check(lib().ggml_mi355x_quantize(C.byref(src), C.byref(dst), _stream_ptr(stream)), "quantize")
+
+
+def repack_size(a: MmTensor) -> int:
+    """bytes of the repacked (MFMA-fragment order) copy of quantized src0 `a`"""
+    n = C.c_size_t(0)
+    _check(lib().ggml_mi355x_repack_size(C.byref(a), C.byref(n)), "repack_size")
+    return n.value
+
+
+def repack(a: MmTensor, dst_ptr: int, nbytes: int, stream=None) -> None:
+    _check(lib().ggml_mi355x_repack(C.byref(a), dst_ptr, nbytes, _stream_ptr(stream)), "repack")
+
+
+def mul_mat_repacked(a: MmTensor, rp_ptr: int, b: MmTensor, d: MmTensor, stream=None) -> None:
+    _check(lib().ggml_mi355x_mul_mat_repacked(C.byref(a), rp_ptr, C.byref(b), C.byref(d), _stream_ptr(stream)),
+           "mul_mat_repacked")
 
 
 def cpy(src: MmTensor, dst: MmTensor, stream=None) -> None:

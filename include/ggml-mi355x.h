@@ -125,6 +125,19 @@ GGML_MI355X_API int ggml_mi355x_cpy(const ggml_mi355x_tensor *src, ggml_mi355x_t
  * ggml_cpy_f32_q4_0_cuda / ggml_cpy_f32_q8_0_cuda (src/ggml-cuda/cpy.cu). */
 GGML_MI355X_API int ggml_mi355x_quantize(const ggml_mi355x_tensor *src, ggml_mi355x_tensor *dst, void *stream);
 
+/* Repacked weights for the int8 mat-mat tile (the reference's analogue is the CPU
+ * backend's repack extra buffer type, src/ggml-cpu/repack.cpp:1967): the quantized codes of src0 as
+ * int8 in MFMA-fragment order plus f32 block scales, made once (e.g. at weight upload) so that
+ * MUL_MAT with many tokens streams them with no per-call decode. ggml_mi355x_repack_size gives the
+ * bytes for src0 (every matrix of a 3-d / 4-d tensor), ggml_mi355x_repack writes them to `dst`
+ * (device memory) on `stream`; ggml_mi355x_mul_mat_repacked is ggml_mi355x_mul_mat with that copy
+ * beside src0 (src0 itself still serves the mat-vec shapes, ne11 <= 8). The copy must be remade
+ * when src0's bytes change. */
+GGML_MI355X_API int ggml_mi355x_repack_size(const ggml_mi355x_tensor *src0, size_t *bytes);
+GGML_MI355X_API int ggml_mi355x_repack(const ggml_mi355x_tensor *src0, void *dst, size_t bytes, void *stream);
+GGML_MI355X_API int ggml_mi355x_mul_mat_repacked(const ggml_mi355x_tensor *src0, const void *repacked,
+                                                 const ggml_mi355x_tensor *src1, ggml_mi355x_tensor *dst, void *stream);
+
 /* Same predicate the backend's supports_op uses for MUL_MAT / MUL_MAT_ID on these operands
  * (replaces the MUL_MAT arm of ggml_backend_cuda_device_supports_op, ggml-cuda.cu:3270-3330). */
 GGML_MI355X_API int ggml_mi355x_supports_mul_mat(const ggml_mi355x_tensor *src0, const ggml_mi355x_tensor *src1);

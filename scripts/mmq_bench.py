@@ -16,9 +16,13 @@ shapes = sys.argv[1:] or ["q8_0:4096:4096:512", "q4_K:4096:4096:512", "q4_0:4096
                           "q6_K:4096:11008:512", "q4_K:4096:4096:128", "q8_0:4096:4096:2048"]
 M.build()
 tile = os.environ.get("GGML_MI355X_MMQ_TILE", "auto")
+if os.environ.get("MMQ_REPACKED") == "1":
+    tile = "repacked"
+elif os.environ.get("GGML_MI355X_MMQ_REPACK_MIN"):
+    tile = "rp_call"
 for sh in shapes:
     tn, K, N, Mc = sh.split(":")
-    s = bench.MatVecSet(torch, TYPES[tn], int(K), int(N), int(Mc), 1, 24)
+    s = bench.MatVecSet(torch, TYPES[tn], int(K), int(N), int(Mc), 1, 24, repacked=os.environ.get("MMQ_REPACKED") == "1")
     s.launch(0)
     torch.cuda.synchronize()
     ev_us = s.launch_us(24)

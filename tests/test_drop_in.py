@@ -5,6 +5,7 @@
   ggml-cpu (NMSE 5e-4 for MUL_MAT, :3106-3108). Asserted: exit 0, "Backend MI355X0: OK", zero
   failed cases, and at least the executed hot-type f32 case counts of SURVEY Appendix A
   (MUL_MAT 139, MUL_MAT_ID 114) — so the suite cannot pass by declining everything.
+* repack_check (oracle/repack_check.cpp) does the same for the repacked-weight extra buffer type.
 * split_check (oracle/split_check.cpp) runs MUL_MAT with src0 in our row-split buffer type
   (ggml_backend_split_buffer_type from the plugin's proc table) through the reference's backend
   API, against ggml-cpu, for 1, 2 and 3 shards (GGML_MI355X_SPLIT_SHARDS; on a one-GPU box the
@@ -21,6 +22,7 @@ REF = os.path.join(ROOT, "oracle", "_ref")
 LIB = os.path.join(ROOT, "ggml-gfx906_amd", "libggml-hip-mi355x.so")
 TBO = os.path.join(REF, "test-backend-ops")
 SPLIT = os.path.join(REF, "split_check")
+REPACK = os.path.join(REF, "repack_check")
 HOT = ("q4_0", "q8_0", "q4_K", "q5_K", "q6_K")
 ANSI = re.compile(r"\x1b\[[0-9;]*m")
 
@@ -98,3 +100,12 @@ def test_split_buffer_type_matches_cpu(shards, fractions):
     cmd = [SPLIT, LIB] + ([fractions] if fractions else [])
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0 and "SPLIT_CHECK_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+def test_repack_buffer_type_matches_cpu():
+    """weights in the plugin's repacked-weight extra buffer type (ggml_backend_dev_get_extra_bufts),
+    MUL_MAT at mat-vec and mat-mat sizes vs ggml-cpu through the reference's backend API"""
+    if not os.path.exists(REPACK):
+        pytest.skip("oracle/_ref/repack_check not built")
+    r = subprocess.run([REPACK, LIB], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "REPACK_CHECK_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]

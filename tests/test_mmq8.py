@@ -27,15 +27,22 @@ TYPES = [qref.Q4_0, qref.Q8_0, qref.Q4_K, qref.Q5_K, qref.Q6_K]
 TIGHT = {qref.Q4_K: 1e-9, qref.Q5_K: 1e-9, qref.Q6_K: 1e-9, qref.Q4_0: 5e-4, qref.Q8_0: 5e-4}
 
 
-@pytest.fixture(autouse=True)
-def force_i8():
-    old = os.environ.get("GGML_MI355X_MMQ")
+@pytest.fixture(autouse=True, params=["inplace", "repack"])
+def force_i8(request):
+    """every case runs twice: on the in-place int8 tile (mmq8_kernel) and on the tile over a
+    per-call repacked copy of the weights (repack_kernel + mmq8r_kernel, GGML_MI355X_MMQ_REPACK_MIN)"""
+    saved = {k: os.environ.get(k) for k in ("GGML_MI355X_MMQ", "GGML_MI355X_MMQ_REPACK_MIN")}
     os.environ["GGML_MI355X_MMQ"] = "i8"
-    yield
-    if old is None:
-        del os.environ["GGML_MI355X_MMQ"]
+    if request.param == "repack":
+        os.environ["GGML_MI355X_MMQ_REPACK_MIN"] = "9"
     else:
-        os.environ["GGML_MI355X_MMQ"] = old
+        os.environ.pop("GGML_MI355X_MMQ_REPACK_MIN", None)
+    yield request.param
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
 
 
 def exact(t, w, N, K, x, M_):
