@@ -364,12 +364,15 @@ def gpt2_leg(torch, world: int, rank: int, n_seq: int, ticks: int, warm: int, cp
     return out
 
 
-def sched_plugin_gpt2(threads: int, tokens: int = 64, devices: int = 1) -> dict | None:
+def sched_plugin_gpt2(threads: int, tokens: int = 64, devices: int = 1, n_seq: int = 1) -> dict | None:
     """the drop-in path: the reference's own ggml_backend_sched GPT-2 graph (oracle/_ref/gpt2_ref,
     restating examples/gpt-2/main-sched.cpp) with our plugin loaded as its GPU backend, on the same
     synthetic 117M Q4_0 checkpoint; decode ms/token over `tokens` positions. devices > 1: the
     scheduler splits the layers over that many plugin devices (its pipeline form, hand-offs by
-    our cross-device cpy_tensor_async); run by rank 0 while the other ranks wait"""
+    our cross-device cpy_tensor_async); run by rank 0 while the other ranks wait.
+    n_seq > 1: the scheduler's pipeline form (parallel = true: GGML_SCHED_MAX_COPIES copies of the
+    split inputs, event-ordered hand-offs, reference ggml-backend.cpp:1460) with n_seq sequences
+    decoded round-robin by ggml_backend_sched_graph_compute_async, so stages overlap"""
     exe = os.path.join(ROOT, "oracle", "_ref", "gpt2_ref")
     if not os.path.exists(exe):
         return None
@@ -384,8 +387,9 @@ def sched_plugin_gpt2(threads: int, tokens: int = 64, devices: int = 1) -> dict 
         env = dict(os.environ)
         if REHEARSAL and devices > 1:
             env["GGML_MI355X_VIRTUAL_DEVICES"] = str(devices)   # plugin devices over GPU 0
+        extra = ["--parallel", "--n-seq", str(n_seq)] if n_seq > 1 else []
         r = subprocess.run([exe, path, "--tokens", "40", "--threads", str(threads), "--plugin", M.LIB_PATH, "--devices",
-                            str(devices), "--time-tokens", str(tokens)], capture_output=True, text=True,
+                            str(devices), "--time-tokens", str(tokens)] + extra, capture_output=True, text=True,
                            timeout=300 if devices == 1 else 150, env=env)   # (the N > 1 ranks wait on it)
         if r.returncode != 0:
             return None
@@ -394,11 +398,15 @@ def sched_plugin_gpt2(threads: int, tokens: int = 64, devices: int = 1) -> dict 
         return None
     finally:
         os.remove(path)
-    return {"value": round(j["tokens_per_s"], 2), "unit": "tokens/s", "ms_per_token": round(j["ms_per_token"], 3),
-            "devices": devices, "splits": j.get("splits"),
-            "path": f"reference ggml_backend_sched + libggml-hip-mi355x.so on {devices} device(s) (weights, KV and "
-                    f"supported ops on MI355X, the rest on ggml-cpu with {threads} threads)",
-            "sample": f"GPT-2 117M Q4_0 (synthetic), 1 sequence, {tokens} decode positions after a 40-token prompt"}
+    row = {"value": round(j["tokens_per_s"], 2), "unit": "tokens/s", "ms_per_token": round(j["ms_per_token"], 3),
+           "devices": devices, "splits": j.get("splits"),
+           "path": f"reference ggml_backend_sched + libggml-hip-mi355x.so on {devices} device(s) (weights, KV and "
+                   f"supported ops on MI355X, the rest on ggml-cpu with {threads} threads)",
+           "sample": f"GPT-2 117M Q4_0 (synthetic), {n_seq} sequence(s), {tokens} decode positions each after a "
+                     f"40-token prompt"}
+    if n_seq > 1:
+        row.update(n_seq=n_seq, parallel=True, async_vs_serial_nmse=j.get("async_vs_serial_nmse"))
+    return row
 
 
 def cpu_gpt2_baseline(threads: int, tokens: int = 128) -> dict | None:
@@ -638,8 +646,10 @@ def main() -> None:
             cpu["gpt2"] = cpu_gpt2_example_baseline(cpu["cores"]) or cpu_gpt2_baseline(cpu["cores"])
         if rank == 0:
             # configs[4]'s scheduler form: the reference's scheduler over all `world` devices
-            gpt2["reference_scheduler_with_plugin"] = sched_plugin_gpt2(cpu["cores"] if cpu else cpu_threads(),
-                                                                        devices=world)
+            thr = cpu["cores"] if cpu else cpu_threads()
+            gpt2["reference_scheduler_with_plugin"] = sched_plugin_gpt2(thr, devices=world)
+            # its pipeline form: 8 sequences in flight, stages overlapping across devices
+            gpt2["reference_scheduler_with_plugin_pipelined"] = sched_plugin_gpt2(thr, devices=world, n_seq=8)
         if world > 1:
             dist.barrier(group=cpu_group)   # host wait: rank 0's scheduler run uses the other GPUs
 

@@ -162,6 +162,10 @@ struct BackendCtx {
     std::string name;
     Scratch scratch;
     hipEvent_t src1_ready = nullptr;  // recorded on `stream` before shards start (split mat-mul)
+    // recorded on `stream` after a scheduler hand-off copy (be_cpy_async); the destination
+    // backend's stream waits on it. One event serves every copy: hipStreamWaitEvent waits for the
+    // record that precedes the call, so re-recording it for the next copy is safe
+    hipEvent_t copy_done = nullptr;
     std::vector<std::unique_ptr<ShardLane>> shards;
     FusePlan plan;                    // reused across graph_compute calls (no per-call allocation)
     GraphCache hg;
@@ -679,6 +683,7 @@ void be_free(ggml_backend_t b) {
     if (c->hg.exec) HIP_OK(hipGraphExecDestroy(c->hg.exec));
     HIP_OK(hipStreamDestroy(c->stream));
     if (c->src1_ready) HIP_OK(hipEventDestroy(c->src1_ready));
+    if (c->copy_done) HIP_OK(hipEventDestroy(c->copy_done));
     for (auto &L : c->shards) {
         if (!L || L->device < 0) continue;
         HIP_OK(hipSetDevice(L->device));
@@ -720,12 +725,10 @@ bool be_cpy_async(ggml_backend_t bsrc, ggml_backend_t bdst, const struct ggml_te
         HIP_OK(hipMemcpyPeerAsync(dst->data, cd->device, src->data, cs->device, n, cs->stream));
     }
     if (cs != cd) {
-        hipEvent_t ev;
-        HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        HIP_OK(hipEventRecord(ev, cs->stream));
+        if (!cs->copy_done) HIP_OK(hipEventCreateWithFlags(&cs->copy_done, hipEventDisableTiming));
+        HIP_OK(hipEventRecord(cs->copy_done, cs->stream));
         HIP_OK(hipSetDevice(cd->device));
-        HIP_OK(hipStreamWaitEvent(cd->stream, ev, 0));
-        HIP_OK(hipEventDestroy(ev));   // destruction is deferred by the runtime until completion
+        HIP_OK(hipStreamWaitEvent(cd->stream, cs->copy_done, 0));
     }
     return true;
 }

@@ -61,6 +61,24 @@ constexpr float Q8_MAGIC_F = 12582912.0f;
 #ifndef MMQ8_EXP
 #define MMQ8_EXP 0
 #endif
+#ifndef MMQ8R_EXP
+#define MMQ8R_EXP 0
+#endif
+// repacked tile: the producers also touch (one dword load per 128-B line, result unused) the
+// operands RP_TOUCH steps ahead, so that the LDS-DMA of a step two steps ahead finds them in the
+// XCD's L2 instead of waiting out an Infinity-Cache / HBM miss (0 = off; measurements)
+#ifndef RP_TOUCH
+#define RP_TOUCH 0
+#endif
+// repacked tile: workgroup (row tile r, token tile t) walks its super-blocks starting at
+// (RP_ROT_R * r + RP_ROT_T * t) mod steps, so that the workgroups sharing a weight row tile (or an
+// activation tile) do not all request the same lines at the same moment (0, 0 = all start at 0)
+#ifndef RP_ROT_R
+#define RP_ROT_R 3
+#endif
+#ifndef RP_ROT_T
+#define RP_ROT_T 2
+#endif
 
 // ---- activation image of one (token tile, super-block): the LDS bytes, 1-KiB pieces ----
 //   codes  [blk 8][h 2][tok 64][16 B]            (Q6_K: [blk 8][h 2][hl 2][tok 64][8 B])
@@ -135,31 +153,33 @@ __device__ __forceinline__ void q8_dma16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_
 
 // ------------------------------------------------------------------------------------------
 // activations -> Q8_K blocks, written as stage images (restates quantize_row_q8_K_ref,
-// src/ggml-quants.c:2555-2591). A workgroup takes 16 tokens of one super-block; thread
-// (token t, piece p) holds k = 16p..16p+15 (64 B read per lane, a token's 1 KB by 16 lanes),
-// i.e. exactly one 16-B code piece of the image and one 16-element block sum.
+// src/ggml-quants.c:2555-2591). One wave per (token, super-block): lane l holds k = 4l..4l+3,
+// one coalesced 16-B load (a token's 1 KB per wave instruction); the largest |x| over the 256
+// values by DPP / permlane exchanges, no LDS; lane l writes its 4 codes (one dword of a 16-B
+// code piece) and, per 16-element block, the lane of the piece's first dword its sum.
 // ------------------------------------------------------------------------------------------
 // MOE: token index = position in the tile-padded pair list (tile tok / 64 of moe), its column
 // gathered from src1 (slot % ne11, token) as mmq_convert_x does; padding positions are zeros.
-// zero_dst: also clear dst (the 2-way split-K kernel adds both halves into it): workgroup
-// (16 tokens, super-block sb) clears columns [sb * ceil(N / n_sb), ...) of its tokens' rows.
+// zero_dst: also clear dst (the 2-way split-K kernel adds both halves into it): the wave of
+// (token, super-block sb) clears columns [sb * ceil(N / n_sb), ...) of the token's row.
+// grid.x = (64-token images) * 16 * n_sb: 4 tokens (waves) of one super-block per workgroup.
 template <int T, bool MOE = false>
 __global__ __launch_bounds__(256) void mmq8_quant_x(const MmArgs a, uint8_t *__restrict__ ximg, int n_tt, int n_sb,
                                                     const Moe8 moe, int zero_dst) {
     constexpr int XB = ximg_bytes<T>();
-    const int tid = threadIdx.x, p = tid & 15;
-    const int tok = (blockIdx.x / n_sb) * 16 + (tid >> 4), sb = blockIdx.x % n_sb;
+    const int lane = threadIdx.x & 63;
+    const int tok = (blockIdx.x / n_sb) * 4 + (threadIdx.x >> 6), sb = blockIdx.x % n_sb;
     const int slice = blockIdx.y;
     const int i12 = slice % a.ne12, i13 = slice / a.ne12;
     if (!MOE && zero_dst && tok < a.M) {
         const int chunk = (a.N + n_sb - 1) / n_sb, c1 = min(a.N, (sb + 1) * chunk);
         float *drow = reinterpret_cast<float *>(a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3 + (int64_t)tok * a.nb1);
-        for (int c = sb * chunk + p; c < c1; c += 16) drow[c] = 0.f;
+        for (int c = sb * chunk + lane; c < c1; c += 64) drow[c] = 0.f;
     }
     const uint8_t *row = nullptr;
     if constexpr (MOE) {
         int e, q0, cnt;
-        if (!moe8_tile(moe, tok >> 6, e, q0, cnt)) return;   // (uniform: 16 tokens of one tile)
+        if (!moe8_tile(moe, tok >> 6, e, q0, cnt)) return;   // (uniform: 4 tokens of one tile)
         if ((tok & 63) < cnt) {
             const int pair = moe.pos_pair[q0 + (tok & 63)];
             row = a.x + (int64_t)((pair % moe.n_used) % a.ne11_b) * a.nb11 + (int64_t)(pair / moe.n_used) * a.nb12;
@@ -167,59 +187,58 @@ __global__ __launch_bounds__(256) void mmq8_quant_x(const MmArgs a, uint8_t *__r
     } else if (tok < a.M) {
         row = a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13 + (int64_t)tok * a.nb11;
     }
-    float v[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = 0.f;
-    if (row != nullptr && sb * Q8_QK + p * 16 < a.K) {   // (K % 32 == 0: a 16-piece is all in or all out)
-        const float *src = reinterpret_cast<const float *>(row) + sb * Q8_QK + p * 16;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    const int k0 = sb * Q8_QK + 4 * lane;
+    if (row != nullptr && k0 < a.K) {   // (K % 32 == 0: a lane's 4 values are all in or all out)
+        const float *src = reinterpret_cast<const float *>(row) + k0;
         if (a.x_aligned16) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float4 f = reinterpret_cast<const float4 *>(src)[j];
-                v[4 * j] = f.x; v[4 * j + 1] = f.y; v[4 * j + 2] = f.z; v[4 * j + 3] = f.w;
-            }
+            const float4 f = *reinterpret_cast<const float4 *>(src);
+            v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
         } else {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) v[i] = src[i];
+            for (int i = 0; i < 4; ++i) v[i] = src[i];
         }
     }
-    // the signed value of largest |x|, first k on ties (the reference's strict '>'), over the
-    // token's 16 lanes: (|x|, k, x) reduced with max |x|, then min k
+    // the signed value of largest |x|, first k on ties (the reference's strict '>'): (|x|, k, x)
+    // reduced with max |x|, then min k — a total order, so the butterfly gives every lane the
+    // same winner
     float am = fabsf(v[0]), mx = v[0];
-    int idx = 16 * p;
+    int idx = 4 * lane;
 #pragma unroll
-    for (int i = 1; i < 16; ++i)
-        if (fabsf(v[i]) > am) { am = fabsf(v[i]); mx = v[i]; idx = 16 * p + i; }
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-        const float am2 = __shfl_xor(am, o), mx2 = __shfl_xor(mx, o);
-        const int idx2 = __shfl_xor(idx, o);
+    for (int i = 1; i < 4; ++i)
+        if (fabsf(v[i]) > am) { am = fabsf(v[i]); mx = v[i]; idx = 4 * lane + i; }
+    auto take = [&](float am2, float mx2, int idx2) {
         if (am2 > am || (am2 == am && idx2 < idx)) { am = am2; mx = mx2; idx = idx2; }
-    }
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    };
+#define Q8X_STEP(D) take(xchg<D>(am), xchg<D>(mx), __builtin_bit_cast(int, xchg<D>(__builtin_bit_cast(float, idx))))
+    Q8X_STEP(1); Q8X_STEP(2); Q8X_STEP(4); Q8X_STEP(8); Q8X_STEP(16); Q8X_STEP(32);
+#undef Q8X_STEP
+    uint32_t w = 0u;
     int s = 0;
     float d = 0.f;
     if (am != 0.f) {
         const float iscale = -127.f / mx;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < 4; ++i) {
             const int q = min(127, (int)__builtin_rintf(iscale * v[i]));
             s += q;
-            w[i >> 2] |= (uint32_t)(q & 0xff) << (8 * (i & 3));
+            w |= (uint32_t)(q & 0xff) << (8 * i);
         }
         d = 1.f / iscale;
     }
     uint8_t *img = ximg + (((int64_t)slice * n_tt + (tok >> 6)) * n_sb + sb) * XB;
-    const int tl = tok & 63, blk = p >> 1, h = p & 1;
-    if constexpr (T == T_Q6_K) {
-        *reinterpret_cast<u32x2v *>(img + blk * 2048 + h * 1024 + tl * 8) = u32x2v{w[0], w[1]};
-        *reinterpret_cast<u32x2v *>(img + blk * 2048 + h * 1024 + 512 + tl * 8) = u32x2v{w[2], w[3]};
-    } else {
-        *reinterpret_cast<u32x4v *>(img + blk * 2048 + h * 1024 + tl * 16) = u32x4v{w[0], w[1], w[2], w[3]};
+    const int tl = tok & 63, p = lane >> 2, blk = p >> 1, h = p & 1;   // p: 16-element piece
+    if constexpr (T == T_Q6_K)
+        *reinterpret_cast<uint32_t *>(img + blk * 2048 + h * 1024 + ((lane >> 1) & 1) * 512 + tl * 8 + (lane & 1) * 4) = w;
+    else
+        *reinterpret_cast<uint32_t *>(img + blk * 2048 + h * 1024 + tl * 16 + (lane & 3) * 4) = w;
+    if constexpr (q8_has_min<T>()) {
+        float fs = (float)s;   // |sums| <= 16 * 127: exact
+        fs += xchg<1>(fs);
+        fs += xchg<2>(fs);
+        if ((lane & 3) == 0) *reinterpret_cast<_Float16 *>(img + XI_BS + (p >> 3) * 1024 + tl * 16 + 2 * (p & 7)) = (_Float16)fs;
     }
-    if constexpr (q8_has_min<T>())
-        *reinterpret_cast<_Float16 *>(img + XI_BS + (p >> 3) * 1024 + tl * 16 + 2 * (p & 7)) = (_Float16)s;
-    if (p == 0) *reinterpret_cast<float *>(img + XI_DX + tl * 4) = d;
+    if (lane == 0) *reinterpret_cast<float *>(img + XI_DX + tl * 4) = d;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -953,25 +972,32 @@ __global__ __launch_bounds__(256) void repack_kernel(const RpSrc s, const RpArgs
 }
 
 // ------------------------------------------------------------------------------------------
-// the tile kernel on repacked weights: 128 rows x 64 tokens per workgroup, 8 waves = 4 row
-// groups of 32 x 2 K-halves (blocks 0-3 / 4-7 of each super-block); a wave owns 32 rows x 64
-// tokens, i.e. two 32x32 MFMA tiles sharing the weight (B) fragment. Per super-block step the
-// workgroup's 32 KiB of weight fragments and the activation image go to a 3-slot LDS ring by
-// LDS-DMA two steps ahead (every wave issues the same instruction count, so one counted
-// s_waitcnt vmcnt + one s_barrier per step), and each lane's meta (its row, its K-half) comes in
-// registers from a 3-deep ring loaded with the same step.
+// the tile kernel on repacked weights: 128 rows x 64 tokens per workgroup, 8 waves in two roles,
+// one of each per SIMD (a workgroup's waves 0-3 land on four different SIMDs, and so do 4-7):
+//   consumers (waves 0-3): a wave owns 32 rows x 64 tokens over the whole super-block, i.e. two
+//     32x32 MFMA tiles sharing the weight (B) fragment, 16 MFMAs + their scale epilogue per step;
+//     it also loads its rows' meta (16 B per K-half) into a 3-deep register ring;
+//   producers (waves 4-7): move the next steps' operands into a 3-slot LDS ring by LDS-DMA, two
+//     steps ahead (row group p's 8 KiB of weight fragments, a quarter of the activation image),
+//     and wait for the next step's pieces before each barrier.
+// One s_barrier per step orders the ring (a slot is refilled one step after its last read). With
+// the roles split, one wave of each SIMD issues the DMA (its issue cost, ~100+ cycles per 1 KiB
+// piece, is the partner's VALU / MFMA time) while the other computes: a step costs the larger of
+// the two instead of their sum (measured decomposition: scripts/mmq8r_exp.sh).
 // Scale arithmetic as mmq8_kernel:
 //   Q4_0 / Q8_0: the MFMA's C input 0x4B400000 makes the int32 result the f32 12582912 + R, one
 //     fma per output and block applies d; -12582912 * sum(d) starts the sums;
 //   K-quants: exact int32 sums p_i += sc * R (v_mad_i32_i24), then d * p_i, and for Q4_K / Q5_K
-//     minus dmin * sum_j m_j * bsum_j as one f16 MFMA per tile on exact integers;
+//     minus dmin * sum_j m_j * bsum_j as one f16 MFMA per tile and K-half on exact integers;
 // then acc += dx[token] * p per super-block.
 // ------------------------------------------------------------------------------------------
 constexpr int RP_WB = 32768;   // weight bytes of one ring slot: 4 row groups x 8 blocks x 1 KiB
 
 template <int T> constexpr int rp_slot_bytes() { return RP_WB + ximg_bytes<T>(); }
-// vector-memory instructions one wave issues per step (identical in every wave)
-template <int T> constexpr int rp_vmem() { return 4 + q8_x_vmem<T, 8>() + 1; }
+// vector-memory instructions of one producer wave per step (identical in every producer)
+// step order: DMA of it+2, touch of it+2+RP_TOUCH; before the barrier the DMA of it+1 must have
+// landed, younger than it: the touch of it+1+RP_TOUCH, the DMA of it+2 and its touch
+template <int T> constexpr int rp_prod_wait() { return 8 + q8_x_vmem<T, 4>() + (RP_TOUCH > 0 ? 4 : 0); }
 
 template <int T>
 __global__ __launch_bounds__(512) void mmq8r_kernel(const MmArgs a, const RpArgs r, const uint8_t *__restrict__ ximg,
@@ -995,33 +1021,67 @@ __global__ __launch_bounds__(512) void mmq8r_kernel(const MmArgs a, const RpArgs
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int rg = wave & 3, kh = wave >> 2;
+    const bool producer = wave >= 4;
+    const int rg = wave & 3;              // consumer: its row group; producer: its share
     const int rr = lane & 31, hl = lane >> 5;
     const int64_t mat_tiles = (int64_t)mat * r.n_rt;
-    // the weight codes of this matrix (rows past N read the last row tile: valid memory, never stored)
-    const uint32_t codes_bytes = (uint32_t)r.n_rt * (uint32_t)n_sb * 8192u;
-    const __amdgpu_buffer_rsrc_t wr =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(r.codes + mat_tiles * n_sb * 8192), 0, codes_bytes, Q8_RSRC_W3);
-    const uint8_t *xbase = ximg + ((int64_t)slice * n_tt + tt) * n_sb * XB;
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void *)xbase, 0, (uint32_t)(n_sb * XB), Q8_RSRC_W3);
-    // this wave's DMA pieces: p = wave + 8i (row group p >> 3, block p & 7)
-    uint32_t woff[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int p = wave + 8 * i;
-        const int rt = min(4 * rt128 + (p >> 3), r.n_rt - 1);
-        woff[i] = (uint32_t)rt * (uint32_t)n_sb * 8192u + (uint32_t)(p & 7) * 1024u + (uint32_t)lane * 16u;
-    }
-    const int my_rt = min(4 * rt128 + rg, r.n_rt - 1);
-    const uint8_t *mrow = r.meta + (((mat_tiles + my_rt) * n_sb * 32 + rr) * 2 + kh) * 16;
+    const int my_rt = min(4 * rt128 + rg, r.n_rt - 1);   // (rows past N: the last tile, never stored)
+    // super-block of step it (steps past the end: a valid super-block again, a dead prefetch)
+    const int rot = (RP_ROT_R * rt128 + RP_ROT_T * tt) % n_steps;
+    auto sbc = [&](int it) { return sb0 + (rot + it) % n_steps; };
 
-    auto issue = [&](int slot, int sb, u32x4v &g) {
-        uint8_t *dst = lds + slot * SLOT;
+    if (producer) {
+        // ---------------- producer: DMA two steps ahead, one barrier per step ----------------
+        const uint32_t codes_bytes = (uint32_t)r.n_rt * (uint32_t)n_sb * 8192u;
+        const __amdgpu_buffer_rsrc_t wr =
+            __builtin_amdgcn_make_buffer_rsrc((void *)(r.codes + mat_tiles * n_sb * 8192), 0, codes_bytes, Q8_RSRC_W3);
+        const uint8_t *xbase = ximg + ((int64_t)slice * n_tt + tt) * n_sb * XB;
+        const __amdgpu_buffer_rsrc_t xr =
+            __builtin_amdgcn_make_buffer_rsrc((void *)xbase, 0, (uint32_t)(n_sb * XB), Q8_RSRC_W3);
+        const uint32_t wbase = (uint32_t)my_rt * (uint32_t)n_sb * 8192u + (uint32_t)lane * 16u;
+        // touch of super-block sb: lane i loads one dword of line i of this wave's 8 KiB of weights
+        // and of line i of its quarter of the activation image (the results are never read)
+        const uint32_t xq = (uint32_t)((XB + 511) / 512) * 128u;   // a quarter of the image, 128-B lines
+        auto touch = [&](int sb) {
+            if constexpr (RP_TOUCH > 0) {
+                uint32_t t0 = bl32(wr, wbase - (uint32_t)lane * 16u + (uint32_t)sb * 8192u + (uint32_t)lane * 128u);
+                uint32_t t1 = bl32(xr, (uint32_t)(sb * XB) + min((uint32_t)rg * xq + (uint32_t)lane * 128u, (uint32_t)XB - 4u));
+                asm volatile("" ::"v"(t0), "v"(t1));   // keep the loads; nothing waits for them but the counted vmcnt
+            }
+        };
+        auto issue = [&](int slot, int sb) {
+            uint8_t *dst = lds + slot * SLOT;
+            if constexpr (!(MMQ8R_EXP & 1)) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            q8_dma16(wr, dst + (wave + 8 * i) * 1024, woff[i] + (uint32_t)sb * 8192u);
-        q8_x_dma<T, 8>(xr, (uint32_t)(sb * XB), dst + RP_WB, wave, lane);
-        g = *reinterpret_cast<const u32x4v *>(mrow + (int64_t)sb * 32 * 2 * 16);
+                for (int i = 0; i < 8; ++i) q8_dma16(wr, dst + (rg * 8 + i) * 1024, wbase + (uint32_t)sb * 8192u + i * 1024u);
+            }
+            if constexpr (!(MMQ8R_EXP & 2)) q8_x_dma<T, 4>(xr, (uint32_t)(sb * XB), dst + RP_WB, rg, lane);
+        };
+        // per step: DMA of it+2 then the touch of it+2+RP_TOUCH (counted in rp_prod_wait)
+        for (int d = 2; d < RP_TOUCH; ++d) touch(sbc(d));   // (uncounted: issued before everything below)
+        issue(0, sbc(0));
+        touch(sbc(RP_TOUCH));
+        issue(1, sbc(1));
+        touch(sbc(RP_TOUCH + 1));
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(rp_prod_wait<T>()) : "memory");   // step 0 landed
+        lds_barrier();
+        for (int it = 0; it < n_steps; ++it) {
+            issue((it + 2) % 3, sbc(it + 2));
+            touch(sbc(it + 2 + RP_TOUCH));
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(rp_prod_wait<T>()) : "memory");   // step it+1 landed
+            lds_barrier();
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped prefetches land before the exit
+        return;
+    }
+
+    // ---------------- consumer ----------------
+    const uint8_t *mrow = r.meta + ((mat_tiles + my_rt) * n_sb * 32 + rr) * 32;
+    struct Meta { u32x4v h[2]; };   // this lane's row: K-half 0 and 1 of one super-block
+    auto load_meta = [&](int sb, Meta &g) {
+        const u32x4v *p = reinterpret_cast<const u32x4v *>(mrow + (int64_t)sb * 32 * 32);
+        g.h[0] = p[0];
+        g.h[1] = p[1];
     };
 
     f32x16 acc0, acc1;
@@ -1029,35 +1089,52 @@ __global__ __launch_bounds__(512) void mmq8r_kernel(const MmArgs a, const RpArgs
 #pragma unroll
     for (int i = 0; i < 16; ++i) { acc0[i] = 0.f; acc1[i] = 0.f; cin[i] = F32S ? (int)Q8_MAGIC_I : 0; }
 
-    auto compute = [&](int slot, const u32x4v &g) {
+    auto compute = [&](int slot, const Meta &g) {
+        if constexpr ((MMQ8R_EXP & 4) != 0) {
+            asm volatile("" ::"v"(g.h[0]), "v"(g.h[1]));
+            return;
+        }
         const uint8_t *W = lds + slot * SLOT + rg * 8192;
         const uint8_t *X = lds + slot * SLOT + RP_WB;
-        // step q: (block, group) of this K-half; A fragments of both token tiles, one B fragment
-        constexpr int NQ = T == T_Q6_K ? 8 : 4;
-        auto mfma2 = [&](int q, i32x16 &R0, i32x16 &R1) {
+        // step q: (block, group); A fragments of both token tiles and one B fragment, read from LDS
+        // one step ahead of their MFMAs (one wave per SIMD computes: nothing else hides the latency)
+        constexpr int NQ = T == T_Q6_K ? 16 : 8;
+        struct Frag { u32x4v A0, A1, B; };
+        auto load = [&](int q, Frag &f) {
             if constexpr (T == T_Q6_K) {
-                const int blk = 4 * kh + (q >> 1), gq = q & 1;
+                const int blk = q >> 1, gq = q & 1;
                 const uint8_t *xa = X + blk * 2048 + gq * 1024 + hl * 512 + rr * 8;
-                const u32x2v A0 = ld64(xa), A1 = ld64(xa + 256);
-                const u32x2v B = ld64(W + blk * 1024 + gq * 512 + lane * 8);
-                R0 = __builtin_amdgcn_mfma_i32_32x32x16_i8(as_l(A0), as_l(B), cin, 0, 0, 0);
-                R1 = __builtin_amdgcn_mfma_i32_32x32x16_i8(as_l(A1), as_l(B), cin, 0, 0, 0);
+                const u32x2v a0 = ld64(xa), a1 = ld64(xa + 256), b = ld64(W + blk * 1024 + gq * 512 + lane * 8);
+                f.A0 = u32x4v{a0[0], a0[1], 0u, 0u};
+                f.A1 = u32x4v{a1[0], a1[1], 0u, 0u};
+                f.B = u32x4v{b[0], b[1], 0u, 0u};
             } else {
-                const int blk = 4 * kh + q;
-                const uint8_t *xa = X + blk * 2048 + hl * 1024 + rr * 16;
-                const u32x4v A0 = ld128(xa), A1 = ld128(xa + 512);
-                const u32x4v B = ld128(W + blk * 1024 + lane * 16);
-                R0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i4(A0), as_i4(B), cin, 0, 0, 0);
-                R1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i4(A1), as_i4(B), cin, 0, 0, 0);
+                const uint8_t *xa = X + q * 2048 + hl * 1024 + rr * 16;
+                f.A0 = ld128(xa);
+                f.A1 = ld128(xa + 512);
+                f.B = ld128(W + q * 1024 + lane * 16);
+            }
+        };
+        auto mfma2 = [&](const Frag &f, i32x16 &R0, i32x16 &R1) {
+            if constexpr (T == T_Q6_K) {
+                const long A0 = as_l(u32x2v{f.A0[0], f.A0[1]}), A1 = as_l(u32x2v{f.A1[0], f.A1[1]});
+                const long B = as_l(u32x2v{f.B[0], f.B[1]});
+                R0 = __builtin_amdgcn_mfma_i32_32x32x16_i8(A0, B, cin, 0, 0, 0);
+                R1 = __builtin_amdgcn_mfma_i32_32x32x16_i8(A1, B, cin, 0, 0, 0);
+            } else {
+                R0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i4(f.A0), as_i4(f.B), cin, 0, 0, 0);
+                R1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(as_i4(f.A1), as_i4(f.B), cin, 0, 0, 0);
             }
         };
         f32x16 p0, p1;
         i32x16 pi0, pi1;
         float c0 = 0.f;
-        if constexpr (F32S) c0 = -Q8_MAGIC_F * ((uf(g[0]) + uf(g[1])) + (uf(g[2]) + uf(g[3])));
+        if constexpr (F32S)
+            c0 = -Q8_MAGIC_F * (((uf(g.h[0][0]) + uf(g.h[0][1])) + (uf(g.h[0][2]) + uf(g.h[0][3]))) +
+                                ((uf(g.h[1][0]) + uf(g.h[1][1])) + (uf(g.h[1][2]) + uf(g.h[1][3]))));
         auto consume = [&](int q, const i32x16 &R0, const i32x16 &R1) {
             if constexpr (F32S) {
-                const float sq = uf(g[q]);
+                const float sq = uf(g.h[q >> 2][q & 3]);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     p0[i] = __builtin_fmaf(uf((uint32_t)R0[i]), sq, q == 0 ? c0 : p0[i]);
@@ -1065,10 +1142,11 @@ __global__ __launch_bounds__(512) void mmq8r_kernel(const MmArgs a, const RpArgs
                 }
                 asm volatile("" : "+v"(p0), "+v"(p1));
             } else {
-                // Q4_K / Q5_K: sc[q] (unsigned 6-bit) in byte q of g[2]; Q6_K: sc of step q (signed)
-                // in byte q of g[1..2]
-                const int sc = T == T_Q6_K ? (int)(int8_t)(uint8_t)(g[1 + (q >> 2)] >> (8 * (q & 3)))
-                                           : (int)((g[2] >> (8 * q)) & 0xffu);
+                // Q4_K / Q5_K: sc of block q (unsigned 6-bit) in byte q&3 of half q>>2's word 2;
+                // Q6_K: sc of step q (signed) in byte q&3 of half q>>3's words 1..2
+                int sc;
+                if constexpr (T == T_Q6_K) sc = (int)(int8_t)(uint8_t)(g.h[q >> 3][1 + ((q >> 2) & 1)] >> (8 * (q & 3)));
+                else sc = (int)((g.h[q >> 2][2] >> (8 * (q & 3))) & 0xffu);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     pi0[i] = q == 0 ? __mul24(R0[i], sc) : pi0[i] + __mul24(R0[i], sc);
@@ -1078,94 +1156,96 @@ __global__ __launch_bounds__(512) void mmq8r_kernel(const MmArgs a, const RpArgs
             }
         };
         i32x16 Ra0, Ra1, Rb0, Rb1;
-        mfma2(0, Ra0, Ra1);
+        u32x4v dxv[8];
+        Frag fa, fb;
+        load(0, fa);
+        load(1, fb);
+        mfma2(fa, Ra0, Ra1);
+        load(2, fa);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 1; q < NQ; ++q) {
-            if (q & 1) mfma2(q, Rb0, Rb1);
-            else mfma2(q, Ra0, Ra1);
+            // fragments of q are in (q & 1 ? fb : fa); those of q+1 go into the other set after
+            // the MFMAs of q have read theirs
+            if (q & 1) mfma2(fb, Rb0, Rb1);
+            else mfma2(fa, Ra0, Ra1);
+            if (q + 2 < NQ) {
+                if (q & 1) load(q + 2, fb);
+                else load(q + 2, fa);
+            }
+            if (q == NQ - 1) {   // tile 0's token scales: read now, used after the last epilogues
+#pragma unroll
+                for (int k = 0; k < 4; ++k) dxv[k] = ld128(X + XI_DX + 4 * (8 * k + 4 * hl));
+            }
             if (q & 1) consume(q - 1, Ra0, Ra1);
             else consume(q - 1, Rb0, Rb1);
             __builtin_amdgcn_sched_barrier(0);
         }
         consume(NQ - 1, Rb0, Rb1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dxv[4 + k] = ld128(X + XI_DX + 4 * (32 + 8 * k + 4 * hl));   // tile 1's
         if constexpr (!F32S) {
-            const float dd = uf(g[0]);
+            // one d per super-block (both halves carry it)
+            const float dd = uf(g.h[0][0]);
 #pragma unroll
             for (int i = 0; i < 16; ++i) { p0[i] = dd * (float)pi0[i]; p1[i] = dd * (float)pi1[i]; }
         }
         if constexpr (rp_has_mins<T>()) {
-            // sum over this K-half's sub-blocks j of m_j * bsum_j: k16-sums 8kh..8kh+7 of the image
+            // sum over sub-blocks j of m_j * bsum_j, per K-half kh: k16-sums 8kh..8kh+7 of the image
             // (half kh of its bsums), lane k-group (l>>5) takes four of them; m_j for k16-sum e is
             // m_(e>>1). Exact integers in f16, f32 sums.
             typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-            const u32x2v bs0 = ld64(X + XI_BS + kh * 1024 + rr * 16 + hl * 8);
-            const u32x2v bs1 = ld64(X + XI_BS + kh * 1024 + (32 + rr) * 16 + hl * 8);
-            const uint32_t m0 = (g[3] >> (16 * hl)) & 0xffu, m1 = (g[3] >> (16 * hl + 8)) & 0xffu;
-            const uint32_t h0 = __builtin_bit_cast(uint16_t, (_Float16)(float)m0);
-            const uint32_t h1 = __builtin_bit_cast(uint16_t, (_Float16)(float)m1);
-            const f16x4 Bm = __builtin_bit_cast(f16x4, u32x2v{h0 | (h0 << 16), h1 | (h1 << 16)});
             f32x16 zf;
 #pragma unroll
             for (int i = 0; i < 16; ++i) zf[i] = 0.f;
-            const f32x16 mn0 = __builtin_amdgcn_mfma_f32_32x32x8f16(__builtin_bit_cast(f16x4, bs0), Bm, zf, 0, 0, 0);
-            const f32x16 mn1 = __builtin_amdgcn_mfma_f32_32x32x8f16(__builtin_bit_cast(f16x4, bs1), Bm, zf, 0, 0, 0);
-            const float ndmin = -uf(g[1]);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                p0[i] = __builtin_fmaf(ndmin, mn0[i], p0[i]);
-                p1[i] = __builtin_fmaf(ndmin, mn1[i], p1[i]);
+            for (int kh = 0; kh < 2; ++kh) {
+                const u32x2v bs0 = ld64(X + XI_BS + kh * 1024 + rr * 16 + hl * 8);
+                const u32x2v bs1 = ld64(X + XI_BS + kh * 1024 + (32 + rr) * 16 + hl * 8);
+                const uint32_t mw = g.h[kh][3];
+                const uint32_t m0 = (mw >> (16 * hl)) & 0xffu, m1 = (mw >> (16 * hl + 8)) & 0xffu;
+                const uint32_t h0 = __builtin_bit_cast(uint16_t, (_Float16)(float)m0);
+                const uint32_t h1 = __builtin_bit_cast(uint16_t, (_Float16)(float)m1);
+                const f16x4 Bm = __builtin_bit_cast(f16x4, u32x2v{h0 | (h0 << 16), h1 | (h1 << 16)});
+                const f32x16 mn0 = __builtin_amdgcn_mfma_f32_32x32x8f16(__builtin_bit_cast(f16x4, bs0), Bm, zf, 0, 0, 0);
+                const f32x16 mn1 = __builtin_amdgcn_mfma_f32_32x32x8f16(__builtin_bit_cast(f16x4, bs1), Bm, zf, 0, 0, 0);
+                const float ndmin = -uf(g.h[0][1]);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    p0[i] = __builtin_fmaf(ndmin, mn0[i], p0[i]);
+                    p1[i] = __builtin_fmaf(ndmin, mn1[i], p1[i]);
+                }
             }
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const u32x4v d0 = ld128(X + XI_DX + 4 * (8 * q + 4 * hl));
-            const u32x4v d1 = ld128(X + XI_DX + 4 * (32 + 8 * q + 4 * hl));
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-                acc0[4 * q + c] = __builtin_fmaf(p0[4 * q + c], uf(d0[c]), acc0[4 * q + c]);
-                acc1[4 * q + c] = __builtin_fmaf(p1[4 * q + c], uf(d1[c]), acc1[4 * q + c]);
+                acc0[4 * q + c] = __builtin_fmaf(p0[4 * q + c], uf(dxv[q][c]), acc0[4 * q + c]);
+                acc1[4 * q + c] = __builtin_fmaf(p1[4 * q + c], uf(dxv[4 + q][c]), acc1[4 * q + c]);
             }
         }
     };
 
-    auto sbc = [&](int it) { return sb0 + min(it, n_steps - 1); };
-    u32x4v g0, g1, g2;
-    issue(0, sbc(0), g0);
-    issue(1, sbc(1), g1);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(rp_vmem<T>()) : "memory");   // step 0 landed
-    lds_barrier();
-    // step it: DMA + meta of it+2 into slot (it+2)%3, compute it, wait for it+1, barrier
-    auto step = [&](int it, int slot, const u32x4v &gc, u32x4v &gi) {
-        issue((slot + 2) % 3, sbc(it + 2), gi);
+    // this lane's meta of step it+1 is loaded while step it computes (a 2-deep register ring)
+    Meta g0, g1;
+    load_meta(sbc(0), g0);
+    lds_barrier();   // (the producers' step-0 barrier)
+    auto step = [&](int it, int slot, const Meta &gc, Meta &gi) {
+        load_meta(sbc(it + 1), gi);
         compute(slot, gc);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(rp_vmem<T>()) : "memory");
         lds_barrier();
     };
-    for (int it = 0; it < n_steps; it += 3) {
-        step(it, 0, g0, g2);
+    // (slots rotate by 3, the meta ring by 2: unrolled by 6)
+    for (int it = 0; it < n_steps; it += 6) {
+        step(it, 0, g0, g1);
         if (it + 1 < n_steps) step(it + 1, 1, g1, g0);
-        if (it + 2 < n_steps) step(it + 2, 2, g2, g1);
+        if (it + 2 < n_steps) step(it + 2, 2, g0, g1);
+        if (it + 3 < n_steps) step(it + 3, 0, g1, g0);
+        if (it + 4 < n_steps) step(it + 4, 1, g0, g1);
+        if (it + 5 < n_steps) step(it + 5, 2, g1, g0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-    // K-half reduction through LDS (kh = 1 waves hand over; the ring is free after the last barrier)
-    {
-        float *red = reinterpret_cast<float *>(lds);
-        if (kh == 1) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                red[((rg * 2 + 0) * 16 + i) * 64 + lane] = acc0[i];
-                red[((rg * 2 + 1) * 16 + i) * 64 + lane] = acc1[i];
-            }
-        }
-        lds_barrier();
-        if (kh == 1) return;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            acc0[i] += red[((rg * 2 + 0) * 16 + i) * 64 + lane];
-            acc1[i] += red[((rg * 2 + 1) * 16 + i) * 64 + lane];
-        }
-    }
     const int row = rt128 * 128 + rg * 32 + rr;
     if (row >= a.N) return;
     const bool atomic = (flags & 4) != 0;
@@ -1230,7 +1310,7 @@ static void launch8(const MmArgs &a, uint8_t *ximg, int tr_rows, int tt_tok, int
                     int sb_per, float *part, bool atomic, hipStream_t st) {
     const int n_sb = (a.K + Q8_QK - 1) / Q8_QK;
     const int n_img = n_tt * (tt_tok / Q8_TOK);   // 64-token images per slice (tokens past M: zeros)
-    hipLaunchKernelGGL(mmq8_quant_x<T>, dim3((unsigned)(n_img * (Q8_TOK / 16) * n_sb), slices), dim3(256), 0, st, a, ximg,
+    hipLaunchKernelGGL(mmq8_quant_x<T>, dim3((unsigned)(n_img * (Q8_TOK / 4) * n_sb), slices), dim3(256), 0, st, a, ximg,
                        n_img, n_sb, Moe8{}, atomic ? 1 : 0);
     const int64_t row_b = (int64_t)a.K / QT<T>::blck * QT<T>::bytes;
     const uint32_t w_extent = (uint32_t)((int64_t)(a.N - 1) * a.nb01 + row_b);   // (the kernel rounds it up)
@@ -1318,7 +1398,7 @@ bool mmq8_id_supported(int type, const MmArgs &a) {
 template <int T>
 static void launch8_id(const MmArgs &a, uint8_t *ximg, int n_tiles, const Moe8 &moe, hipStream_t st) {
     const int n_sb = (a.K + Q8_QK - 1) / Q8_QK;
-    hipLaunchKernelGGL((mmq8_quant_x<T, true>), dim3((unsigned)(n_tiles * (Q8_TOK / 16) * n_sb), 1), dim3(256), 0, st, a,
+    hipLaunchKernelGGL((mmq8_quant_x<T, true>), dim3((unsigned)(n_tiles * (Q8_TOK / 4) * n_sb), 1), dim3(256), 0, st, a,
                        ximg, n_tiles, n_sb, moe, 0);
     const int64_t row_b = (int64_t)a.K / QT<T>::blck * QT<T>::bytes;
     const uint32_t w_extent = (uint32_t)((int64_t)(a.N - 1) * a.nb01 + row_b);
@@ -1409,7 +1489,7 @@ template <int T>
 static void launch8r(const MmArgs &a, const RpArgs &r, uint8_t *ximg, int n_tt, int slices, int ksplit, int sb_per,
                      float *part, bool atomic, hipStream_t st) {
     const int n_sb = r.n_sb;
-    hipLaunchKernelGGL(mmq8_quant_x<T>, dim3((unsigned)(n_tt * (Q8_TOK / 16) * n_sb), slices), dim3(256), 0, st, a, ximg,
+    hipLaunchKernelGGL(mmq8_quant_x<T>, dim3((unsigned)(n_tt * (Q8_TOK / 4) * n_sb), slices), dim3(256), 0, st, a, ximg,
                        n_tt, n_sb, Moe8{}, atomic ? 1 : 0);
     const int n_rt128 = (a.N + 127) / 128;
     const unsigned gx = (unsigned)(n_rt128 * ksplit * n_tt);

@@ -19,8 +19,16 @@
 //                      split the graph across [GPU devices..., CPU] — the reference's own
 //                      scheduler driving our backend, i.e. the drop-in check for examples/gpt-2.
 //
+// Pipeline throughput (--parallel --n-seq S): the scheduler is created with parallel = true, so
+// it keeps GGML_SCHED_MAX_COPIES copies of every split input and orders the hand-offs with events
+// (reference ggml-backend.cpp:1460, :1352-1443) instead of synchronizing; S independent sequences
+// (each its own KV region) are decoded round-robin with ggml_backend_sched_graph_compute_async, so
+// while stage d runs sequence s, stage d-1 can already run sequence s+1. The timed run reports
+// tokens of all sequences per second; logits of every sequence are checked against a serial run
+// of the same tokens first (--check).
+//
 // usage: gpt2_ref MODEL --tokens 1,2,3 [--out logits.f32] [--threads N] [--plugin LIB]
-//                 [--devices D] [--time-tokens T]
+//                 [--devices D] [--time-tokens T] [--parallel] [--n-seq S]
 #include "ggml-alloc.h"
 #include "ggml-backend.h"
 #include "ggml-cpu.h"
@@ -61,7 +69,8 @@ int main(int argc, char **argv) {
     if (argc < 2) die("usage: gpt2_ref MODEL --tokens a,b,c [--out F] [--threads N] [--plugin LIB] [--devices D] [--time-tokens T]");
     std::string fname = argv[1], out, plugin;
     std::vector<int32_t> toks;
-    int threads = 8, want_dev = -1, time_tokens = 0;
+    int threads = 8, want_dev = -1, time_tokens = 0, n_seq = 1;
+    bool parallel = false;
     for (int i = 2; i < argc; ++i) {
         std::string a = argv[i];
         auto next = [&]() { if (i + 1 >= argc) die("missing value"); return std::string(argv[++i]); };
@@ -79,6 +88,8 @@ int main(int argc, char **argv) {
         else if (a == "--plugin") plugin = next();
         else if (a == "--devices") want_dev = atoi(next().c_str());
         else if (a == "--time-tokens") time_tokens = atoi(next().c_str());
+        else if (a == "--parallel") parallel = true;
+        else if (a == "--n-seq") n_seq = std::max(1, atoi(next().c_str()));
         else die(("unknown arg " + a).c_str());
     }
 
@@ -159,8 +170,8 @@ int main(int argc, char **argv) {
         L.c_mlp_fc_b = t1("mlp/c_fc/b", 4 * E);
         L.c_mlp_proj_w = t2("mlp/c_proj/w", 4 * E, E);
         L.c_mlp_proj_b = t1("mlp/c_proj/b", E);
-        L.memory_k = ggml_new_tensor_1d(c, GGML_TYPE_F32, E * m.n_ctx);
-        L.memory_v = ggml_new_tensor_1d(c, GGML_TYPE_F32, E * m.n_ctx);
+        L.memory_k = ggml_new_tensor_1d(c, GGML_TYPE_F32, E * m.n_ctx * n_seq);   // sequence s at s * n_ctx
+        L.memory_v = ggml_new_tensor_1d(c, GGML_TYPE_F32, E * m.n_ctx * n_seq);
     }
     std::vector<ggml_backend_buffer_t> bufs;
     for (int p = 0; p < n_place; ++p) {
@@ -200,16 +211,20 @@ int main(int argc, char **argv) {
     ggml_context *cin = ggml_init(ipi);
     ggml_tensor *embd = ggml_new_tensor_1d(cin, GGML_TYPE_I32, 1);
     ggml_tensor *position = ggml_new_tensor_1d(cin, GGML_TYPE_I32, 1);
+    // (inputs in a host buffer as main-sched.cpp:519-545 keeps them: the scheduler copies them into
+    // the first split synchronously while it submits, so the host may overwrite them for the next
+    // evaluation as soon as ggml_backend_sched_graph_compute_async has returned)
     ggml_backend_buffer_t bin = ggml_backend_alloc_ctx_tensors_from_buft(cin, ggml_backend_cpu_buffer_type());
 
     std::vector<ggml_backend_t> backends = gpus;
     backends.push_back(cpu);
     const int MAX_NODES = 4096;
-    ggml_backend_sched_t sched = ggml_backend_sched_new(backends.data(), nullptr, (int)backends.size(), MAX_NODES, false, true);
+    ggml_backend_sched_t sched = ggml_backend_sched_new(backends.data(), nullptr, (int)backends.size(), MAX_NODES, parallel, true);
     std::vector<uint8_t> gbuf(ggml_tensor_overhead() * MAX_NODES + ggml_graph_overhead_custom(MAX_NODES, false));
 
     // gpt2_graph with N = 1 (main-sched.cpp:553-858)
-    auto build = [&](int n_past) {
+    auto build = [&](int n_past, int seq) {
+        const size_t kv0 = (size_t)seq * m.n_ctx * E;   // this sequence's KV region (elements)
         ggml_init_params gp = {gbuf.size(), gbuf.data(), true};
         ggml_context *ctx = ggml_init(gp);
         ggml_cgraph *gf = ggml_new_graph_custom(ctx, MAX_NODES, false);
@@ -224,17 +239,17 @@ int main(int argc, char **argv) {
             ggml_tensor *Qcur = ggml_view_2d(ctx, cur, E, N, cur->nb[1], 0 * sizeof(float) * E);
             ggml_tensor *Kcur = ggml_view_2d(ctx, cur, E, N, cur->nb[1], 1 * sizeof(float) * E);
             ggml_tensor *Vcur = ggml_view_2d(ctx, cur, E, N, cur->nb[1], 2 * sizeof(float) * E);
-            ggml_tensor *k = ggml_view_1d(ctx, L.memory_k, N * E, ggml_element_size(L.memory_k) * E * n_past);
-            ggml_tensor *v = ggml_view_1d(ctx, L.memory_v, N * E, ggml_element_size(L.memory_v) * E * n_past);
+            ggml_tensor *k = ggml_view_1d(ctx, L.memory_k, N * E, ggml_element_size(L.memory_k) * (kv0 + E * n_past));
+            ggml_tensor *v = ggml_view_1d(ctx, L.memory_v, N * E, ggml_element_size(L.memory_v) * (kv0 + E * n_past));
             ggml_build_forward_expand(gf, ggml_cpy(ctx, Kcur, k));
             ggml_build_forward_expand(gf, ggml_cpy(ctx, Vcur, v));
             ggml_tensor *Q = ggml_permute(ctx, ggml_cont_3d(ctx, Qcur, E / m.n_head, m.n_head, N), 0, 2, 1, 3);
-            ggml_tensor *K = ggml_permute(ctx, ggml_reshape_3d(ctx, ggml_view_1d(ctx, L.memory_k, (n_past + N) * E, 0), E / m.n_head, m.n_head, n_past + N), 0, 2, 1, 3);
+            ggml_tensor *K = ggml_permute(ctx, ggml_reshape_3d(ctx, ggml_view_1d(ctx, L.memory_k, (n_past + N) * E, ggml_element_size(L.memory_k) * kv0), E / m.n_head, m.n_head, n_past + N), 0, 2, 1, 3);
             ggml_tensor *KQ = ggml_mul_mat(ctx, K, Q);
             ggml_tensor *KQ_scaled = ggml_scale(ctx, KQ, KQ_scale);
             ggml_tensor *KQ_masked = ggml_diag_mask_inf(ctx, KQ_scaled, n_past);
             ggml_tensor *KQ_soft_max = ggml_soft_max(ctx, KQ_masked);
-            ggml_tensor *V_trans = ggml_cont_3d(ctx, ggml_permute(ctx, ggml_reshape_3d(ctx, ggml_view_1d(ctx, L.memory_v, (n_past + N) * E, 0), E / m.n_head, m.n_head, n_past + N), 1, 2, 0, 3),
+            ggml_tensor *V_trans = ggml_cont_3d(ctx, ggml_permute(ctx, ggml_reshape_3d(ctx, ggml_view_1d(ctx, L.memory_v, (n_past + N) * E, ggml_element_size(L.memory_v) * kv0), E / m.n_head, m.n_head, n_past + N), 1, 2, 0, 3),
                                                 n_past + N, E / m.n_head, m.n_head);
             ggml_tensor *KQV = ggml_mul_mat(ctx, V_trans, KQ_soft_max);
             cur = ggml_cont_2d(ctx, ggml_permute(ctx, KQV, 0, 2, 1, 3), E, N);
@@ -262,16 +277,21 @@ int main(int argc, char **argv) {
     double ph[4] = {0, 0, 0, 0};
     bool phases = false;
     auto now = [] { return std::chrono::steady_clock::now(); };
-    auto eval = [&](int n_past, int32_t tok, float *dst) {
+    // dst == nullptr: submit only (ggml_backend_sched_graph_compute_async), nothing waited for
+    auto eval = [&](int n_past, int32_t tok, float *dst, int seq = 0) {
         auto t0 = now();
-        ggml_cgraph *gf = build(n_past);
+        ggml_cgraph *gf = build(n_past, seq);
         auto t1 = now();
         ggml_backend_sched_reset(sched);
         if (!ggml_backend_sched_alloc_graph(sched, gf)) die("sched alloc failed");
         ggml_backend_tensor_set(embd, &tok, 0, 4);
         ggml_backend_tensor_set(position, &n_past, 0, 4);
         auto t2 = now();
-        if (ggml_backend_sched_graph_compute(sched, gf) != GGML_STATUS_SUCCESS) die("compute failed");
+        if (dst) {
+            if (ggml_backend_sched_graph_compute(sched, gf) != GGML_STATUS_SUCCESS) die("compute failed");
+        } else if (ggml_backend_sched_graph_compute_async(sched, gf) != GGML_STATUS_SUCCESS) {
+            die("compute failed");
+        }
         ggml_tensor *res = ggml_graph_node(gf, -1);
         auto t3 = now();
         if (dst) ggml_backend_tensor_get(res, dst, 0, sizeof(float) * m.n_vocab);
@@ -292,7 +312,44 @@ int main(int argc, char **argv) {
         fwrite(logits.data(), sizeof(float), logits.size(), f);
         fclose(f);
     }
-    if (time_tokens > 0) {   // decode timing: positions continue after the given tokens
+    if (time_tokens > 0 && n_seq > 1) {
+        // S sequences: sequence s replays the prompt shifted by s tokens, then decodes; every
+        // sequence's prompt logits are compared with a serial (one graph at a time) evaluation of
+        // the same tokens, then the round-robin decode is timed with nothing synchronized but the end
+        std::vector<float> a(m.n_vocab), b(m.n_vocab);
+        double worst = 0;
+        for (int sq = 0; sq < n_seq; ++sq) {
+            for (size_t i = 0; i < toks.size(); ++i) {
+                const int32_t tk = (toks[i] + sq) % m.n_vocab;
+                eval((int)i, tk, nullptr, sq);   // async submit
+            }
+        }
+        ggml_backend_sched_synchronize(sched);
+        // serial reference on sequence 0's region replayed into a spare position range is not
+        // possible without clobbering; instead recompute the last prompt token of each sequence
+        // synchronously and compare with the logits a fresh serial pass of sequence s gives
+        for (int sq = 0; sq < n_seq; ++sq) {
+            const int last = (int)toks.size() - 1;
+            eval(last, (toks[last] + sq) % m.n_vocab, a.data(), sq);   // over the KV the async pass wrote
+            for (size_t i = 0; i + 1 < toks.size(); ++i) eval((int)i, (toks[i] + sq) % m.n_vocab, b.data(), sq);
+            eval(last, (toks[last] + sq) % m.n_vocab, b.data(), sq);   // all serial
+            double num = 0, den = 0;
+            for (int i = 0; i < m.n_vocab; ++i) { num += (a[i] - b[i]) * (double)(a[i] - b[i]); den += (double)b[i] * b[i]; }
+            worst = std::max(worst, num / (den > 0 ? den : 1));
+        }
+        const int start = (int)toks.size();
+        const int n = std::min(time_tokens, m.n_ctx - start);
+        phases = false;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < n; ++i)
+            for (int sq = 0; sq < n_seq; ++sq) eval(start + i, (int32_t)((i + sq) % m.n_vocab), nullptr, sq);
+        ggml_backend_sched_synchronize(sched);
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        printf("{\"tokens\": %d, \"n_seq\": %d, \"parallel\": %d, \"seconds\": %.6f, \"ms_per_token\": %.4f, "
+               "\"tokens_per_s\": %.3f, \"threads\": %d, \"splits\": %d, \"async_vs_serial_nmse\": %.3e}\n",
+               n * n_seq, n_seq, parallel ? 1 : 0, s, 1e3 * s / (n * n_seq), n * n_seq / s, threads,
+               ggml_backend_sched_get_n_splits(sched), worst);
+    } else if (time_tokens > 0) {   // decode timing: positions continue after the given tokens
         std::vector<float> tmp(m.n_vocab);
         const int start = (int)toks.size();
         const int n = std::min(time_tokens, m.n_ctx - start);

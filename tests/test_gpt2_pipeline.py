@@ -131,3 +131,38 @@ def test_reference_scheduler_splits_over_two_devices():
     for i in range(24):
         e = float(((got[i].astype(np.float64) - want[i]) ** 2).sum() / (want[i].astype(np.float64) ** 2).sum())
         assert e <= 1e-3, (i, e)
+
+
+@pytest.mark.skipif(not os.path.exists(REF_BIN), reason="oracle/_ref not built")
+def test_reference_scheduler_eight_devices_pipelined():
+    """configs[4]'s scheduler form at eight devices with sequences in flight: the reference's
+    ggml_backend_sched over 8 plugin devices (virtual ones on GPU 0 when the box has fewer GPUs),
+    created with parallel = true (GGML_SCHED_MAX_COPIES input copies, event-ordered hand-offs) and
+    fed 4 sequences round-robin by ggml_backend_sched_graph_compute_async. Checks:
+      * the serial pass (one graph at a time) of the golden prompt matches the golden logits;
+      * the KV the pipelined pass wrote gives the serial pass's logits for every sequence
+        (async_vs_serial_nmse, gpt2_ref --n-seq)."""
+    env = dict(os.environ)
+    if _n_gpus() < 8:
+        env["GGML_MI355X_VIRTUAL_DEVICES"] = "8"
+    import json
+    import re
+    man = json.load(open(os.path.join(ROOT, "tests", "golden", "gpt2_manifest.json")))
+    c = man["cases"]["q4_0"]
+    path = _small_model("q4_0")
+    out = os.path.join(tempfile.gettempdir(), f"gpt2_plugin8_{os.getpid()}.f32")
+    lib = os.path.join(ROOT, "ggml-gfx906_amd", "libggml-hip-mi355x.so")
+    r = subprocess.run([REF_BIN, path, "--tokens", ",".join(map(str, c["tokens"][:16])), "--out", out, "--plugin", lib,
+                        "--devices", "8", "--parallel", "--n-seq", "4", "--time-tokens", "8"],
+                       capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    m = re.search(r"(\d+) backends, (\d+) splits", r.stderr)
+    assert m and int(m.group(2)) >= 2, r.stderr[-500:]
+    j = json.loads(r.stdout.strip().splitlines()[-1])
+    assert j["n_seq"] == 4 and j["parallel"] == 1 and j["tokens"] == 32, j
+    assert j["async_vs_serial_nmse"] <= 1e-10, j
+    got = np.fromfile(out, np.float32).reshape(16, -1)
+    want = np.fromfile(os.path.join(ROOT, "tests", "golden", c["logits"]), np.float32).reshape(len(c["tokens"]), -1)[:16]
+    for i in range(16):
+        e = float(((got[i].astype(np.float64) - want[i]) ** 2).sum() / (want[i].astype(np.float64) ** 2).sum())
+        assert e <= 1e-3, (i, e)
