@@ -55,6 +55,7 @@ sys.path.insert(0, os.path.join(ROOT, "ggml-gfx906_amd"))
 import mi355x_qmm as M  # noqa: E402
 
 MFMA_F16_PEAK_TFLOPS = 2500.0   # dense f16/bf16 MFMA peak, MI355X_MICROARCH.md (no sparsity)
+MFMA_I8_PEAK_TOPS = 5000.0      # dense int8 MFMA peak (2x the bf16 rate, MI355X_MICROARCH.md MFMA table)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 HBM_MEASURED_GBS = 6290.0      # float4 copy measured on MI355X (same guide)
 I8_PEAK_TOPS = 5000.0          # dense int8 / fp8 MFMA (no sparsity)
@@ -168,7 +169,9 @@ def config_row(s: MatVecSet, us: float) -> dict:
     row = {"us": round(us, 3), "GB/s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
            "TFLOP/s": round(tf, 3)}
     if s.Mc > 8:   # mat-mat path: f16 MFMA tiles, priced against the dense f16 peak
-        row.update(bound="mfma", mfma_frac_f16=round(tf / MFMA_F16_PEAK_TFLOPS, 4),
+        # the default mat-mat path is the int8 tile (v_mfma_i32_32x32x32_i8): priced against the
+        # dense int8 peak
+        row.update(bound="mfma", mfma_frac_i8=round(tf / MFMA_I8_PEAK_TOPS, 4),
                    graph_period_us=round(s.graph_period_us(16), 3))
     return row
 
@@ -603,8 +606,12 @@ def main() -> None:
             ("q6_K_4096x11008_m1_b24", M.Q6_K, 4096, 11008, 1, 24),
             ("q8_0_4096x4096_m512", M.Q8_0, 4096, 4096, 512, 1),
             ("q4_K_4096x4096_m512", M.Q4_K, 4096, 4096, 512, 1),
+            # the same with the weights in the repacked layout (ggml_mi355x_repack, made once as a
+            # repacked weight buffer does at upload)
+            ("q8_0_4096x4096_m512_repacked", M.Q8_0, 4096, 4096, 512, 1),
+            ("q4_K_4096x4096_m512_repacked", M.Q4_K, 4096, 4096, 512, 1),
         ):
-            s2 = MatVecSet(torch, t, K, N, Mc, batch, 2 if batch > 1 else 24)
+            s2 = MatVecSet(torch, t, K, N, Mc, batch, 2 if batch > 1 else 24, repacked=name.endswith("_repacked"))
             s2.launch(0)
             torch.cuda.synchronize()
             extra[name] = config_row(s2, s2.launch_us(16))

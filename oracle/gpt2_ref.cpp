@@ -176,6 +176,7 @@ int main(int argc, char **argv) {
     std::vector<ggml_backend_buffer_t> bufs;
     for (int p = 0; p < n_place; ++p) {
         ggml_backend_buffer_type_t bt = D > 0 ? ggml_backend_get_default_buffer_type(gpus[p]) : ggml_backend_cpu_buffer_type();
+        if (ggml_get_first_tensor(m.ctxs[p]) == nullptr) continue;   // more devices than layers: nothing placed here
         ggml_backend_buffer_t b = ggml_backend_alloc_ctx_tensors_from_buft(m.ctxs[p], bt);
         if (!b) die("weight buffer allocation failed");
         ggml_backend_buffer_clear(b, 0);
