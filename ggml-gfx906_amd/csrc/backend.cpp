@@ -125,9 +125,27 @@ struct ShardLane {
 
 // graph fusion plan of one graph_compute (be_graph_compute): nodes skipped because a later fused
 // launch computes them, and the fused attention launches by node index
+// a whole GPT-2 decode layer (main-sched.cpp:600-812, one token) run as the engine's two launches
+// (gpt2_block.hip); see plan_layers
+struct LayerRun {
+    int last = 0;                              // graph index of the layer's output node
+    int type = 0, E = 0, n_head = 0, n_past = 0;
+    const float *x = nullptr;                  // layer input (its first NORM's source)
+    float *out = nullptr;                      // layer output (the last ADD)
+    const float *ln1_g = nullptr, *ln1_b = nullptr, *ln2_g = nullptr, *ln2_b = nullptr;
+    float eps1 = 0.f, eps2 = 0.f, scale = 0.f;
+    const uint8_t *w_qkv = nullptr, *w_o = nullptr, *w_fc = nullptr, *w_mp = nullptr;
+    int64_t nb_qkv = 0, nb_o = 0, nb_fc = 0, nb_mp = 0;
+    const float *b_qkv = nullptr, *b_o = nullptr, *b_fc = nullptr, *b_mp = nullptr;
+    float *kc = nullptr, *vc = nullptr;        // this layer's key / value rows (row p at p * E)
+    const struct ggml_tensor *out_t = nullptr;
+    bool chain_in = false, chain_out = false;  // residual from / to the neighbouring fused layer
+    const float *b_in = nullptr;               // chain_in: the previous layer's MLP-projection bias
+};
 struct FusePlan {
     std::vector<int8_t> skip;
     std::map<int, AttnView> attn;
+    std::map<int, LayerRun> layers;   // by the graph index of the layer's first node
 };
 
 // hipGraph of the last graph_compute (cf. the reference's CUDA graphs, ggml-cuda.cu:2757-2998):
@@ -169,6 +187,12 @@ struct BackendCtx {
     std::vector<std::unique_ptr<ShardLane>> shards;
     FusePlan plan;                    // reused across graph_compute calls (no per-call allocation)
     GraphCache hg;
+    // fused GPT-2 layers (plan_layers): partial slabs, the materialized residuals and the
+    // position, allocated with the backend (a graph_compute may run inside a stream capture)
+    float *lf_attn = nullptr, *lf_mlp = nullptr, *lf_x = nullptr, *lf_y = nullptr;
+    int32_t *lf_pos = nullptr;
+    void *lf_mem = nullptr;
+    hipStream_t aux = nullptr;        // weight copies made for fused layers (not captured)
 };
 
 const char *BUFT_TAG = "MI355X";
@@ -176,6 +200,7 @@ const char *BUFT_TAG = "MI355X";
 DeviceCtx *dev_ctx(ggml_backend_dev_t d) { return static_cast<DeviceCtx *>(d->context); }
 
 bool is_our_buft(ggml_backend_buffer_type_t buft);
+void lr_invalidate(int device, const void *p, size_t n);   // fused-layer weight copies (plan_layers)
 
 bool is_view_op(int op) {
     return op == GGMLABI_OP_NONE || op == GGMLABI_OP_RESHAPE || op == GGMLABI_OP_VIEW || op == GGMLABI_OP_PERMUTE ||
@@ -248,6 +273,7 @@ bool graph_op_of(const struct ggml_tensor *node, GraphOp &g) {
 // ------------------------------------------------------------------------------------------
 void buf_free(ggml_backend_buffer_t b) {
     auto *c = static_cast<BufferCtx *>(b->context);
+    lr_invalidate(c->device, c->base, b->size);
     HIP_OK(hipSetDevice(c->device));
     HIP_OK(hipFree(c->base));
     delete c;
@@ -262,6 +288,7 @@ void buf_memset(ggml_backend_buffer_t b, struct ggml_tensor *t, uint8_t v, size_
     HIP_OK(hipSetDevice(c->device));
     HIP_OK(hipMemsetAsync(static_cast<uint8_t *>(t->data) + off, v, n, nullptr));
     HIP_OK(hipStreamSynchronize(nullptr));
+    lr_invalidate(c->device, static_cast<uint8_t *>(t->data) + off, n);
 }
 
 void buf_set(ggml_backend_buffer_t b, struct ggml_tensor *t, const void *data, size_t off, size_t n) {
@@ -269,6 +296,7 @@ void buf_set(ggml_backend_buffer_t b, struct ggml_tensor *t, const void *data, s
     HIP_OK(hipSetDevice(c->device));
     HIP_OK(hipMemcpyAsync(static_cast<uint8_t *>(t->data) + off, data, n, hipMemcpyHostToDevice, nullptr));
     HIP_OK(hipStreamSynchronize(nullptr));
+    lr_invalidate(c->device, static_cast<uint8_t *>(t->data) + off, n);
 }
 
 void buf_get(ggml_backend_buffer_t b, const struct ggml_tensor *t, void *data, size_t off, size_t n) {
@@ -291,6 +319,7 @@ bool buf_cpy(ggml_backend_buffer_t b, const struct ggml_tensor *src, struct ggml
         HIP_OK(hipMemcpyPeerAsync(dst->data, dc->device, src->data, sc->device, n, nullptr));
     }
     HIP_OK(hipStreamSynchronize(nullptr));
+    lr_invalidate(dc->device, dst->data, n);
     return true;
 }
 
@@ -299,6 +328,7 @@ void buf_clear(ggml_backend_buffer_t b, uint8_t v) {
     HIP_OK(hipSetDevice(c->device));
     HIP_OK(hipMemsetAsync(c->base, v, b->size, nullptr));
     HIP_OK(hipStreamSynchronize(nullptr));
+    lr_invalidate(c->device, c->base, b->size);
 }
 
 const struct ggml_backend_buffer_i BUFFER_IFACE = {
@@ -682,6 +712,8 @@ void be_free(ggml_backend_t b) {
     HIP_OK(hipStreamSynchronize(c->stream));
     if (c->hg.exec) HIP_OK(hipGraphExecDestroy(c->hg.exec));
     HIP_OK(hipStreamDestroy(c->stream));
+    HIP_OK(hipStreamDestroy(c->aux));
+    if (c->lf_mem) HIP_OK(hipFree(c->lf_mem));
     if (c->src1_ready) HIP_OK(hipEventDestroy(c->src1_ready));
     if (c->copy_done) HIP_OK(hipEventDestroy(c->copy_done));
     for (auto &L : c->shards) {
@@ -1305,12 +1337,285 @@ void match_attention(const struct ggml_cgraph *g, int n, int ism, FusePlan &plan
     plan.attn[ianchor] = a;
 }
 
-void plan_fusion(const struct ggml_cgraph *g, int n, FusePlan &plan) {
+// ------------------------------------------------------------------------------------------
+// GPT-2 layer fusion (a graph pre-pass, like the attention fusion below it in the plan). One
+// decode layer of the reference example (main-sched.cpp:600-812 at N = 1: norm -> qkv -> K / V
+// cache copies -> attention -> c_proj + residual -> norm -> fc + GELU -> proj + residual, ~28
+// compute nodes) whose intermediates nobody outside the layer reads runs as the decode engine's
+// two launches (gpt2_block.hip: the attention block and the MLP block, K-split c_proj and MLP
+// projection as f32 partial slabs). Consecutive fused layers pass the residual as (base, bias,
+// partials), summed by the next launch's prologue, exactly as the engine does; the last one of
+// a run materializes its output node with one resid launch. Same arithmetic as the node-by-node
+// path (int8 activations per 32-block, f32 scales), only the fp32 order of the K-split sums
+// differs. GGML_MI355X_LAYER_FUSION=0 turns it off.
+// ------------------------------------------------------------------------------------------
+bool layer_fusion_on() {
+    static const bool on = !(getenv("GGML_MI355X_LAYER_FUSION") && atoi(getenv("GGML_MI355X_LAYER_FUSION")) == 0);
+    return on;
+}
+
+// head-major c_proj and slice-major MLP-projection copies of a fused layer's weights (Q4_0 /
+// Q8_0: the block kernels stream those K-splits contiguously, gpt2_block_repack). Made on first
+// use and kept while the weights' bytes are unchanged: every write into one of our buffers drops
+// the copies whose source bytes it overlaps (lr_invalidate).
+struct LayerCopies {
+    int device;
+    uintptr_t o0, o1, m0, m1;   // source byte ranges (c_proj, MLP projection)
+    uint8_t *o, *mp;            // one allocation: c_proj copy, then the projection copy
+};
+std::mutex g_lr_mu;
+std::vector<LayerCopies> g_lr;
+
+void lr_invalidate(int device, const void *p, size_t n) {
+    const uintptr_t a0 = reinterpret_cast<uintptr_t>(p), a1 = a0 + n;
+    std::lock_guard<std::mutex> lk(g_lr_mu);
+    for (size_t i = 0; i < g_lr.size();) {
+        const LayerCopies &L = g_lr[i];
+        if (L.device == device && ((a0 < L.o1 && L.o0 < a1) || (a0 < L.m1 && L.m0 < a1))) {
+            HIP_OK(hipSetDevice(device));
+            HIP_OK(hipFree(L.o));   // (hipFree waits for the kernels still reading it)
+            g_lr[i] = g_lr.back();
+            g_lr.pop_back();
+        } else {
+            ++i;
+        }
+    }
+}
+
+// the copies of (w_o, w_mp) on c's device; nullptr when they would have to be made inside a
+// stream capture (the caller then fails the capture and the eager run makes them)
+bool layer_copies(BackendCtx *c, int type, int E, const uint8_t *w_o, size_t o_bytes, const uint8_t *w_mp, size_t mp_bytes,
+                  const uint8_t *&o, const uint8_t *&mp) {
+    const uintptr_t o0 = reinterpret_cast<uintptr_t>(w_o), m0 = reinterpret_cast<uintptr_t>(w_mp);
+    {
+        std::lock_guard<std::mutex> lk(g_lr_mu);
+        for (const LayerCopies &L : g_lr)
+            if (L.device == c->device && L.o0 == o0 && L.m0 == m0) {
+                o = L.o;
+                mp = L.mp;
+                return true;
+            }
+    }
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(c->stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+    size_t ob = 0, mb = 0;
+    (void)gpt2_block_repack(type, E, nullptr, nullptr, nullptr, nullptr, &ob, &mb, nullptr);
+    LayerCopies L{c->device, o0, o0 + o_bytes, m0, m0 + mp_bytes, nullptr, nullptr};
+    HIP_OK(hipMalloc(&L.o, ob + mb));
+    L.mp = L.o + ob;
+    // the weights were written by synchronous set_tensor calls; earlier graph work on the
+    // backend stream may still read other buffers, not these new copies
+    HIP_OK(gpt2_block_repack(type, E, w_o, L.o, w_mp, L.mp, nullptr, nullptr, c->aux));
+    HIP_OK(hipStreamSynchronize(c->aux));
+    std::lock_guard<std::mutex> lk(g_lr_mu);
+    g_lr.push_back(L);
+    o = L.o;
+    mp = L.mp;
+    return true;
+}
+
+bool quant_2d(const struct ggml_tensor *w, int64_t ne0, int64_t ne1) {
+    return is_hot_quant(w->type) && w->ne[0] == ne0 && w->ne[1] == ne1 && w->ne[2] == 1 && w->ne[3] == 1 &&
+           (int64_t)w->nb[0] == type_bytes(w->type) && !(w->buffer && is_split_buft(w->buffer->buft));
+}
+
+// one layer starting at the NORM node i; the run's nodes are consecutive in the node order (the
+// example's graph builds them so: the cache copies are expanded first, then the rest of the
+// layer, main-sched.cpp:650-655). True and r filled when every check passes.
+bool match_layer(const struct ggml_cgraph *g, int n, int i, LayerRun &r) {
+    struct ggml_tensor *nodes[24];
+    int idx[24], k = 0;
+    for (int j = i; j < n && k < 24; j = next_compute(g, j, n)) {
+        idx[k] = j;
+        nodes[k++] = g->nodes[j];
+        if (j == n - 1) break;
+    }
+    if (k < 24) return false;
+#define NOLAYER(why)                                                      \
+    do {                                                                  \
+        logf("layer at %s not fused: %s\n", g->nodes[i]->name, why);      \
+        return false;                                                     \
+    } while (0)
+    auto op_is = [](const struct ggml_tensor *t, int op) { return t->op == op; };
+    struct ggml_tensor *n0 = nodes[0], *mul1 = nodes[1], *add1 = nodes[2], *mq = nodes[3], *qb = nodes[4];
+    const struct ggml_tensor *X = n0->src[0];
+    if (!op_is(n0, GGMLABI_OP_NORM) || !f32_2d(X) || X->ne[1] != 1 || !f32_2d(n0) || !same_shape_t(X, n0)) return false;
+    const int64_t E = X->ne[0];
+    if (E % 64 != 0 || !gpt2_block_supported((int)E, (int)(E / 64))) return false;
+    if (!op_is(mul1, GGMLABI_OP_MUL) || mul1->src[0] != n0 || !f32_vec(mul1->src[1], E)) return false;
+    if (!op_is(add1, GGMLABI_OP_ADD) || add1->src[0] != mul1 || !f32_vec(add1->src[1], E)) return false;
+    if (!op_is(mq, GGMLABI_OP_MUL_MAT) || mq->src[1] != add1 || !quant_2d(mq->src[0], E, 3 * E)) return false;
+    if (!op_is(qb, GGMLABI_OP_ADD) || qb->src[0] != mq || !f32_vec(qb->src[1], 3 * E) || !f32_2d(qb)) return false;
+    const int T = mq->src[0]->type;
+    // K / V cache copies: rows E.. and 2E.. of qkv into views of the caches
+    struct ggml_tensor *ck = nodes[5], *cv = nodes[6];
+    auto qkv_view = [&](const struct ggml_tensor *v, size_t off) {
+        return v && v->view_src == qb && v->view_offs == off && v->ne[0] == E && v->ne[1] == 1 && v->type == GGMLABI_TYPE_F32 &&
+               v->nb[0] == 4;
+    };
+    if (!op_is(ck, GGMLABI_OP_CPY) || !op_is(cv, GGMLABI_OP_CPY) || !qkv_view(ck->src[0], 4 * E) || !qkv_view(cv->src[0], 8 * E))
+        NOLAYER("K / V cache copies");
+    if (ck->type != GGMLABI_TYPE_F32 || cv->type != GGMLABI_TYPE_F32 || !f32_dense(ck) || !f32_dense(cv)) NOLAYER("cache type");
+    // Q contiguous and V^T (either order), then KQ, scale, mask, soft_max, KQV, merge
+    struct ggml_tensor *qc = nodes[7], *vt = nodes[8];
+    if (qc->src[0] && qc->src[0]->view_src != qb) std::swap(qc, vt);
+    if (!op_is(qc, GGMLABI_OP_CONT) || !qkv_view(qc->src[0], 0) || qc->ne[0] != 64 || qc->ne[1] != E / 64 || qc->ne[2] != 1)
+        NOLAYER("Q");
+    const int H = (int)(E / 64);
+    struct ggml_tensor *kq = nodes[9], *sc = nodes[10], *dm = nodes[11], *sm = nodes[12], *kqv = nodes[13], *cur = nodes[14];
+    if (!op_is(kq, GGMLABI_OP_MUL_MAT) || !op_is(sc, GGMLABI_OP_SCALE) || !op_is(dm, GGMLABI_OP_DIAG_MASK_INF) ||
+        !op_is(sm, GGMLABI_OP_SOFT_MAX) || !op_is(kqv, GGMLABI_OP_MUL_MAT) || !op_is(cur, GGMLABI_OP_CONT))
+        NOLAYER("attention ops");
+    const struct ggml_tensor *K = kq->src[0], *Q = kq->src[1];
+    if (!Q || Q->view_src != qc || Q->ne[0] != 64 || Q->ne[1] != 1 || Q->ne[2] != H) NOLAYER("Q permute");
+    const int n_past = dm->op_params[0];
+    const int64_t n_kv = n_past + 1;
+    if (n_past < 0 || K->type != GGMLABI_TYPE_F32 || K->ne[0] != 64 || K->ne[1] != n_kv || K->ne[2] != H || K->nb[0] != 4 ||
+        (int64_t)K->nb[1] != 4 * E || K->nb[2] != 256 || !K->view_src)
+        NOLAYER("K view");
+    if (sc->src[0] != kq || dm->src[0] != sc || sm->src[0] != dm || sm->src[1] || sm->src[2]) NOLAYER("score chain");
+    float s_scale, s_bias, sm_scale, max_bias;
+    std::memcpy(&s_scale, &sc->op_params[0], 4);
+    std::memcpy(&s_bias, &sc->op_params[1], 4);
+    std::memcpy(&sm_scale, &sm->op_params[0], 4);
+    std::memcpy(&max_bias, &sm->op_params[1], 4);
+    if (s_bias != 0.f || sm_scale != 1.f || max_bias != 0.f) NOLAYER("score parameters");
+    const struct ggml_tensor *P = vt->src[0];
+    if (!op_is(vt, GGMLABI_OP_CONT) || kqv->src[0] != vt || kqv->src[1] != sm || !P || !P->view_src || P->type != GGMLABI_TYPE_F32 ||
+        P->ne[0] != n_kv || P->ne[1] != 64 || P->ne[2] != H || (int64_t)P->nb[0] != 4 * E || P->nb[1] != 4 || P->nb[2] != 256 ||
+        vt->ne[0] != n_kv || vt->ne[1] != 64 || vt->ne[2] != H)
+        NOLAYER("V^T");
+    float *kc = static_cast<float *>(K->data), *vc = static_cast<float *>(P->data);
+    if (ck->data != kc + n_past * E || cv->data != vc + n_past * E) NOLAYER("cache copies are not row n_past of the caches read");
+    const struct ggml_tensor *mg = cur->src[0];
+    if (!mg || mg->view_src != kqv || kqv->ne[0] != 64 || kqv->ne[1] != 1 || kqv->ne[2] != H || cur->ne[0] != E || cur->ne[1] != 1)
+        NOLAYER("attention output");
+    // c_proj + bias + residual, then the MLP
+    struct ggml_tensor *mo = nodes[15], *ob = nodes[16], *r1 = nodes[17], *n1 = nodes[18], *mul2 = nodes[19], *add2 = nodes[20];
+    struct ggml_tensor *mf = nodes[21], *fb = nodes[22], *ge = nodes[23];
+    if (!op_is(mo, GGMLABI_OP_MUL_MAT) || mo->src[1] != cur || !quant_2d(mo->src[0], E, E) || mo->src[0]->type != T) NOLAYER("c_proj");
+    if (!op_is(ob, GGMLABI_OP_ADD) || ob->src[0] != mo || !f32_vec(ob->src[1], E)) NOLAYER("c_proj bias");
+    if (!op_is(r1, GGMLABI_OP_ADD) || !((r1->src[0] == ob && r1->src[1] == X) || (r1->src[0] == X && r1->src[1] == ob)))
+        NOLAYER("attention residual");
+    if (!op_is(n1, GGMLABI_OP_NORM) || n1->src[0] != r1) NOLAYER("ln_2");
+    if (!op_is(mul2, GGMLABI_OP_MUL) || mul2->src[0] != n1 || !f32_vec(mul2->src[1], E)) NOLAYER("ln_2 gain");
+    if (!op_is(add2, GGMLABI_OP_ADD) || add2->src[0] != mul2 || !f32_vec(add2->src[1], E)) NOLAYER("ln_2 bias");
+    if (!op_is(mf, GGMLABI_OP_MUL_MAT) || mf->src[1] != add2 || !quant_2d(mf->src[0], E, 4 * E) || mf->src[0]->type != T)
+        NOLAYER("fc");
+    if (!op_is(fb, GGMLABI_OP_ADD) || fb->src[0] != mf || !f32_vec(fb->src[1], 4 * E)) NOLAYER("fc bias");
+    if (!op_is(ge, GGMLABI_OP_UNARY) || ge->op_params[0] != GGMLABI_UNARY_OP_GELU || ge->src[0] != fb) NOLAYER("gelu");
+    const int j24 = next_compute(g, idx[23], n), j25 = j24 < n ? next_compute(g, j24, n) : n, j26 = j25 < n ? next_compute(g, j25, n) : n;
+    if (j26 >= n) NOLAYER("graph ends inside the layer");
+    struct ggml_tensor *mp = g->nodes[j24], *pb = g->nodes[j25], *r2 = g->nodes[j26];
+    if (!op_is(mp, GGMLABI_OP_MUL_MAT) || mp->src[1] != ge || !quant_2d(mp->src[0], 4 * E, E) || mp->src[0]->type != T) NOLAYER("mlp proj");
+    if (!op_is(pb, GGMLABI_OP_ADD) || pb->src[0] != mp || !f32_vec(pb->src[1], E)) NOLAYER("mlp proj bias");
+    if (!op_is(r2, GGMLABI_OP_ADD) || !((r2->src[0] == pb && r2->src[1] == r1) || (r2->src[0] == r1 && r2->src[1] == pb)) ||
+        !f32_2d(r2) || !same_shape_t(r2, X))
+        NOLAYER("mlp residual");
+    // every tensor the layer produces (views included) is read only inside the layer and is not
+    // a requested output, except the layer's output
+    std::map<const struct ggml_tensor *, int> uses;
+    for (int j = i; j <= j26; ++j)
+        for (int s = 0; s < GGMLABI_MAX_SRC; ++s)
+            if (g->nodes[j]->src[s]) ++uses[g->nodes[j]->src[s]];
+    for (int j = i; j < j26; ++j) {
+        const struct ggml_tensor *t = g->nodes[j];
+        if (t->flags & GGMLABI_TENSOR_FLAG_OUTPUT) NOLAYER("an intermediate is a requested output");
+        const int u = use_count(g, t);
+        if (u < 0 || u != uses[t]) NOLAYER("an intermediate is read outside the layer");
+    }
+    // (the output may sit on the input's memory: the input is read by the first launch only, the
+    // output written by the last)
+    if (!disjoint(r2, K) || !disjoint(r2, P)) NOLAYER("output overlaps the caches");
+#undef NOLAYER
+    r = LayerRun{};
+    r.last = j26;
+    r.type = T;
+    r.E = (int)E;
+    r.n_head = H;
+    r.n_past = n_past;
+    r.x = static_cast<const float *>(X->data);
+    r.out = static_cast<float *>(r2->data);
+    r.out_t = r2;
+    r.ln1_g = static_cast<const float *>(mul1->src[1]->data);
+    r.ln1_b = static_cast<const float *>(add1->src[1]->data);
+    r.ln2_g = static_cast<const float *>(mul2->src[1]->data);
+    r.ln2_b = static_cast<const float *>(add2->src[1]->data);
+    std::memcpy(&r.eps1, &n0->op_params[0], 4);
+    std::memcpy(&r.eps2, &n1->op_params[0], 4);
+    r.scale = s_scale;
+    r.w_qkv = static_cast<const uint8_t *>(mq->src[0]->data);
+    r.nb_qkv = (int64_t)mq->src[0]->nb[1];
+    r.w_o = static_cast<const uint8_t *>(mo->src[0]->data);
+    r.nb_o = (int64_t)mo->src[0]->nb[1];
+    r.w_fc = static_cast<const uint8_t *>(mf->src[0]->data);
+    r.nb_fc = (int64_t)mf->src[0]->nb[1];
+    r.w_mp = static_cast<const uint8_t *>(mp->src[0]->data);
+    r.nb_mp = (int64_t)mp->src[0]->nb[1];
+    r.b_qkv = static_cast<const float *>(qb->src[1]->data);
+    r.b_o = static_cast<const float *>(ob->src[1]->data);
+    r.b_fc = static_cast<const float *>(fb->src[1]->data);
+    r.b_mp = static_cast<const float *>(pb->src[1]->data);
+    r.kc = kc;
+    r.vc = vc;
+    return true;
+}
+
+void plan_layers(BackendCtx *c, const struct ggml_cgraph *g, int n, FusePlan &plan) {
+    plan.layers.clear();
+    if (!layer_fusion_on() || c->lf_mem == nullptr) return;
+    LayerRun *prev = nullptr;
+    for (int i = 0; i < n; ++i) {
+        if (g->nodes[i]->op != GGMLABI_OP_NORM || plan.skip[i]) continue;
+        LayerRun r;
+        if (!match_layer(g, n, i, r)) continue;
+        // chained: this layer's input is the previous fused layer's output, read by nothing else
+        if (prev && prev->out == r.x && prev->E == r.E && next_compute(g, prev->last, n) == i && use_count(g, prev->out_t) == 2 &&
+            !(prev->out_t->flags & GGMLABI_TENSOR_FLAG_OUTPUT)) {
+            prev->chain_out = true;
+            r.chain_in = true;
+            r.b_in = prev->b_mp;
+        }
+        for (int j = i + 1; j <= r.last; ++j) plan.skip[j] = 1;
+        auto it = plan.layers.emplace(i, r).first;
+        prev = &it->second;
+        logf("layer fused: %s .. %s (n_past %d%s%s)\n", g->nodes[i]->name, g->nodes[r.last]->name, r.n_past,
+             r.chain_in ? ", residual from the previous layer" : "", r.chain_out ? ", residual to the next layer" : "");
+        i = r.last;
+    }
+}
+
+int run_layer(BackendCtx *c, const LayerRun &r) {
+    const uint8_t *w_o = r.w_o, *w_mp = r.w_mp;
+    if (gpt2_block_repacks(r.type) &&
+        !layer_copies(c, r.type, r.E, r.w_o, (size_t)r.nb_o * r.E, r.w_mp, (size_t)r.nb_mp * r.E, w_o, w_mp))
+        return GGML_MI355X_EHIP;   // inside a capture: the eager run makes the copies
+    const int n_sl = gpt2_block_mlp_slices(r.E);
+    auto ok = [](hipError_t e) { return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP; };
+    int rc;
+    // the position, once per run of chained layers (they share n_past)
+    if (!r.chain_in && (rc = ok(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->lf_pos), r.n_past, 1, c->stream)))) return rc;
+    const float *base = r.chain_in ? c->lf_y : r.x;
+    rc = ok(gpt2_attn_block_launch(0, r.type, base, r.b_in, r.chain_in ? c->lf_mlp : nullptr,
+                                   r.chain_in ? n_sl : 0, c->lf_x, r.ln1_g, r.ln1_b, r.eps1, r.w_qkv, r.nb_qkv, r.b_qkv, r.kc,
+                                   r.vc, c->lf_pos, r.scale, r.n_past + 1, w_o, r.nb_o, c->lf_attn, r.E, r.n_head, 1, nullptr, 0,
+                                   nullptr, nullptr, 0, c->stream));
+    if (rc) return rc;
+    rc = ok(gpt2_mlp_block_launch(0, r.type, c->lf_x, r.b_o, c->lf_attn, r.n_head, c->lf_y, r.ln2_g, r.ln2_b, r.eps2, r.w_fc, r.nb_fc,
+                                  r.b_fc, w_mp, r.nb_mp, c->lf_mlp, r.E, r.n_head, 1, c->stream));
+    if (rc) return rc;
+    if (!r.chain_out) rc = ok(gpt2_resid_launch(c->lf_y, r.b_mp, c->lf_mlp, n_sl, r.out, r.E, 1, c->stream));
+    return rc;
+}
+
+void plan_fusion(BackendCtx *c, const struct ggml_cgraph *g, int n, FusePlan &plan) {
     plan.skip.assign(n, 0);
     plan.attn.clear();
+    plan.layers.clear();
     if (!fusion_on()) return;
+    plan_layers(c, g, n, plan);
     for (int i = 0; i < n; ++i)
-        if (g->nodes[i]->op == GGMLABI_OP_SOFT_MAX) match_attention(g, n, i, plan);
+        if (g->nodes[i]->op == GGMLABI_OP_SOFT_MAX && !plan.skip[i]) match_attention(g, n, i, plan);
 }
 
 // queue every node of g on the backend stream (fused runs as planned); quiet: a failure is
@@ -1319,7 +1624,7 @@ enum ggml_status run_nodes(BackendCtx *c, struct ggml_cgraph *g, bool quiet) {
     const GgmlBase &gb = ggml_base();
     const int n = gb.graph_n_nodes(g);
     FusePlan &plan = c->plan;
-    plan_fusion(g, n, plan);
+    plan_fusion(c, g, n, plan);
     for (int i = 0; i < n; ++i) {
         struct ggml_tensor *node = gb.graph_node(g, i);
         if (is_empty(node) || is_view_op(node->op) || plan.skip[i]) continue;
@@ -1327,7 +1632,11 @@ enum ggml_status run_nodes(BackendCtx *c, struct ggml_cgraph *g, bool quiet) {
         GraphOp gop;
         int fused = 0;
         auto at = plan.attn.find(i);
-        if (at != plan.attn.end()) {
+        auto lr = plan.layers.find(i);
+        if (lr != plan.layers.end()) {
+            rc = run_layer(c, lr->second);
+            fused = lr->second.last - i + 1;
+        } else if (at != plan.attn.end()) {
             rc = run_attention(at->second, c->stream);
             logf("fused attention at %s (n_kv=%d, n_q=%d, H=%d)\n", node->name, at->second.n_kv, at->second.n_q, at->second.H);
             fused = 1;
@@ -1529,6 +1838,16 @@ ggml_backend_t dv_init_backend(ggml_backend_dev_t d, const char *) {
     c->name = dc->name;
     HIP_OK(hipSetDevice(c->device));
     HIP_OK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+    {   // fused GPT-2 layers (plan_layers): n_embd <= 1024, <= 16 heads, <= 32 MLP slices, one sequence
+        constexpr size_t E = 1024;
+        HIP_OK(hipMalloc(&c->lf_mem, (16 + 32 + 2) * E * sizeof(float) + 256));
+        c->lf_attn = static_cast<float *>(c->lf_mem);
+        c->lf_mlp = c->lf_attn + 16 * E;
+        c->lf_x = c->lf_mlp + 32 * E;
+        c->lf_y = c->lf_x + E;
+        c->lf_pos = reinterpret_cast<int32_t *>(c->lf_y + E);
+    }
     // raise the fused mat-vec LDS limits now: that is not a stream operation, so it must not
     // first happen inside a hipGraph capture of be_graph_compute
     for (int t : {2, 8, 12, 13, 14}) HIP_OK(mmvq_fused_prepare(t));   // Q4_0 Q8_0 Q4_K Q5_K Q6_K

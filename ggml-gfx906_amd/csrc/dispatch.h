@@ -138,4 +138,25 @@ hipError_t mmvq_fused_launch(int type, const MmArgs &a, int nc, int rpw, hipStre
 hipError_t mmvq_fused_prepare(int type);
 int mmvq_fused_pick_nc(int M, int K);
 
+// the GPT-2 two-launch layer (gpt2_block.hip): used by the decode engine (gpt2.cpp) and by the
+// plugin's graph fusion of whole GPT-2 layers (backend.cpp)
+bool gpt2_block_supported(int n_embd, int n_head);
+int gpt2_block_mlp_slices(int n_embd);
+hipError_t gpt2_attn_block_launch(int layer, int type, const float *base, const float *bias_in, const float *parts_in, int n_parts_in,
+                                  float *x_out, const float *ln_g, const float *ln_b, float eps, const uint8_t *w_qkv,
+                                  int64_t nb_qkv, const float *b_qkv, float *kc, float *vc, const int32_t *pos, float scale,
+                                  int n_ctx, const uint8_t *w_o, int64_t nb_o, float *parts_out, int E, int n_head, int n_seq,
+                                  const uint8_t *wte, int64_t wte_nb, const float *wpe, const int32_t *tokens, int n_vocab,
+                                  hipStream_t st);
+bool gpt2_block_embeds(int type);
+hipError_t gpt2_mlp_block_launch(int layer, int type, const float *base, const float *bias_in, const float *parts_in, int n_parts_in,
+                                 float *x_out, const float *ln_g, const float *ln_b, float eps, const uint8_t *w_fc,
+                                 int64_t nb_fc, const float *b_fc, const uint8_t *w_mp, int64_t nb_mp, float *parts_out, int E,
+                                 int n_head, int n_seq, hipStream_t st);
+bool gpt2_block_repacks(int type);
+hipError_t gpt2_block_repack(int type, int E, const uint8_t *w_o, uint8_t *o_dst, const uint8_t *w_mp, uint8_t *mp_dst,
+                             size_t *o_bytes, size_t *mp_bytes, hipStream_t st);
+hipError_t gpt2_resid_launch(const float *base, const float *bias_in, const float *parts_in, int n_parts_in, float *x_out, int E,
+                             int n_seq, hipStream_t st);
+
 }  // namespace mi355x

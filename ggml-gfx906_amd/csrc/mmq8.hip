@@ -467,6 +467,7 @@ __device__ __forceinline__ void q8_sb_compute(const uint8_t *W, const uint8_t *X
         i32x16 magic;
 #pragma unroll
         for (int i = 0; i < 16; ++i) magic[i] = (int)Q8_MAGIC_I;
+        asm volatile("" : "+v"(magic));   // opaque: not rematerialized, so the pin below holds its registers
         // the magic constant's share, -12582912 * sum(d_w), starts the sums (folded into the first
         // fma of every output instead of a subtraction at the end)
         // (NG = 2 reads the meta again per group rather than holding 16 more registers)
@@ -515,6 +516,9 @@ __device__ __forceinline__ void q8_sb_compute(const uint8_t *W, const uint8_t *X
             __builtin_amdgcn_sched_barrier(0);
             consume(3, Rb0, Rb1);
         }
+        // keep the C-input registers allocated past the last MFMA that reads them (without this
+        // the compiler recycles them as epilogue destinations 7 wait states after that MFMA)
+        asm volatile("" ::"v"(magic));
     } else {   // K-quants: integer sub-block (or 16-group) scales, exact int32 sums
         i32x16 pi0, pi1;
 #pragma unroll
@@ -1088,6 +1092,7 @@ __global__ __launch_bounds__(512) void mmq8r_kernel(const MmArgs a, const RpArgs
     i32x16 cin;   // MFMA C input: the magic constant (float scales) or zero (integer scales)
 #pragma unroll
     for (int i = 0; i < 16; ++i) { acc0[i] = 0.f; acc1[i] = 0.f; cin[i] = F32S ? (int)Q8_MAGIC_I : 0; }
+    asm volatile("" : "+v"(cin));   // opaque: not rematerialized, so the pins after the MFMAs hold its registers
 
     auto compute = [&](int slot, const Meta &g) {
         if constexpr ((MMQ8R_EXP & 4) != 0) {
@@ -1182,6 +1187,7 @@ __global__ __launch_bounds__(512) void mmq8r_kernel(const MmArgs a, const RpArgs
             __builtin_amdgcn_sched_barrier(0);
         }
         consume(NQ - 1, Rb0, Rb1);
+        asm volatile("" ::"v"(cin));   // C-input registers stay allocated past the last MFMA (see q8_sb_compute)
 #pragma unroll
         for (int k = 0; k < 4; ++k) dxv[4 + k] = ld128(X + XI_DX + 4 * (32 + 8 * k + 4 * hl));   // tile 1's
         if constexpr (!F32S) {

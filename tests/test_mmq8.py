@@ -318,3 +318,28 @@ def test_mmq8_two_halves_bitwise_repeatable(mm, t):
     outs = [run_mul_mat(mm, a, b, [N, M_, 1, 1]) for _ in range(3)]
     assert all(np.array_equal(outs[0].view(np.uint32), o.view(np.uint32)) for o in outs[1:])
     assert qref.nmse(outs[0], G.oracle_mul_mat(a, b, [N, M_, 1, 1])) <= TIGHT[t]
+
+
+@pytest.mark.parametrize("t", [qref.Q8_0, qref.Q4_0], ids=lambda t: qref.NAMES[t])
+def test_mmq8_config3_repeat_bitwise(mm, t):
+    """the magic-constant tiles (Q8_0 / Q4_0) at BASELINE configs[3] size, 48 calls back to back:
+    every call bit-identical to the first. The fault this guards against (the
+    packed-f32 fault: the compiler reused the MFMA C-input registers 7 wait states after the last
+    MFMA that read them) showed as a few wrong (register, lane) positions varying run to run."""
+    from test_gpu_parity import dev_bytes
+    N, M_, K = 4096, 512, 4096
+    w = qref.quantize(t, qref.fill_uniform(N * K, 5), n_per_row=K)
+    x = qref.fill_uniform(M_ * K, 6)
+    da, db = dev_bytes(w), dev_bytes(x)
+    A = mm.tensor(t, da.data_ptr(), [K, N, 1, 1], qref.contiguous_nb(t, [K, N, 1, 1]))
+    B = mm.tensor(qref.F32, db.data_ptr(), [K, M_, 1, 1], qref.contiguous_nb(qref.F32, [K, M_, 1, 1]))
+    outs = [torch.empty(M_ * N, dtype=torch.float32, device="cuda") for _ in range(2)]
+    Ds = [mm.tensor(qref.F32, o.data_ptr(), [N, M_, 1, 1], qref.contiguous_nb(qref.F32, [N, M_, 1, 1])) for o in outs]
+    mm.mul_mat(A, B, Ds[0])
+    bad = 0
+    for _ in range(48):
+        outs[1].fill_(float("nan"))
+        mm.mul_mat(A, B, Ds[1])
+        bad += int((outs[0].view(torch.int32) != outs[1].view(torch.int32)).sum().item())
+    assert bad == 0, f"{bad} elements differ from the first call over 48 calls"
+    assert torch.isfinite(outs[0]).all()
