@@ -11,7 +11,8 @@ for f in "$@"; do
   base=$(basename "$f"); stem=${base%.*}
   git show "$rev:$f" > scratch_libs/obj/$name/$base
   cp ggml-gfx906_amd/csrc/*.h scratch_libs/obj/$name/ 2>/dev/null || true
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden -Iinclude -Iggml-gfx906_amd/csrc \
+  x=""; [ "$stem" = mmq8 ] && x="-Xclang -target-feature -Xclang -packed-fp32-ops"   # as the Makefile
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden -Iinclude -Iggml-gfx906_amd/csrc $x \
       -c scratch_libs/obj/$name/$base -o scratch_libs/obj/$name/$stem.o 2>&1 | grep -v "recognized feature" || true
   objs="$objs scratch_libs/obj/$name/$stem.o"
 done
