@@ -362,3 +362,37 @@ def test_reference_scheduler_drives_plugin():
     want = golden_logits("q4_0")[:24]
     errs = [nmse(got[i], want[i]) for i in range(24)]
     assert max(errs) <= NMSE_VS_REF, errs
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REF_BIN), reason="oracle/_ref not built")
+@pytest.mark.parametrize("name", ["q4_0", "q8_0", "q4_K", "q5_K", "q6_K"])
+def test_reference_scheduler_layer_fusion(name):
+    """drop-in, whole-layer fusion (backend.cpp plan_layers): the reference scheduler's GPT-2 with
+    the plugin runs every decode layer as the engine's two launches (the debug log names each
+    fused layer, chained layers pass the residual on as partial slabs) and its logits match the
+    golden ggml-cpu logits, as the node-by-node path (GGML_MI355X_LAYER_FUSION=0) does. Q4_0 / Q8_0
+    read the c_proj / MLP-projection copies the plugin makes, K-quants read the ggml rows in place."""
+    c = MANIFEST["cases"][name]
+    n = 24
+    want = golden_logits(name)[:n]
+    got = {}
+    for fuse in ("1", "0"):
+        out = os.path.join(tempfile.gettempdir(), f"gpt2_plugin_lf{fuse}_{name}_{os.getpid()}.f32")
+        env = dict(os.environ, GGML_MI355X_LAYER_FUSION=fuse, GGML_MI355X_DEBUG="1")
+        r = subprocess.run([REF_BIN, small_model(name), "--tokens", ",".join(map(str, c["tokens"][:n])), "--out", out,
+                            "--plugin", G.Q.LIB_PATH, "--devices", "1"], capture_output=True, text=True, timeout=120, env=env)
+        assert r.returncode == 0, r.stderr[-2000:]
+        fused = [ln for ln in r.stderr.splitlines() if "layer fused" in ln]
+        if fuse == "1":
+            # every decode graph (positions 1 .. n-1) fuses all its layers, chained
+            assert len(fused) >= (n - 1) * SMALL["n_layer"], (len(fused), [ln for ln in r.stderr.splitlines() if "layer" in ln][:5])
+            assert any("residual to the next layer" in ln for ln in fused) or SMALL["n_layer"] == 1
+        else:
+            assert not fused
+        got[fuse] = np.fromfile(out, np.float32).reshape(n, -1)
+        os.remove(out)
+    for fuse, lg in got.items():
+        errs = [nmse(lg[i], want[i]) for i in range(n)]
+        assert max(errs) <= NMSE_VS_REF, (fuse, max(errs))
+    assert max(nmse(got["1"][i], got["0"][i]) for i in range(n)) <= NMSE_VS_REF
