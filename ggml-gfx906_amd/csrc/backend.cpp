@@ -1579,8 +1579,8 @@ void plan_layers(BackendCtx *c, const struct ggml_cgraph *g, int n, FusePlan &pl
         for (int j = i + 1; j <= r.last; ++j) plan.skip[j] = 1;
         auto it = plan.layers.emplace(i, r).first;
         prev = &it->second;
-        logf("layer fused: %s .. %s (n_past %d%s%s)\n", g->nodes[i]->name, g->nodes[r.last]->name, r.n_past,
-             r.chain_in ? ", residual from the previous layer" : "", r.chain_out ? ", residual to the next layer" : "");
+        logf("layer fused: %s .. %s (n_past %d%s)\n", g->nodes[i]->name, g->nodes[r.last]->name, r.n_past,
+             r.chain_in ? ", residual from the previous layer" : "");
         i = r.last;
     }
 }
@@ -1593,8 +1593,6 @@ int run_layer(BackendCtx *c, const LayerRun &r) {
     const int n_sl = gpt2_block_mlp_slices(r.E);
     auto ok = [](hipError_t e) { return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP; };
     int rc;
-    // the position, once per run of chained layers (they share n_past)
-    if (!r.chain_in && (rc = ok(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->lf_pos), r.n_past, 1, c->stream)))) return rc;
     const float *base = r.chain_in ? c->lf_y : r.x;
     rc = ok(gpt2_attn_block_launch(0, r.type, base, r.b_in, r.chain_in ? c->lf_mlp : nullptr,
                                    r.chain_in ? n_sl : 0, c->lf_x, r.ln1_g, r.ln1_b, r.eps1, r.w_qkv, r.nb_qkv, r.b_qkv, r.kc,
@@ -1846,7 +1844,10 @@ ggml_backend_t dv_init_backend(ggml_backend_dev_t d, const char *) {
         c->lf_mlp = c->lf_attn + 16 * E;
         c->lf_x = c->lf_mlp + 32 * E;
         c->lf_y = c->lf_x + E;
+        // the block kernels take the position as min(pos[s], n_ctx - 1): pos holds INT32_MAX and
+        // each launch passes n_ctx = n_past + 1, so no per-token write of the position
         c->lf_pos = reinterpret_cast<int32_t *>(c->lf_y + E);
+        HIP_OK(hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(c->lf_pos), 0x7fffffff, 1));
     }
     // raise the fused mat-vec LDS limits now: that is not a stream operation, so it must not
     // first happen inside a hipGraph capture of be_graph_compute

@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPT-2 attention-block iteration: engine parity tests, A/B against scratch_libs variants, phase stamps
+# GPT-2 attention-block iteration: engine + drop-in parity tests, A/B against scratch_libs variants, phase stamps
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

@@ -39,6 +39,8 @@ step prof_singles 300 $RP -d $O/singles -o run -- python scripts/prof_singles.py
 squash $O/singles
 step prof_mmq 300 $RP -d $O/mmq -o run -- python scripts/mmq_bench.py q8_0:4096:4096:512 q4_K:4096:4096:512 q6_K:4096:11008:512 q4_K:4096:4096:32 q8_0:4096:4096:2048
 squash $O/mmq
+step prof_mmq_rp 300 env MMQ_REPACKED=1 $RP -d $O/mmq_rp -o run -- python scripts/mmq_bench.py q8_0:4096:4096:512 q4_K:4096:4096:512 q6_K:4096:11008:512
+squash $O/mmq_rp
 step prof_gpt2 300 $RP -d $O/gpt2 -o run -- python scripts/gpt2_bench.py 1 256 1
 squash $O/gpt2
 step block_stamps 200 bash -c 'python scripts/block_stamps.py 24 64 && python scripts/block_stamps.py 24 600'

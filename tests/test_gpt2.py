@@ -374,7 +374,7 @@ def test_reference_scheduler_layer_fusion(name):
     golden ggml-cpu logits, as the node-by-node path (GGML_MI355X_LAYER_FUSION=0) does. Q4_0 / Q8_0
     read the c_proj / MLP-projection copies the plugin makes, K-quants read the ggml rows in place."""
     c = MANIFEST["cases"][name]
-    n = 24
+    n = min(24, len(c["tokens"]))
     want = golden_logits(name)[:n]
     got = {}
     for fuse in ("1", "0"):
@@ -386,8 +386,8 @@ def test_reference_scheduler_layer_fusion(name):
         fused = [ln for ln in r.stderr.splitlines() if "layer fused" in ln]
         if fuse == "1":
             # every decode graph (positions 1 .. n-1) fuses all its layers, chained
-            assert len(fused) >= (n - 1) * SMALL["n_layer"], (len(fused), [ln for ln in r.stderr.splitlines() if "layer" in ln][:5])
-            assert any("residual to the next layer" in ln for ln in fused) or SMALL["n_layer"] == 1
+            assert len(fused) >= (n - 1) * SMALL["n_layer"], (len(fused), [ln for ln in r.stderr.splitlines() if "not fused" in ln][:8])
+            assert any("residual from the previous layer" in ln for ln in fused) or SMALL["n_layer"] == 1
         else:
             assert not fused
         got[fuse] = np.fromfile(out, np.float32).reshape(n, -1)
