@@ -30,7 +30,6 @@
 // contiguous. Measured choices: 128-unit slices beat 256 (4207 vs 3850
 // tokens/s, GPT-2 117M Q4_0), LDS-only barriers keep weight streams in flight.
 #include <algorithm>
-#include <type_traits>
 
 #include "mmvq_impl.h"
 
@@ -361,7 +360,6 @@ __device__ __forceinline__ void load_ln(const float *gp, const float *bp, int E,
 // ------------------------------------------------------------------------------------------
 constexpr int AGROUPS = NW * 4;            // 16-lane key groups per workgroup
 constexpr int AU = 8;                      // keys per group in flight per round
-constexpr int AU0 = 2;                     // keys per group issued at the kernel's start (keys 0 .. 63)
 
 template <int T, int QNIT, int RR, bool EMB = false>
 __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
@@ -391,21 +389,6 @@ __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
     const int p = min(max(a.pos[s], 0), a.n_ctx - 1);
     RowsDot<T, 16, 6, QNIT> qd;
     qd.load([&](int vr) { return a.w_qkv + (int64_t)((vr >> 6) * E + h * HD + (vr & 63)) * a.nb_qkv; }, 3 * HD, 0, 0, E / 64);
-    // cached keys / values 0 .. AGROUPS * AU0 - 1 (rows < p: nothing of this launch writes them),
-    // issued behind the weight stream and consumed once q is known, so their latency hides under
-    // the residual, layer-norm and q/k/v phases (exactly the rows needed up to position 64; the
-    // rest stream in the loop below)
-    const float *K = a.kc + (int64_t)s * a.n_ctx * E + h * HD;
-    const float *Vc = a.vc + (int64_t)s * a.n_ctx * E + h * HD;
-    const int grp = wave * 4 + (lane >> 4), d4 = lane & 15;
-    const int nk = p;
-    float4 k0[AU0], v0[AU0];
-#pragma unroll
-    for (int u = 0; u < AU0; ++u) {
-        const int jc = max(min(u * AGROUPS + grp, nk - 1), 0);
-        k0[u] = reinterpret_cast<const float4 *>(K + (int64_t)jc * E)[d4];
-        v0[u] = reinterpret_cast<const float4 *>(Vc + (int64_t)jc * E)[d4];
-    }
     __builtin_amdgcn_sched_barrier(0);
     stamp(a, 0, 8);
     if (a.stamps != nullptr) {   // diagnostics: when this wave's first residual row has landed
@@ -446,24 +429,32 @@ __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
 
     // ---- the new token's K / V row of head h into the cache (the reference's ggml_cpy into
     // memory_k / memory_v, main-sched.cpp:648-655); attention reads key p from LDS
-    float *Kw = a.kc + (int64_t)s * a.n_ctx * E + h * HD;
-    float *Vw = a.vc + (int64_t)s * a.n_ctx * E + h * HD;
-    if (tid < 16) reinterpret_cast<float4 *>(Kw + (int64_t)p * E)[tid] = reinterpret_cast<const float4 *>(qkv_s + HD)[tid];
-    else if (tid < 32) reinterpret_cast<float4 *>(Vw + (int64_t)p * E)[tid - 16] = reinterpret_cast<const float4 *>(qkv_s + 2 * HD)[tid - 16];
+    float *K = a.kc + (int64_t)s * a.n_ctx * E + h * HD;
+    float *Vc = a.vc + (int64_t)s * a.n_ctx * E + h * HD;
+    if (tid < 16) reinterpret_cast<float4 *>(K + (int64_t)p * E)[tid] = reinterpret_cast<const float4 *>(qkv_s + HD)[tid];
+    else if (tid < 32) reinterpret_cast<float4 *>(Vc + (int64_t)p * E)[tid - 16] = reinterpret_cast<const float4 *>(qkv_s + 2 * HD)[tid - 16];
 
     // ---- keys 0 .. p-1 (softmax(K.q * scale) . V, main-sched.cpp:685-735, in the rescaling
     // order of online softmax): a 16-lane group owns one key at a time, lane d4 the dims
-    // 4 d4 .. 4 d4 + 3 (16-B coalesced row reads); keys 0 .. 63 from the start's loads, then
-    // rounds of 32 groups x AU keys in flight
+    // 4 d4 .. 4 d4 + 3 (16-B coalesced row reads); 32 groups x AU keys in flight per round
+    const int grp = wave * 4 + (lane >> 4), d4 = lane & 15;
+    const int nk = p;
     const float4 q4 = reinterpret_cast<const float4 *>(qkv_s)[d4];
     float m = -INFINITY, l = 0.f;
     float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    auto keys = [&](const float4 *kk, const float4 *vv, int jb, auto nu) {
-        constexpr int NU = decltype(nu)::value;
-        float sc[NU];
+    for (int jb = 0; jb < nk; jb += AGROUPS * AU) {
+        float4 kk[AU], vv[AU];
+#pragma unroll
+        for (int u = 0; u < AU; ++u) {
+            const int jc = min(jb + u * AGROUPS + grp, nk - 1);
+            kk[u] = reinterpret_cast<const float4 *>(K + (int64_t)jc * E)[d4];
+            vv[u] = reinterpret_cast<const float4 *>(Vc + (int64_t)jc * E)[d4];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        float sc[AU];
         float mn = m;
 #pragma unroll
-        for (int u = 0; u < NU; ++u) {
+        for (int u = 0; u < AU; ++u) {
             float t = q4.x * kk[u].x + q4.y * kk[u].y + q4.z * kk[u].z + q4.w * kk[u].w;
             t += xchg<1>(t);
             t += xchg<2>(t);
@@ -477,25 +468,13 @@ __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
             l *= cr;
             o4.x *= cr; o4.y *= cr; o4.z *= cr; o4.w *= cr;
 #pragma unroll
-            for (int u = 0; u < NU; ++u) {
+            for (int u = 0; u < AU; ++u) {
                 const float e = expf(sc[u] - mn);
                 l += e;
                 o4.x += e * vv[u].x; o4.y += e * vv[u].y; o4.z += e * vv[u].z; o4.w += e * vv[u].w;
             }
             m = mn;
         }
-    };
-    keys(k0, v0, 0, std::integral_constant<int, AU0>{});
-    for (int jb = AGROUPS * AU0; jb < nk; jb += AGROUPS * AU) {
-        float4 kk[AU], vv[AU];
-#pragma unroll
-        for (int u = 0; u < AU; ++u) {
-            const int jc = min(jb + u * AGROUPS + grp, nk - 1);
-            kk[u] = reinterpret_cast<const float4 *>(K + (int64_t)jc * E)[d4];
-            vv[u] = reinterpret_cast<const float4 *>(Vc + (int64_t)jc * E)[d4];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        keys(kk, vv, jb, std::integral_constant<int, AU>{});
     }
     reinterpret_cast<float4 *>(go[grp])[d4] = o4;
     if (d4 == 0) { gm[grp] = m; gl[grp] = l; }
