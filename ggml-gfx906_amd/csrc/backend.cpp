@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <atomic>
 #include <array>
 #include <map>
 #include <memory>
@@ -170,6 +171,7 @@ struct GraphCache {
     hipGraphExec_t exec = nullptr;
     std::vector<NodeProps> props;
     uint64_t scratch_gen = 0;
+    uint64_t lr_gen = 0;              // fused-layer weight copies' generation at capture (g_lr_gen)
     int updates = 0;
     bool disabled = false;
 };
@@ -1365,6 +1367,9 @@ struct LayerCopies {
 };
 std::mutex g_lr_mu;
 std::vector<LayerCopies> g_lr;
+// bumped whenever copies are freed: a hipGraph captured before must not be replayed (its
+// launches hold the freed copies' addresses), as the scratch generation guards the scratch
+std::atomic<uint64_t> g_lr_gen{0};
 
 void lr_invalidate(int device, const void *p, size_t n) {
     const uintptr_t a0 = reinterpret_cast<uintptr_t>(p), a1 = a0 + n;
@@ -1374,6 +1379,7 @@ void lr_invalidate(int device, const void *p, size_t n) {
         if (L.device == device && ((a0 < L.o1 && L.o0 < a1) || (a0 < L.m1 && L.m0 < a1))) {
             HIP_OK(hipSetDevice(device));
             HIP_OK(hipFree(L.o));   // (hipFree waits for the kernels still reading it)
+            g_lr_gen.fetch_add(1);
             g_lr[i] = g_lr.back();
             g_lr.pop_back();
         } else {
@@ -1745,7 +1751,7 @@ enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
         // generation check below then refuses to replay it
         return run_nodes(c, g, false);
     }
-    const bool same = graph_unchanged(hg, g) && hg.scratch_gen == c->scratch.gen;
+    const bool same = graph_unchanged(hg, g) && hg.scratch_gen == c->scratch.gen && hg.lr_gen == g_lr_gen.load();
     if (same && hg.exec) {
         hg.updates = 0;
         HIP_OK(hipGraphLaunch(hg.exec, c->stream));
@@ -1780,6 +1786,7 @@ enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
     }
     if (!hg.exec) HIP_OK(hipGraphInstantiate(&hg.exec, graph, nullptr, nullptr, 0));
     hg.scratch_gen = c->scratch.gen;
+    hg.lr_gen = g_lr_gen.load();
     HIP_OK(hipGraphDestroy(graph));
     HIP_OK(hipGraphLaunch(hg.exec, c->stream));
     return GGML_STATUS_SUCCESS;
