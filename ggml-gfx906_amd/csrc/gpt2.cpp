@@ -455,6 +455,10 @@ int model_repack(ggml_mi355x_gpt2_model *m) {
             m->rep_mp.push_back(m->rep + l * (ob + mb) + ob);
         }
     }
+    // other contexts of this model may have decode work queued on their own streams that reads
+    // these copies: let it finish before rewriting them (a ctx_init must not run concurrently with
+    // another thread's decode calls on the same model; include/ggml-mi355x-gpt2.h)
+    if (hipDeviceSynchronize() != hipSuccess) return GGML_MI355X_EHIP;
     for (size_t l = 0; l < n_layers; ++l) {
         const Layer &L = m->layers[l];
         if (gpt2_block_repack(m->wtype, m->hp.n_embd, L.proj_w.data, const_cast<uint8_t *>(m->rep_o[l]), L.mproj_w.data,

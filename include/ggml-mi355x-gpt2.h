@@ -71,7 +71,9 @@ GGML_MI355X_API void ggml_mi355x_gpt2_model_free(ggml_mi355x_gpt2_model *model);
  * For Q4_0 / Q8_0 stages on the two-launch layer, ctx_init also (re)makes the model's one shared
  * set of head-/slice-major c_proj and MLP-projection copies from the current weights: weights
  * written through ggml_mi355x_gpt2_model_tensor after a context exists reach decoding once a
- * context is created after the write (every context of the model then reads the new copies). */
+ * context is created after the write (every context of the model then reads the new copies).
+ * ctx_init waits for the device to drain before rewriting them; it must not run concurrently with
+ * decode calls on the same model from another thread. */
 GGML_MI355X_API int ggml_mi355x_gpt2_ctx_init(ggml_mi355x_gpt2_model *model, int32_t n_seq, ggml_mi355x_gpt2_ctx **out);
 
 /* Device buffers of the context:
