@@ -62,6 +62,38 @@ std::vector<std::vector<float>> run(ggml_backend_t be, const Builder &build, con
     return res;
 }
 
+// the same allocated graph computed once per step; a step sets only the tensors it names (a
+// later step that names nothing but x leaves the plugin's captured hipGraph valid: a replay)
+std::vector<std::vector<std::vector<float>>> run_steps(ggml_backend_t be, const Builder &build, const std::vector<Inputs> &steps) {
+    ggml_init_params p = {ggml_tensor_overhead() * 256 + ggml_graph_overhead(), nullptr, true};
+    ggml_context *ctx = ggml_init(p);
+    ggml_cgraph *gf = ggml_new_graph(ctx);
+    std::vector<ggml_tensor *> outs = build(ctx, gf);
+    for (ggml_tensor *t : outs) ggml_build_forward_expand(gf, t);
+    ggml_gallocr_t ga = ggml_gallocr_new(ggml_backend_get_default_buffer_type(be));
+    if (!ggml_gallocr_alloc_graph(ga, gf)) { fprintf(stderr, "graph allocation failed\n"); exit(2); }
+    std::vector<std::vector<std::vector<float>>> res;
+    for (const Inputs &in : steps) {
+        for (const auto &kv : in.bytes) {
+            ggml_tensor *t = ggml_get_tensor(ctx, kv.first.c_str());
+            if (!t) continue;
+            if (ggml_nbytes(t) != kv.second.size()) { fprintf(stderr, "size mismatch %s\n", kv.first.c_str()); exit(2); }
+            ggml_backend_tensor_set(t, kv.second.data(), 0, kv.second.size());
+        }
+        if (ggml_backend_graph_compute(be, gf) != GGML_STATUS_SUCCESS) { fprintf(stderr, "graph_compute failed\n"); exit(2); }
+        std::vector<std::vector<float>> r;
+        for (ggml_tensor *t : outs) {
+            std::vector<float> v(ggml_nelements(t));
+            ggml_backend_tensor_get(t, v.data(), 0, v.size() * sizeof(float));
+            r.push_back(std::move(v));
+        }
+        res.push_back(std::move(r));
+    }
+    ggml_gallocr_free(ga);
+    ggml_free(ctx);
+    return res;
+}
+
 ggml_tensor *input(ggml_context *ctx, const char *name, ggml_type t, int64_t n0, int64_t n1 = 1, int64_t n2 = 1) {
     ggml_tensor *x = ggml_new_tensor_3d(ctx, t, n0, n1, n2);
     ggml_set_name(x, name);
@@ -342,6 +374,82 @@ int main(int argc, char **argv) {
                     return std::vector<ggml_tensor *>{out};
                 }, in);
             }
+        }
+    }
+
+    // a whole GPT-2 decode layer (main-sched.cpp:600-812 at N = 1, n_past = 5 of n_ctx = 16): the
+    // plugin runs it as the engine's two launches (backend.cpp plan_layers). The same allocated
+    // graph is computed four times: new x (capture), new x (a hipGraph replay), new x again, then
+    // new c_proj / MLP-projection weights (for Q4_0 / Q8_0 that frees the plugin's copies of
+    // them: the captured graph must not be replayed). Each step against a fresh ggml-cpu run on the
+    // same inputs, the layer output and both caches (row n_past written by the layer).
+    for (ggml_type t : types) {
+        const int E = 256, H = E / 64, F = 4 * E, n_ctx = 16, n_past = 5;
+        std::vector<Inputs> steps(4);
+        Inputs &in = steps[0];
+        in.bytes["x"] = f32_bytes(E, -2.f, 2.f);
+        in.bytes["g1"] = f32_bytes(E, 0.5f, 1.5f);
+        in.bytes["b1"] = f32_bytes(E, -0.2f, 0.2f);
+        in.bytes["g2"] = f32_bytes(E, 0.5f, 1.5f);
+        in.bytes["b2"] = f32_bytes(E, -0.2f, 0.2f);
+        in.bytes["w_qkv"] = q_bytes(t, E, 3 * E);
+        in.bytes["b_qkv"] = f32_bytes(3 * E, -0.5f, 0.5f);
+        in.bytes["w_o"] = q_bytes(t, E, E);
+        in.bytes["b_o"] = f32_bytes(E, -0.5f, 0.5f);
+        in.bytes["w_fc"] = q_bytes(t, E, F);
+        in.bytes["b_fc"] = f32_bytes(F, -0.5f, 0.5f);
+        in.bytes["w_mp"] = q_bytes(t, F, E);
+        in.bytes["b_mp"] = f32_bytes(E, -0.5f, 0.5f);
+        in.bytes["memk"] = f32_bytes((size_t)n_ctx * E, -1.f, 1.f);
+        in.bytes["memv"] = f32_bytes((size_t)n_ctx * E, -1.f, 1.f);
+        for (int k = 1; k < 4; ++k) steps[k].bytes["x"] = f32_bytes(E, -2.f, 2.f);
+        steps[3].bytes["w_o"] = q_bytes(t, E, E);
+        steps[3].bytes["w_mp"] = q_bytes(t, F, E);
+        const std::string name = std::string("gpt2_layer ") + ggml_type_name(t);
+        fprintf(stderr, "CASE %s\n", name.c_str());
+        const Builder layer = [&](ggml_context *c, ggml_cgraph *gf) {
+            ggml_tensor *x = input(c, "x", GGML_TYPE_F32, E);
+            ggml_tensor *memk = resident(input(c, "memk", GGML_TYPE_F32, n_ctx * E));
+            ggml_tensor *memv = resident(input(c, "memv", GGML_TYPE_F32, n_ctx * E));
+            ggml_tensor *cur = ggml_add(c, ggml_mul(c, ggml_norm(c, x, eps), input(c, "g1", GGML_TYPE_F32, E)), input(c, "b1", GGML_TYPE_F32, E));
+            cur = ggml_add(c, ggml_mul_mat(c, input(c, "w_qkv", t, E, 3 * E), cur), input(c, "b_qkv", GGML_TYPE_F32, 3 * E));
+            ggml_tensor *Qcur = ggml_view_2d(c, cur, E, 1, cur->nb[1], 0);
+            ggml_tensor *Kcur = ggml_view_2d(c, cur, E, 1, cur->nb[1], 1 * sizeof(float) * E);
+            ggml_tensor *Vcur = ggml_view_2d(c, cur, E, 1, cur->nb[1], 2 * sizeof(float) * E);
+            ggml_build_forward_expand(gf, ggml_cpy(c, Kcur, ggml_view_1d(c, memk, E, ggml_element_size(memk) * E * n_past)));
+            ggml_build_forward_expand(gf, ggml_cpy(c, Vcur, ggml_view_1d(c, memv, E, ggml_element_size(memv) * E * n_past)));
+            ggml_tensor *Q = ggml_permute(c, ggml_cont_3d(c, Qcur, 64, H, 1), 0, 2, 1, 3);
+            ggml_tensor *K = ggml_permute(c, ggml_reshape_3d(c, ggml_view_1d(c, memk, (n_past + 1) * E, 0), 64, H, n_past + 1), 0, 2, 1, 3);
+            ggml_tensor *sm = ggml_soft_max(c, ggml_diag_mask_inf(c, ggml_scale(c, ggml_mul_mat(c, K, Q), 0.125f), n_past));
+            ggml_tensor *Vt = ggml_cont_3d(c, ggml_permute(c, ggml_reshape_3d(c, ggml_view_1d(c, memv, (n_past + 1) * E, 0), 64, H, n_past + 1), 1, 2, 0, 3),
+                                           n_past + 1, 64, H);
+            cur = ggml_cont_2d(c, ggml_permute(c, ggml_mul_mat(c, Vt, sm), 0, 2, 1, 3), E, 1);
+            cur = ggml_add(c, ggml_mul_mat(c, input(c, "w_o", t, E, E), cur), input(c, "b_o", GGML_TYPE_F32, E));
+            ggml_tensor *r1 = ggml_add(c, cur, x);
+            cur = ggml_add(c, ggml_mul(c, ggml_norm(c, r1, eps), input(c, "g2", GGML_TYPE_F32, E)), input(c, "b2", GGML_TYPE_F32, E));
+            cur = ggml_gelu(c, ggml_add(c, ggml_mul_mat(c, input(c, "w_fc", t, E, F), cur), input(c, "b_fc", GGML_TYPE_F32, F)));
+            cur = ggml_add(c, ggml_mul_mat(c, input(c, "w_mp", t, F, E), cur), input(c, "b_mp", GGML_TYPE_F32, E));
+            ggml_tensor *r2 = ggml_add(c, cur, r1);
+            return std::vector<ggml_tensor *>{r2, memk, memv};
+        };
+        const auto got = run_steps(gpu, layer, steps);
+        Inputs merged;
+        for (int k = 0; k < 4; ++k) {
+            for (const auto &kv : steps[k].bytes) merged.bytes[kv.first] = kv.second;
+            const auto want = run(cpu, layer, merged);
+            bool ok = true;
+            std::string detail;
+            for (size_t j = 0; j < want.size(); ++j) {
+                bool finite = true;
+                const double e = nmse(got[k][j], want[j], &finite);
+                ok = ok && finite && e <= 5e-4;
+                char buf[64];
+                snprintf(buf, sizeof buf, " out%zu=%.3e%s", j, e, finite ? "" : "(nonfinite)");
+                detail += buf;
+            }
+            fails += !ok;
+            printf("%s %s step %d%s\n", ok ? "OK  " : "FAIL", name.c_str(), k, detail.c_str());
+            fflush(stdout);
         }
     }
 

@@ -22,6 +22,7 @@ pytestmark = pytest.mark.gpu
 
 folds = {}   # copies folded into a fused mat-vec, by case (filled by _run)
 embeds = {}  # fused embedding launches, by case
+layers = {}  # whole GPT-2 layers fused (plan_layers), by case
 
 
 def _run(fusion: bool, **extra):
@@ -34,6 +35,7 @@ def _run(fusion: bool, **extra):
     fused, attn, pairs = {}, {}, {}
     folds.clear()
     embeds.clear()
+    layers.clear()
     case = None
     for line in r.stderr.splitlines():
         if line.startswith("CASE "):
@@ -43,6 +45,9 @@ def _run(fusion: bool, **extra):
             pairs[case] = 0
             folds[case] = 0
             embeds[case] = 0
+            layers[case] = 0
+        if "layer fused" in line and case is not None:
+            layers[case] += 1
         if "fused embedding" in line and case is not None:
             embeds[case] += 1
         if "folded into the mat-vec's epilogue" in line and case is not None:
@@ -87,6 +92,10 @@ def test_fused_chains_match_cpu_and_fuse(attn_kernel):
         elif k.startswith("attention_sm_output"):  # soft_max is an output: scale/mask/soft_max only
             assert v == [3] and attn[k] == 0, (k, v, attn[k])
     assert sum(1 for k in attn if k.startswith("attention ")) == 6
+    # the whole-layer cases: every compute plans the layer as one run (a replayed hipGraph plans
+    # nothing), and every step matched ggml-cpu (fusion_check prints FAIL otherwise)
+    for t in ("q4_0", "q8_0", "q4_K", "q5_K", "q6_K"):
+        assert layers[f"gpt2_layer {t}"] >= 1, (t, layers[f"gpt2_layer {t}"])
 
 
 def test_unfused_graph_matches_cpu():
@@ -94,3 +103,4 @@ def test_unfused_graph_matches_cpu():
     assert all(v == [] for v in fused.values()), fused
     assert not any(attn.values()) and not any(pairs.values()) and not any(folds.values()), (attn, pairs, folds)
     assert not any(embeds.values()), embeds
+    assert not any(layers.values()), layers
