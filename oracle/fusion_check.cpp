@@ -407,12 +407,17 @@ int main(int argc, char **argv) {
         steps[3].bytes["w_mp"] = q_bytes(t, F, E);
         const std::string name = std::string("gpt2_layer ") + ggml_type_name(t);
         fprintf(stderr, "CASE %s\n", name.c_str());
+        // weights stay allocated (as in a weight buffer): later steps compute without re-setting
+        // them, so ggml-alloc must not hand their memory to an intermediate after their last use
+        auto W = [&](ggml_context *c, const char *nm, ggml_type ty, int64_t n0, int64_t n1 = 1) {
+            return resident(input(c, nm, ty, n0, n1));
+        };
         const Builder layer = [&](ggml_context *c, ggml_cgraph *gf) {
             ggml_tensor *x = input(c, "x", GGML_TYPE_F32, E);
             ggml_tensor *memk = resident(input(c, "memk", GGML_TYPE_F32, n_ctx * E));
             ggml_tensor *memv = resident(input(c, "memv", GGML_TYPE_F32, n_ctx * E));
-            ggml_tensor *cur = ggml_add(c, ggml_mul(c, ggml_norm(c, x, eps), input(c, "g1", GGML_TYPE_F32, E)), input(c, "b1", GGML_TYPE_F32, E));
-            cur = ggml_add(c, ggml_mul_mat(c, input(c, "w_qkv", t, E, 3 * E), cur), input(c, "b_qkv", GGML_TYPE_F32, 3 * E));
+            ggml_tensor *cur = ggml_add(c, ggml_mul(c, ggml_norm(c, x, eps), W(c, "g1", GGML_TYPE_F32, E)), W(c, "b1", GGML_TYPE_F32, E));
+            cur = ggml_add(c, ggml_mul_mat(c, W(c, "w_qkv", t, E, 3 * E), cur), W(c, "b_qkv", GGML_TYPE_F32, 3 * E));
             ggml_tensor *Qcur = ggml_view_2d(c, cur, E, 1, cur->nb[1], 0);
             ggml_tensor *Kcur = ggml_view_2d(c, cur, E, 1, cur->nb[1], 1 * sizeof(float) * E);
             ggml_tensor *Vcur = ggml_view_2d(c, cur, E, 1, cur->nb[1], 2 * sizeof(float) * E);
@@ -424,11 +429,11 @@ int main(int argc, char **argv) {
             ggml_tensor *Vt = ggml_cont_3d(c, ggml_permute(c, ggml_reshape_3d(c, ggml_view_1d(c, memv, (n_past + 1) * E, 0), 64, H, n_past + 1), 1, 2, 0, 3),
                                            n_past + 1, 64, H);
             cur = ggml_cont_2d(c, ggml_permute(c, ggml_mul_mat(c, Vt, sm), 0, 2, 1, 3), E, 1);
-            cur = ggml_add(c, ggml_mul_mat(c, input(c, "w_o", t, E, E), cur), input(c, "b_o", GGML_TYPE_F32, E));
+            cur = ggml_add(c, ggml_mul_mat(c, W(c, "w_o", t, E, E), cur), W(c, "b_o", GGML_TYPE_F32, E));
             ggml_tensor *r1 = ggml_add(c, cur, x);
-            cur = ggml_add(c, ggml_mul(c, ggml_norm(c, r1, eps), input(c, "g2", GGML_TYPE_F32, E)), input(c, "b2", GGML_TYPE_F32, E));
-            cur = ggml_gelu(c, ggml_add(c, ggml_mul_mat(c, input(c, "w_fc", t, E, F), cur), input(c, "b_fc", GGML_TYPE_F32, F)));
-            cur = ggml_add(c, ggml_mul_mat(c, input(c, "w_mp", t, F, E), cur), input(c, "b_mp", GGML_TYPE_F32, E));
+            cur = ggml_add(c, ggml_mul(c, ggml_norm(c, r1, eps), W(c, "g2", GGML_TYPE_F32, E)), W(c, "b2", GGML_TYPE_F32, E));
+            cur = ggml_gelu(c, ggml_add(c, ggml_mul_mat(c, W(c, "w_fc", t, E, F), cur), W(c, "b_fc", GGML_TYPE_F32, F)));
+            cur = ggml_add(c, ggml_mul_mat(c, W(c, "w_mp", t, F, E), cur), W(c, "b_mp", GGML_TYPE_F32, E));
             ggml_tensor *r2 = ggml_add(c, cur, r1);
             return std::vector<ggml_tensor *>{r2, memk, memv};
         };
