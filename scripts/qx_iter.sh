@@ -1,7 +1,7 @@
 #!/bin/bash
 # activation-quantizer iteration: graph-fusion and int8 mat-mat parity, then mat-mat timing with
 # 4 super-blocks per quantizer wave (default) against 1 (GGML_MI355X_QX_SBW=1), interleaved
-# (GGML_MI355X_QX_SBW and the 4-per-wave quantizer existed only in the measured build, commit 78929fe~; profiles/r04_quant_x_sbw_ab.txt)
+# (GGML_MI355X_QX_SBW and the 4-per-wave quantizer existed only in an uncommitted measurement build; results in profiles/r04_quant_x_sbw_ab.txt)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
