@@ -293,18 +293,60 @@ void buf_memset(ggml_backend_buffer_t b, struct ggml_tensor *t, uint8_t v, size_
     lr_invalidate(c->device, static_cast<uint8_t *>(t->data) + off, n);
 }
 
+// small host <-> device copies (a decode step's token id and position, and its logits row read
+// back: three per token under the reference scheduler) go through a pinned bounce buffer on a stream of their own: a DMA from
+// pinned memory, instead of the staged copy a pageable source takes. Same contract as the
+// reference's set_tensor (cudaMemcpyAsync on its own stream + synchronize, ggml-cuda.cu:614-620):
+// the bytes are on the device when the call returns; not ordered with the backend streams.
+struct Bounce {
+    std::mutex mu;
+    void *host = nullptr;
+    hipStream_t st = nullptr;
+};
+constexpr size_t BOUNCE_BYTES = 256 * 1024;   // (a GPT-2 logits row is 201 KB)
+Bounce &bounce_of(int device) {
+    static Bounce b[64];
+    return b[device & 63];
+}
+
 void buf_set(ggml_backend_buffer_t b, struct ggml_tensor *t, const void *data, size_t off, size_t n) {
     auto *c = static_cast<BufferCtx *>(b->context);
     HIP_OK(hipSetDevice(c->device));
-    HIP_OK(hipMemcpyAsync(static_cast<uint8_t *>(t->data) + off, data, n, hipMemcpyHostToDevice, nullptr));
-    HIP_OK(hipStreamSynchronize(nullptr));
+    uint8_t *dst = static_cast<uint8_t *>(t->data) + off;
+    if (n <= BOUNCE_BYTES) {
+        Bounce &bb = bounce_of(c->device);
+        std::lock_guard<std::mutex> lk(bb.mu);
+        if (bb.host == nullptr) {
+            HIP_OK(hipHostMalloc(&bb.host, BOUNCE_BYTES, hipHostMallocDefault));
+            HIP_OK(hipStreamCreateWithFlags(&bb.st, hipStreamNonBlocking));
+        }
+        std::memcpy(bb.host, data, n);
+        HIP_OK(hipMemcpyAsync(dst, bb.host, n, hipMemcpyHostToDevice, bb.st));
+        HIP_OK(hipStreamSynchronize(bb.st));
+    } else {
+        HIP_OK(hipMemcpyAsync(dst, data, n, hipMemcpyHostToDevice, nullptr));
+        HIP_OK(hipStreamSynchronize(nullptr));
+    }
     lr_invalidate(c->device, static_cast<uint8_t *>(t->data) + off, n);
 }
 
 void buf_get(ggml_backend_buffer_t b, const struct ggml_tensor *t, void *data, size_t off, size_t n) {
     auto *c = static_cast<BufferCtx *>(b->context);
     HIP_OK(hipSetDevice(c->device));
-    HIP_OK(hipMemcpyAsync(data, static_cast<const uint8_t *>(t->data) + off, n, hipMemcpyDeviceToHost, nullptr));
+    const uint8_t *src = static_cast<const uint8_t *>(t->data) + off;
+    if (n <= BOUNCE_BYTES) {
+        Bounce &bb = bounce_of(c->device);
+        std::lock_guard<std::mutex> lk(bb.mu);
+        if (bb.host == nullptr) {
+            HIP_OK(hipHostMalloc(&bb.host, BOUNCE_BYTES, hipHostMallocDefault));
+            HIP_OK(hipStreamCreateWithFlags(&bb.st, hipStreamNonBlocking));
+        }
+        HIP_OK(hipMemcpyAsync(bb.host, src, n, hipMemcpyDeviceToHost, bb.st));
+        HIP_OK(hipStreamSynchronize(bb.st));
+        std::memcpy(data, bb.host, n);
+        return;
+    }
+    HIP_OK(hipMemcpyAsync(data, src, n, hipMemcpyDeviceToHost, nullptr));
     HIP_OK(hipStreamSynchronize(nullptr));
 }
 
@@ -1520,15 +1562,19 @@ bool match_layer(const struct ggml_cgraph *g, int n, int i, LayerRun &r) {
         NOLAYER("mlp residual");
     // every tensor the layer produces (views included) is read only inside the layer and is not
     // a requested output, except the layer's output
-    std::map<const struct ggml_tensor *, int> uses;
+    // (a sorted source list, not a map: this runs for every layer of every decode graph)
+    thread_local std::vector<const struct ggml_tensor *> srcs;
+    srcs.clear();
     for (int j = i; j <= j26; ++j)
         for (int s = 0; s < GGMLABI_MAX_SRC; ++s)
-            if (g->nodes[j]->src[s]) ++uses[g->nodes[j]->src[s]];
+            if (g->nodes[j]->src[s]) srcs.push_back(g->nodes[j]->src[s]);
+    std::sort(srcs.begin(), srcs.end());
     for (int j = i; j < j26; ++j) {
         const struct ggml_tensor *t = g->nodes[j];
         if (t->flags & GGMLABI_TENSOR_FLAG_OUTPUT) NOLAYER("an intermediate is a requested output");
         const int u = use_count(g, t);
-        if (u < 0 || u != uses[t]) NOLAYER("an intermediate is read outside the layer");
+        const auto rg = std::equal_range(srcs.begin(), srcs.end(), t);
+        if (u < 0 || u != (int)(rg.second - rg.first)) NOLAYER("an intermediate is read outside the layer");
     }
     // (the output may sit on the input's memory: the input is read by the first launch only, the
     // output written by the last)
