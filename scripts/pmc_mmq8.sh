@@ -11,7 +11,7 @@ P5="TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_REQ_sum"
 i=0
 for C in "$P1" "$P2" "$P3" "$P4" "$P5"; do
     i=$((i+1))
-    timeout -s KILL 90 env GGML_MI355X_MMQ=i8 GGML_MI355X_DIAG=${DIAG:-0} rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc8_${TAG}_$i -o run -- python scripts/mmq_bench.py $SH > gpurun_out/pmc8_${TAG}_$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/pmc8_${TAG}_$i.log; exit 1; }
+    timeout -s KILL 90 env GGML_MI355X_MMQ=i8 GGML_MI355X_DIAG=${DIAG:-0} rocprofv3 --pmc $C --kernel-trace --output-format csv -d gpurun_out/pmc8_${TAG}_$i -o run -- python scripts/mmq_bench.py $SH > gpurun_out/pmc8_${TAG}_$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/pmc8_${TAG}_$i.log; exit 1; }
 done
 python scripts/pmc_summary.py gpurun_out/pmc8_${TAG}_[1-5] > gpurun_out/pmc8_${TAG}.txt
 cat gpurun_out/pmc8_${TAG}.txt
