@@ -1462,9 +1462,12 @@ bool layer_copies(BackendCtx *c, int type, int E, const uint8_t *w_o, size_t o_b
     return true;
 }
 
+// a hot-quant 2-D weight with packed rows (the weight copies of gpt2_block_repack take the ggml
+// row pitch), not row-split
 bool quant_2d(const struct ggml_tensor *w, int64_t ne0, int64_t ne1) {
     return is_hot_quant(w->type) && w->ne[0] == ne0 && w->ne[1] == ne1 && w->ne[2] == 1 && w->ne[3] == 1 &&
-           (int64_t)w->nb[0] == type_bytes(w->type) && !(w->buffer && is_split_buft(w->buffer->buft));
+           ne0 % type_blck(w->type) == 0 && (int64_t)w->nb[0] == type_bytes(w->type) &&
+           (int64_t)w->nb[1] == ne0 / type_blck(w->type) * type_bytes(w->type) && !(w->buffer && is_split_buft(w->buffer->buft));
 }
 
 // one layer starting at the NORM node i; the run's nodes are consecutive in the node order (the
