@@ -520,8 +520,8 @@ def job_gbps(bytes_per_step_per_rank: int, steps: int, world: int, t_max: float)
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)   # ~10 ms of timed launches: the start / stop synchronization is <0.5 % of it
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-extra", action="store_true", help="skip the secondary configs")
