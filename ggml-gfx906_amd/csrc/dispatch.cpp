@@ -55,6 +55,7 @@ bool mmq_id_supported(int type, const MmArgs &a);
 hipError_t mmq_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
 bool mmq8_supported(int type, const MmArgs &a);
 hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
+int mmq8_tile_tokens(const MmArgs &a);
 hipError_t mmq8r_launch(int type, const MmArgs &a, const void *rp, int ne02, int n_mat, hipStream_t st, Scratch &scratch);
 bool mmq8_id_supported(int type, const MmArgs &a);
 hipError_t mmq8_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
@@ -223,7 +224,13 @@ int mul_mat_rp(const TensorView &a, const void *rp, const TensorView &b, const T
     const bool f16 = mmq_f16_forced();
     const int n_mat = (int)(a.ne[2] * a.ne[3]);
     const int rmin = repack_min_tokens();
-    const bool use_rp = m.M > 8 && !f16 && (rp != nullptr || (rmin > 0 && m.M >= rmin)) && repack_size(a) != 0;
+    // a caller's repacked copy serves the 64-token tiles; once the in-place tile runs 128-token
+    // tiles it is the faster one (each weight stage then feeds twice the tokens; the repacked tile
+    // is 64 tokens wide): Q8_0 4096 x 4096 x 2048 110 vs 116 us, Q4_K 110 vs 130 us
+    // (profiles/r04_mmq_m_sweep.txt). Both are exact: only the fp32 order of the scale sums differs.
+    const bool wide = mmq8_supported(a.type, m) && mmq8_tile_tokens(m) == 128;
+    const bool use_rp = m.M > 8 && !f16 && ((rp != nullptr && !wide) || (rmin > 0 && m.M >= rmin)) &&
+                        repack_size(a) != 0;
     if (use_rp) e = mmq8r_launch(a.type, m, rp, (int)a.ne[2], n_mat, st, scratch);
     else if (m.M > 8 && !f16 && mmq8_supported(a.type, m)) e = mmq8_launch(a.type, m, st, scratch);
     else if (m.M > 8 && f16 && mmq_supported(a.type, m)) e = mmq_launch(a.type, m, st, scratch);

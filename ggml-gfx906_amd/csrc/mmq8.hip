@@ -1338,15 +1338,19 @@ static void launch8(const MmArgs &a, uint8_t *ximg, int tr_rows, int tt_tok, int
     }
 }
 
+// rows x tokens per workgroup of the in-place tile: 128-token tiles once they alone give every
+// CU a workgroup (the weight stage then serves twice the tokens)
+// (128-token tiles on half the chip with 2-way split-K measured slower at 4096 x 4096 x 512:
+// 44.9-45.1 vs 41.3 us, profiles/r03_mmq8_split2_atomic.txt)
+int mmq8_tile_tokens(const MmArgs &a) {
+    return (int64_t)((a.N + 127) / 128) * ((a.M + 127) / 128) * a.ne12 * a.ne13 >= 256 ? 128 : 64;
+}
+
 hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch) {
     const int slices = a.ne12 * a.ne13;
     const int n_sb = (a.K + Q8_QK - 1) / Q8_QK;
-    // rows x tokens per workgroup: 128-token tiles once they alone give every CU a workgroup
-    // (the weight stage then serves twice the tokens); GGML_MI355X_MMQ8_TT / _TR override
-    // (measurements; 128 tokens always run 128 rows)
-    // (128-token tiles on half the chip with 2-way split-K measured slower at 4096 x 4096 x 512:
-    // 44.9-45.1 vs 41.3 us, profiles/r03_mmq8_split2_atomic.txt)
-    int tt_tok = (int64_t)((a.N + 127) / 128) * ((a.M + 127) / 128) * slices >= 256 ? 128 : 64;
+    // GGML_MI355X_MMQ8_TT / _TR override (measurements; 128 tokens always run 128 rows)
+    int tt_tok = mmq8_tile_tokens(a);
     if (const char *e = getenv("GGML_MI355X_MMQ8_TT")) tt_tok = atoi(e) == 128 ? 128 : 64;
     int tr_rows = 128;
     if (const char *e = getenv("GGML_MI355X_MMQ8_TR")) tr_rows = (atoi(e) == 64 && tt_tok == 64) ? 64 : 128;

@@ -97,6 +97,16 @@ def test_repacked_equals_per_call_repack(mm, t):
     np.testing.assert_array_equal(once.view(np.uint32), per_call.view(np.uint32))
 
 
+@pytest.mark.parametrize("t", [qref.Q4_0, qref.Q4_K], ids=lambda t: qref.NAMES[t])
+def test_repacked_wide_calls_use_src0(mm, t):
+    """once the in-place tile runs 128-token tiles (>= 256 of them) it reads src0 itself, the
+    repacked copy being slower there (profiles/r04_mmq_m_sweep.txt): bit-identical to mul_mat"""
+    from test_gpu_parity import run_mul_mat
+    a, b, out_ne = operands(t, 4096, 1032, 256, seed=13)
+    np.testing.assert_array_equal(run_repacked(mm, a, b, out_ne).view(np.uint32),
+                                  run_mul_mat(mm, a, b, out_ne).view(np.uint32))
+
+
 def test_repacked_decode_shapes_use_src0(mm):
     """ne11 <= 8 runs the mat-vec on src0 itself; the repacked copy is not read"""
     t = qref.Q4_K
