@@ -56,6 +56,7 @@ hipError_t mmq_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scr
 bool mmq8_supported(int type, const MmArgs &a);
 hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
 int mmq8_tile_tokens(const MmArgs &a);
+int64_t mmq8_tiles128(const MmArgs &a);
 hipError_t mmq8r_launch(int type, const MmArgs &a, const void *rp, int ne02, int n_mat, hipStream_t st, Scratch &scratch);
 bool mmq8_id_supported(int type, const MmArgs &a);
 hipError_t mmq8_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
@@ -224,16 +225,17 @@ int mul_mat_rp(const TensorView &a, const void *rp, const TensorView &b, const T
     const bool f16 = mmq_f16_forced();
     const int n_mat = (int)(a.ne[2] * a.ne[3]);
     const int rmin = repack_min_tokens();
-    // a caller's repacked copy (a 64-token tile) is read up to 1023 tokens; from 1024 on, with the
-    // in-place tile at 128-token tiles (each weight stage feeding twice the tokens), src0 is read
-    // in place: 4096 x 4096 x 2048 Q8_0 110 vs 116 us, Q4_K 109 vs 130, Q6_K 152 vs 164; x 1024
-    // Q8_0 59 vs 64, Q6_K 83 vs 92. At 512 tokens the copy is the faster one even where the
-    // in-place tile already runs 128-token tiles (N = 11008: Q8_0 85 vs 95 us, Q6_K 124 vs 140;
-    // Q4_K the exception, 99 vs 95) (profiles/r04_mmq_m_sweep.txt, r04_rp_shape_sweep.txt). Both
+    // a caller's repacked copy (a 64-token tile) against the in-place tile: the copy wins while the
+    // in-place tile runs 64-token tiles (Q8_0 4096 x 4096 x 512 36 vs 41.5 us) and at 512 tokens
+    // over >= 256 128-token tiles (N = 11008: Q8_0 85 vs 95 us, Q6_K 124 vs 140; Q4_K 99 vs 95);
+    // the in-place 128-token tile wins below 256 such tiles (4096 x 4096 x 768 Q8_0 54 vs 59, Q4_K
+    // 55 vs 67) and from 1024 tokens on (x 2048 Q8_0 110 vs 116, Q4_K 109 vs 130, Q6_K 152 vs
+    // 164) (profiles/r04_mmq_m_sweep.txt, r04_rp_shape_sweep.txt, r04_mmq8_tt_sweep2.txt). Both
     // are exact: only the fp32 order of the scale sums differs.
     // GGML_MI355X_MMQ_RP_ALL=1: always read the copy (measurements)
     static const bool rp_all = getenv("GGML_MI355X_MMQ_RP_ALL") && atoi(getenv("GGML_MI355X_MMQ_RP_ALL")) == 1;
-    const bool wide = !rp_all && m.M >= 1024 && mmq8_supported(a.type, m) && mmq8_tile_tokens(m) == 128;
+    const bool wide = !rp_all && mmq8_supported(a.type, m) && mmq8_tile_tokens(m) == 128 &&
+                      (m.M >= 1024 || mmq8_tiles128(m) < 256);
     const bool use_rp = m.M > 8 && !f16 && ((rp != nullptr && !wide) || (rmin > 0 && m.M >= rmin)) &&
                         repack_size(a) != 0;
     if (use_rp) e = mmq8r_launch(a.type, m, rp, (int)a.ne[2], n_mat, st, scratch);

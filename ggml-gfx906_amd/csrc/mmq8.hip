@@ -1338,13 +1338,15 @@ static void launch8(const MmArgs &a, uint8_t *ximg, int tr_rows, int tt_tok, int
     }
 }
 
-// rows x tokens per workgroup of the in-place tile: 128-token tiles once they alone give every
-// CU a workgroup (the weight stage then serves twice the tokens)
-// (128-token tiles on half the chip with 2-way split-K measured slower at 4096 x 4096 x 512:
-// 44.9-45.1 vs 41.3 us, profiles/r03_mmq8_split2_atomic.txt)
-int mmq8_tile_tokens(const MmArgs &a) {
-    return (int64_t)((a.N + 127) / 128) * ((a.M + 127) / 128) * a.ne12 * a.ne13 >= 256 ? 128 : 64;
+// rows x tokens per workgroup of the in-place tile: 128-token tiles (the weight stage then serves
+// twice the tokens) once more than 128 of them fill the chip without split-K: 4096 x 4096 x 576
+// (160 tiles) 53 vs 67 us, x 768 54 vs 71, 4096 x 6144 x 512 54 vs 70, Q6_K 4096 x 4096 x 768
+// 79 vs 101 (profiles/r04_mmq8_tt_sweep2.txt). At 128 tiles (4096 x 4096 x 512) the 128-token
+// tile needs 2-way split-K and is slower: 44.9-45.1 vs 41.3 us (profiles/r03_mmq8_split2_atomic.txt)
+int64_t mmq8_tiles128(const MmArgs &a) {
+    return (int64_t)((a.N + 127) / 128) * ((a.M + 127) / 128) * a.ne12 * a.ne13;
 }
+int mmq8_tile_tokens(const MmArgs &a) { return mmq8_tiles128(a) > 128 ? 128 : 64; }
 
 hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch) {
     const int slices = a.ne12 * a.ne13;

@@ -131,9 +131,9 @@ GGML_MI355X_API int ggml_mi355x_quantize(const ggml_mi355x_tensor *src, ggml_mi3
  * MUL_MAT with many tokens streams them with no per-call decode. ggml_mi355x_repack_size gives the
  * bytes for src0 (every matrix of a 3-d / 4-d tensor), ggml_mi355x_repack writes them to `dst`
  * (device memory) on `stream`; ggml_mi355x_mul_mat_repacked is ggml_mi355x_mul_mat with that copy
- * beside src0 (src0 itself still serves the mat-vec shapes, ne11 <= 8, and the wide ones,
- * ne11 >= 1024 where the in-place tile runs 128-token tiles). The copy must be remade when
- * src0's bytes change. */
+ * beside src0 (src0 itself still serves the mat-vec shapes, ne11 <= 8, and the shapes where
+ * the in-place tile's 128-token tiles are faster than the copy's 64-token ones). The copy must
+ * be remade when src0's bytes change. */
 GGML_MI355X_API int ggml_mi355x_repack_size(const ggml_mi355x_tensor *src0, size_t *bytes);
 GGML_MI355X_API int ggml_mi355x_repack(const ggml_mi355x_tensor *src0, void *dst, size_t bytes, void *stream);
 GGML_MI355X_API int ggml_mi355x_mul_mat_repacked(const ggml_mi355x_tensor *src0, const void *repacked,
