@@ -32,6 +32,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -114,6 +115,10 @@ struct DeviceCtx {
 struct BufferCtx {
     int device;
     void *base;
+    // repacked-weight buffers: tensors written in part since their last repack (their copy is
+    // stale until a write reaches the tensor's end; MUL_MAT reads src0 in place meanwhile)
+    std::mutex rp_mu;
+    std::set<const struct ggml_tensor *> rp_partial;
 };
 
 // per-shard state of one backend for split (row-sharded) mat-muls
@@ -195,6 +200,7 @@ struct BackendCtx {
     int32_t *lf_pos = nullptr;
     void *lf_mem = nullptr;
     hipStream_t aux = nullptr;        // weight copies made for fused layers (not captured)
+    hipEvent_t aux_ready = nullptr;   // recorded on `stream` before aux starts a copy
 };
 
 const char *BUFT_TAG = "MI355X";
@@ -401,11 +407,32 @@ uint8_t *rp_extra_ptr(const struct ggml_tensor *t) {
     return reinterpret_cast<uint8_t *>((end + 255) & ~(uintptr_t)255);
 }
 
-void rp_refresh(BufferCtx *c, struct ggml_tensor *t) {
+std::atomic<uint64_t> g_lr_gen{0};   // (below: fused-layer copies; also bumped when a repacked copy goes stale / fresh)
+
+// after a write of [off, off + n) into t: remake t's repacked copy on `st` once the write reaches
+// the tensor's end (a whole-tensor write, or the last chunk of an upload in order, as the
+// reference's CPU repack buffer takes only whole-tensor writes, repack.cpp:1879-1889); until then
+// the copy is marked stale and MUL_MAT reads the ggml bytes in place (repacked_of). A change of
+// staleness bumps g_lr_gen, so a hipGraph captured with the other choice is not replayed.
+void rp_written(BufferCtx *c, struct ggml_tensor *t, size_t off, size_t n, hipStream_t st) {
     if (t->extra == nullptr) return;
-    const size_t n = rp_extra_bytes(t) - 256;
+    const size_t nbytes = ggml_base().nbytes(t);
+    const bool complete = off + n >= nbytes;
+    {
+        std::lock_guard<std::mutex> lk(c->rp_mu);
+        const bool was = c->rp_partial.count(t) != 0;
+        if (complete) c->rp_partial.erase(t);
+        else c->rp_partial.insert(t);
+        if (was != !complete) g_lr_gen.fetch_add(1);
+    }
+    if (!complete) return;
     HIP_OK(hipSetDevice(c->device));
-    if (repack(tv(t), t->extra, n, nullptr) != GGML_MI355X_OK) fatal("repack", hipErrorInvalidValue);
+    if (repack(tv(t), t->extra, rp_extra_bytes(t) - 256, st) != GGML_MI355X_OK) fatal("repack", hipErrorInvalidValue);
+}
+
+void rp_refresh(BufferCtx *c, struct ggml_tensor *t, size_t off, size_t n) {
+    if (t->extra == nullptr) return;
+    rp_written(c, t, off, n, nullptr);
     HIP_OK(hipStreamSynchronize(nullptr));
 }
 
@@ -416,17 +443,17 @@ enum ggml_status rp_init_tensor(ggml_backend_buffer_t, struct ggml_tensor *t) {
 
 void rp_memset(ggml_backend_buffer_t b, struct ggml_tensor *t, uint8_t v, size_t off, size_t n) {
     buf_memset(b, t, v, off, n);
-    rp_refresh(static_cast<BufferCtx *>(b->context), t);
+    rp_refresh(static_cast<BufferCtx *>(b->context), t, off, n);
 }
 
 void rp_set(ggml_backend_buffer_t b, struct ggml_tensor *t, const void *data, size_t off, size_t n) {
     buf_set(b, t, data, off, n);
-    rp_refresh(static_cast<BufferCtx *>(b->context), t);
+    rp_refresh(static_cast<BufferCtx *>(b->context), t, off, n);
 }
 
 bool rp_cpy(ggml_backend_buffer_t b, const struct ggml_tensor *src, struct ggml_tensor *dst) {
     if (!buf_cpy(b, src, dst)) return false;
-    rp_refresh(static_cast<BufferCtx *>(b->context), dst);
+    rp_refresh(static_cast<BufferCtx *>(b->context), dst, 0, ggml_base().nbytes(dst));
     return true;
 }
 
@@ -481,8 +508,12 @@ bool is_rp_buft(ggml_backend_buffer_type_t buft) { return buft && buft->iface.ge
 bool is_our_buft(ggml_backend_buffer_type_t buft) { return buft && (buft->iface.get_name == buft_name || is_rp_buft(buft)); }
 
 // src0's repacked copy, when it lives in a repacked-weight buffer (else nullptr)
+// (nullptr too while the copy is stale: the tensor was written in part since its last repack)
 const void *repacked_of(const struct ggml_tensor *a) {
-    return a->buffer && is_rp_buft(a->buffer->buft) && a->view_src == nullptr ? a->extra : nullptr;
+    if (!a->buffer || !is_rp_buft(a->buffer->buft) || a->view_src != nullptr || a->extra == nullptr) return nullptr;
+    auto *c = static_cast<BufferCtx *>(a->buffer->context);
+    std::lock_guard<std::mutex> lk(c->rp_mu);
+    return c->rp_partial.count(a) ? nullptr : a->extra;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -757,6 +788,7 @@ void be_free(ggml_backend_t b) {
     if (c->hg.exec) HIP_OK(hipGraphExecDestroy(c->hg.exec));
     HIP_OK(hipStreamDestroy(c->stream));
     HIP_OK(hipStreamDestroy(c->aux));
+    HIP_OK(hipEventDestroy(c->aux_ready));
     if (c->lf_mem) HIP_OK(hipFree(c->lf_mem));
     if (c->src1_ready) HIP_OK(hipEventDestroy(c->src1_ready));
     if (c->copy_done) HIP_OK(hipEventDestroy(c->copy_done));
@@ -774,10 +806,21 @@ void be_free(ggml_backend_t b) {
     delete b;
 }
 
+// an asynchronous write into one of our buffers, queued on `st`: the same bookkeeping as the
+// buffer's synchronous writes (buf_set / rp_set) — the fused-layer weight copies of the range
+// are dropped, and a repacked-weight tensor's copy is remade on `st` behind the write
+void written_async(struct ggml_tensor *t, size_t off, size_t n, hipStream_t st) {
+    if (!t->buffer || !is_our_buft(t->buffer->buft)) return;
+    auto *bc = static_cast<BufferCtx *>(t->buffer->context);
+    if (is_rp_buft(t->buffer->buft)) rp_written(bc, t, off, n, st);
+}
+
 void be_set_async(ggml_backend_t b, struct ggml_tensor *t, const void *data, size_t off, size_t n) {
     BackendCtx *c = be_ctx(b);
     HIP_OK(hipSetDevice(c->device));
+    lr_invalidate(c->device, static_cast<uint8_t *>(t->data) + off, n);
     HIP_OK(hipMemcpyAsync(static_cast<uint8_t *>(t->data) + off, data, n, hipMemcpyHostToDevice, c->stream));
+    written_async(t, off, n, c->stream);
 }
 
 void be_get_async(ggml_backend_t b, const struct ggml_tensor *t, void *data, size_t off, size_t n) {
@@ -794,6 +837,7 @@ bool be_cpy_async(ggml_backend_t bsrc, ggml_backend_t bdst, const struct ggml_te
     if (!src->buffer || !dst->buffer || !is_our_buft(src->buffer->buft) || !is_our_buft(dst->buffer->buft)) return false;
     BackendCtx *cs = be_ctx(bsrc), *cd = be_ctx(bdst);
     const size_t n = ggml_base().nbytes(src);
+    lr_invalidate(cd->device, dst->data, n);
     HIP_OK(hipSetDevice(cs->device));
     if (cs->device == cd->device) {
         HIP_OK(hipMemcpyAsync(dst->data, src->data, n, hipMemcpyDeviceToDevice, cs->stream));
@@ -806,6 +850,7 @@ bool be_cpy_async(ggml_backend_t bsrc, ggml_backend_t bdst, const struct ggml_te
         HIP_OK(hipSetDevice(cd->device));
         HIP_OK(hipStreamWaitEvent(cd->stream, cs->copy_done, 0));
     }
+    written_async(dst, 0, n, cd->stream);   // (a repacked destination is remade on its own device)
     return true;
 }
 
@@ -813,7 +858,7 @@ void be_sync(ggml_backend_t b) {
     BackendCtx *c = be_ctx(b);
     HIP_OK(hipSetDevice(c->device));
     HIP_OK(hipStreamSynchronize(c->stream));
-    if (take_device_error()) {   // as the reference's GGML_ASSERT in get_rows (src/ggml-cpu/ops.cpp:5157)
+    if (take_device_error(c->device)) {   // as the reference's GGML_ASSERT in get_rows (src/ggml-cpu/ops.cpp:5157)
         fprintf(stderr, "[ggml-mi355x] %s: GET_ROWS row index out of range\n", c->name.c_str());
         abort();
     }
@@ -1409,9 +1454,9 @@ struct LayerCopies {
 };
 std::mutex g_lr_mu;
 std::vector<LayerCopies> g_lr;
-// bumped whenever copies are freed: a hipGraph captured before must not be replayed (its
-// launches hold the freed copies' addresses), as the scratch generation guards the scratch
-std::atomic<uint64_t> g_lr_gen{0};
+// g_lr_gen (declared with the repacked buffer above) is bumped whenever copies are freed: a
+// hipGraph captured before must not be replayed (its launches hold the freed copies' addresses),
+// as the scratch generation guards the scratch
 
 void lr_invalidate(int device, const void *p, size_t n) {
     const uintptr_t a0 = reinterpret_cast<uintptr_t>(p), a1 = a0 + n;
@@ -1451,8 +1496,11 @@ bool layer_copies(BackendCtx *c, int type, int E, const uint8_t *w_o, size_t o_b
     LayerCopies L{c->device, o0, o0 + o_bytes, m0, m0 + mp_bytes, nullptr, nullptr};
     HIP_OK(hipMalloc(&L.o, ob + mb));
     L.mp = L.o + ob;
-    // the weights were written by synchronous set_tensor calls; earlier graph work on the
-    // backend stream may still read other buffers, not these new copies
+    // the copies are made on the side stream behind everything queued on the backend stream so
+    // far (an asynchronous write of the weights, ggml_backend_tensor_set_async, may still be in
+    // flight there)
+    HIP_OK(hipEventRecord(c->aux_ready, c->stream));
+    HIP_OK(hipStreamWaitEvent(c->aux, c->aux_ready, 0));
     HIP_OK(gpt2_block_repack(type, E, w_o, L.o, w_mp, L.mp, nullptr, nullptr, c->aux));
     HIP_OK(hipStreamSynchronize(c->aux));
     std::lock_guard<std::mutex> lk(g_lr_mu);
@@ -1893,6 +1941,8 @@ ggml_backend_t dv_init_backend(ggml_backend_dev_t d, const char *) {
     HIP_OK(hipSetDevice(c->device));
     HIP_OK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&c->aux_ready, hipEventDisableTiming));
+    (void)device_error_word();   // this device's GET_ROWS error word, made outside any capture
     {   // fused GPT-2 layers (plan_layers): n_embd <= 1024, <= 16 heads, <= 32 MLP slices, one sequence
         constexpr size_t E = 1024;
         HIP_OK(hipMalloc(&c->lf_mem, (16 + 32 + 2) * E * sizeof(float) + 256));

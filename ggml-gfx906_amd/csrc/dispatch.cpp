@@ -27,6 +27,7 @@ size_t mmvq_lds_bytes(int K, int nc);
 bool mmvq_has_nc(int nc);
 int mmvq_max_k_for_nc(int nc);
 bool mmvq_bigk(int K);
+hipError_t mmvq_ring_launch(int type, const MmArgs &a, int nc, int rpw, hipStream_t st);
 hipError_t dequant_launch(int type, const void *src, float *dst, int64_t n, hipStream_t st);
 hipError_t mmq_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
 struct RowsArgs {
@@ -54,6 +55,7 @@ bool mmq_supported(int type, const MmArgs &a);
 bool mmq_id_supported(int type, const MmArgs &a);
 hipError_t mmq_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
 bool mmq8_supported(int type, const MmArgs &a);
+bool mmq8_images_fit(int type, const MmArgs &a);
 hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
 int mmq8_tile_tokens(const MmArgs &a);
 int64_t mmq8_tiles128(const MmArgs &a);
@@ -137,8 +139,7 @@ int check_mul_mat(const TensorView &a, const TensorView &b, const TensorView &d)
     if (d.ne[0] != a.ne[1] || d.ne[1] != b.ne[1] || d.ne[2] != b.ne[2] || d.ne[3] != b.ne[3]) return GGML_MI355X_EINVAL;
     if ((int64_t)a.nb[0] != type_bytes(a.type) || b.nb[0] != 4 || d.nb[0] != 4) return GGML_MI355X_EINVAL;
     if (a.ne[0] > (1 << 24) || a.ne[1] > (1LL << 31) - 1 || b.ne[1] > (1LL << 31) - 1) return GGML_MI355X_EINVAL;
-    if (mmvq_lds_bytes((int)a.ne[0], 1) > LDS_LIMIT) return GGML_MI355X_EINVAL;
-    return GGML_MI355X_OK;
+    return GGML_MI355X_OK;   // (any K: past the whole-K kernel's LDS the chunked one runs, use_ring)
 }
 
 static MmArgs base_args(const TensorView &a, const TensorView &b, const TensorView &d) {
@@ -163,18 +164,42 @@ static MmArgs base_args(const TensorView &a, const TensorView &b, const TensorVi
     return m;
 }
 
+// the chunked-K mat-vec (mmvq_ring.hip) takes a column group when K > 4096 and either several
+// columns share the pass (one pass over the weights for up to 8 columns at any K, where the
+// whole-K kernel would split them into passes of 1..3 columns) or the group's whole-K image would
+// not fit LDS. GGML_MI355X_RING: 0 = never (the whole-K kernel's column splits, measurements),
+// 2 = also single columns at K > 4096.
+static int ring_policy() {
+    static const int v = getenv("GGML_MI355X_RING") ? atoi(getenv("GGML_MI355X_RING")) : 1;
+    return v;
+}
+
+static bool use_ring(int K, int ncols) {
+    if (K <= 4096 || ring_policy() == 0) return mmvq_lds_bytes(K, 1) > LDS_LIMIT;
+    return ncols >= 2 || ring_policy() == 2 || mmvq_bigk(K);
+}
+
 // mat-vec over columns [c0, c0 + ncols) in groups of at most 8
 static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st) {
     const int rpw = pick_rpw(type, (int64_t)m.N * m.ne12 * m.ne13);
     while (ncols > 0) {
-        int nc = mmvq_bigk(m.K) ? 1 : std::min(ncols, 8);
-        while (nc > 1 && (!mmvq_has_nc(nc) || mmvq_lds_bytes(m.K, nc) > LDS_LIMIT || m.K > mmvq_max_k_for_nc(nc))) --nc;
         MmArgs g = m;
         g.x = m.x + (int64_t)c0 * m.nb11;
         g.dst = m.dst + (int64_t)c0 * m.nb1;
-        g.M = nc;
-        g.x_aligned16 = m.x_aligned16;
-        const hipError_t e = mmvq_launch(type, g, nc, rpw, st);
+        int nc;
+        hipError_t e;
+        if (use_ring(m.K, ncols)) {
+            const int take = std::min(ncols, 8);   // one launch: the last column group may be partial
+            nc = take <= 1 ? 1 : take <= 2 ? 2 : take <= 4 ? 4 : 8;
+            g.M = take;
+            e = mmvq_ring_launch(type, g, nc, rpw, st);
+            nc = take;
+        } else {
+            nc = mmvq_bigk(m.K) ? 1 : std::min(ncols, 8);
+            while (nc > 1 && (!mmvq_has_nc(nc) || mmvq_lds_bytes(m.K, nc) > LDS_LIMIT || m.K > mmvq_max_k_for_nc(nc))) --nc;
+            g.M = nc;
+            e = mmvq_launch(type, g, nc, rpw, st);
+        }
         if (e != hipSuccess) return e;
         c0 += nc;
         ncols -= nc;
@@ -237,7 +262,7 @@ int mul_mat_rp(const TensorView &a, const void *rp, const TensorView &b, const T
     const bool wide = !rp_all && mmq8_supported(a.type, m) && mmq8_tile_tokens(m) == 128 &&
                       (m.M >= 1024 || mmq8_tiles128(m) < 256);
     const bool use_rp = m.M > 8 && !f16 && ((rp != nullptr && !wide) || (rmin > 0 && m.M >= rmin)) &&
-                        repack_size(a) != 0;
+                        repack_size(a) != 0 && mmq8_images_fit(a.type, m);
     if (use_rp) e = mmq8r_launch(a.type, m, rp, (int)a.ne[2], n_mat, st, scratch);
     else if (m.M > 8 && !f16 && mmq8_supported(a.type, m)) e = mmq8_launch(a.type, m, st, scratch);
     else if (m.M > 8 && f16 && mmq_supported(a.type, m)) e = mmq_launch(a.type, m, st, scratch);
@@ -302,32 +327,50 @@ int mul_mat_id(const TensorView &as, const TensorView &b, const TensorView &ids,
 // precondition they can only see on the device (a GET_ROWS index out of range; the reference
 // GGML_ASSERTs, src/ggml-cpu/ops.cpp:5157). Read after the stream has synchronized.
 // ------------------------------------------------------------------------------------------
-static int *g_err_host = nullptr, *g_err_dev = nullptr;
-static std::once_flag g_err_once;
+// One word per device, made on first use (the backend makes its device's at init, outside any
+// stream capture). A failed allocation is not remembered: the next call tries again.
+// hipHostMallocPortable: the word is valid whichever device is current when it is read.
+static constexpr int ERR_DEVS = 64;
+static int *g_err_host[ERR_DEVS], *g_err_dev[ERR_DEVS];
+static std::mutex g_err_mu;
 
 int *device_error_word() {
-    std::call_once(g_err_once, [] {
-        void *h = nullptr;
-        if (hipHostMalloc(&h, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
-            (void)hipGetLastError();
-            return;
-        }
-        void *d = nullptr;
-        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
-            (void)hipGetLastError();
-            (void)hipHostFree(h);
-            return;
-        }
-        g_err_host = static_cast<int *>(h);
-        *g_err_host = 0;
-        g_err_dev = static_cast<int *>(d);
-    });
-    return g_err_dev;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= ERR_DEVS) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    if (g_err_dev[dev]) return g_err_dev[dev];
+    void *h = nullptr;
+    if (hipHostMalloc(&h, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipHostFree(h);
+        return nullptr;
+    }
+    *static_cast<int *>(h) = 0;
+    g_err_host[dev] = static_cast<int *>(h);
+    g_err_dev[dev] = static_cast<int *>(d);
+    return g_err_dev[dev];
 }
 
-int take_device_error() {
-    if (!g_err_host) return 0;
-    const int v = __atomic_exchange_n(g_err_host, 0, __ATOMIC_ACQ_REL);
+// device < 0: every device's word
+int take_device_error(int device) {
+    int v = 0;
+    for (int i = 0; i < ERR_DEVS; ++i) {
+        if (device >= 0 && i != device) continue;
+        int *h;
+        {
+            std::lock_guard<std::mutex> lk(g_err_mu);
+            h = g_err_host[i];
+        }
+        if (h) v |= __atomic_exchange_n(h, 0, __ATOMIC_ACQ_REL);
+    }
     return v;
 }
 
@@ -586,7 +629,7 @@ int ggml_mi355x_get_rows(const ggml_mi355x_tensor *src0, const ggml_mi355x_tenso
     return get_rows(view_of(src0), view_of(rows), view_of(dst), static_cast<hipStream_t>(stream));
 }
 
-int ggml_mi355x_device_error(void) { return take_device_error(); }
+int ggml_mi355x_device_error(void) { return take_device_error(-1); }
 
 int ggml_mi355x_cpy(const ggml_mi355x_tensor *src, ggml_mi355x_tensor *dst, void *stream) {
     if (!src || !dst) return GGML_MI355X_EINVAL;
@@ -601,7 +644,7 @@ int ggml_mi355x_quantize(const ggml_mi355x_tensor *src, ggml_mi355x_tensor *dst,
 int ggml_mi355x_supports_mul_mat(const ggml_mi355x_tensor *src0, const ggml_mi355x_tensor *src1) {
     if (!src0 || !src1) return 0;
     return is_hot_quant(src0->type) && src1->type == T_F32 && src0->ne[0] % type_blck(src0->type) == 0 &&
-           mmvq_lds_bytes((int)src0->ne[0], 1) <= LDS_LIMIT;
+           src0->ne[0] <= (1 << 24);
 }
 
 int ggml_mi355x_device_count(void) {

@@ -84,7 +84,7 @@ int get_rows_add(const TensorView &a, const TensorView &ra, const TensorView &b,
 // device error word (host-mapped): raised by kernels on a failed device-side precondition;
 // take_device_error() returns and clears it (call after the stream synchronized)
 int *device_error_word();
-int take_device_error();
+int take_device_error(int device);   // device < 0: all devices
 int check_quantize(const TensorView &src, const TensorView &d);
 // GGML_OP_CPY between this path's types: f32 -> Q4_0 / Q8_0, hot -> f32, hot -> same hot
 int check_cpy(const TensorView &src, const TensorView &d);

@@ -1294,6 +1294,7 @@ static int ximg_bytes_rt(int type) {
 // Q8_0 / Q6_K (windows realigned per lane from the block's own offset, the buffer based at the
 // matrix's dword floor). Q4_K / Q5_K rows are 144 / 176 B, so their super-blocks are 16-B aligned
 // whenever the tensor is; a K-quant view at a finer offset takes the mat-vec.
+bool mmq8_images_fit(int type, const MmArgs &a);
 bool mmq8_supported(int type, const MmArgs &a) {
     if (!(type == T_Q4_0 || type == T_Q8_0 || type == T_Q4_K || type == T_Q5_K || type == T_Q6_K)) return false;
     if (a.K <= 0 || a.K % type_blck(type) != 0 || a.M <= 0) return false;
@@ -1306,9 +1307,16 @@ bool mmq8_supported(int type, const MmArgs &a) {
     const int64_t n_sb = (a.K + Q8_QK - 1) / Q8_QK;
     // the last super-block's windows reach past a short row by up to one super-block
     const int64_t w_span = (int64_t)a.N * a.nb01 + n_sb * Q8_QK / type_blck(type) * type_bytes(type) + 8;
-    const int64_t n_tt = (a.M + Q8_TOK - 1) / Q8_TOK;
-    const int64_t img_slice = n_tt * n_sb * ximg_bytes_rt(type);
-    return a.nb01 >= row_b && w_span < (1LL << 32) && img_slice < (1LL << 31);
+    return a.nb01 >= row_b && w_span < (1LL << 32) && mmq8_images_fit(type, a);
+}
+
+// one slice's activation images stay below 2 GiB (32-bit buffer offsets), counted for the
+// 128-token tile, which allocates two 64-token images per tile (ceil(M / 128) * 2 >= ceil(M / 64));
+// the repacked tile's images are the same
+bool mmq8_images_fit(int type, const MmArgs &a) {
+    const int64_t n_sb = (a.K + Q8_QK - 1) / Q8_QK;
+    const int64_t n_img = (a.M + 127) / 128 * 2;
+    return n_img * n_sb * ximg_bytes_rt(type) < (1LL << 31);
 }
 
 template <int T>

@@ -381,6 +381,23 @@ int main(int argc, char **argv) {
     }
     gen_mul_mat_id(GGML_TYPE_Q4_0, 8, 1, false, 128, 129, 256);
 
+    // round 5: the chunked-K mat-vec (mmvq_ring.hip) — K past one 4096 chunk at 1..8 columns,
+    // the reference's perf shapes' K (test-backend-ops.cpp:6195-6201, K = 14336) and LLaMA's
+    // FFN-down K = 11008; ragged K (K % 64 == 32), a partial last chunk, broadcast batches, one
+    // full-size 4096 x 14336 x 8 and K = 131072 (past the whole-K kernel's LDS)
+    for (ggml_type t : HOT)
+        for (int64_t k : {11008, 14336})
+            for (int n : {1, 2, 5, 8}) gen_mul_mat(t, 256, n, k, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q4_0, 200, 3, 14368, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q8_0, 200, 7, 14368, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q4_K, 333, 7, 12288, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q6_K, 96, 4, 9216, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q8_0, 64, 4, 8192, 2, 1, 2, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q5_K, 48, 3, 8192, 1, 1, 1, 1, id4, true);
+    gen_mul_mat(GGML_TYPE_Q4_0, 4096, 8, 14336, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q4_0, 16, 1, 131072, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q6_K, 16, 2, 131072, 1, 1, 1, 1, id4, false);
+
     std::string path = g_dir + "/manifest.json";
     FILE *f = fopen(path.c_str(), "w");
     fprintf(f, "{\n\"generator\": \"oracle/gen_golden.cpp linked to oracle/_ref/libggml-ref.so (reference sources, oracle/ref.mk)\",\n"

@@ -23,6 +23,8 @@
 #                             driven through the reference's backend API (oracle/split_check.cpp)
 #   _ref/repack_check         MUL_MAT with src0 in our repacked-weight (extra) buffer type vs ggml-cpu
 #                             (oracle/repack_check.cpp)
+#   _ref/cpy_check            a seeded sweep of test-backend-ops' CPY cases, plugin vs ggml-cpu
+#                             (oracle/cpy_check.cpp)
 #   _ref/fusion_check         the GPT-2 node chains the plugin fuses, plugin vs ggml-cpu, through the
 #                             reference's graph API and allocator (oracle/fusion_check.cpp)
 #
@@ -54,7 +56,7 @@ CPU_CXX  := ggml-cpu/ggml-cpu.cpp ggml-cpu/repack.cpp ggml-cpu/hbm.cpp ggml-cpu/
 OBJS := $(patsubst %.c,$(OBJ)/%.c.o,$(BASE_C) $(CPU_C)) $(patsubst %.cpp,$(OBJ)/%.cpp.o,$(BASE_CXX) $(CPU_CXX))
 
 all: $(OUT)/libggml-ref.so $(OUT)/test-backend-ops $(OUT)/test-quantize-fns $(OUT)/gen_golden $(OUT)/ref_cpu_bench $(OUT)/gpt2_ref \
-     $(OUT)/gpt-2-sched $(OUT)/split_check $(OUT)/fusion_check $(OUT)/repack_check
+     $(OUT)/gpt-2-sched $(OUT)/split_check $(OUT)/fusion_check $(OUT)/repack_check $(OUT)/cpy_check
 
 $(OBJ)/ggml-cpu/%.c.o: $(REF)/src/ggml-cpu/%.c
 	@mkdir -p $(dir $@)
@@ -103,6 +105,9 @@ $(OUT)/fusion_check: oracle/fusion_check.cpp $(OUT)/libggml-ref.so
 	g++ $(CXXFLAGS) $< -o $@ $(LINK)
 
 $(OUT)/repack_check: oracle/repack_check.cpp $(OUT)/libggml-ref.so
+	g++ $(CXXFLAGS) $< -o $@ $(LINK)
+
+$(OUT)/cpy_check: oracle/cpy_check.cpp $(OUT)/libggml-ref.so
 	g++ $(CXXFLAGS) $< -o $@ $(LINK)
 
 clean:

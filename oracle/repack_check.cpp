@@ -11,7 +11,10 @@
 //   * NMSE(plugin, ggml-cpu) <= 5e-4 (test-backend-ops' MUL_MAT bar, tests/test-backend-ops.cpp:3106),
 //     at mat-vec sizes (ne11 <= 8, which read the ggml bytes) and mat-mat sizes (the repacked copy);
 //   * after a second ggml_backend_tensor_set with other weights the result follows the new
-//     weights (every write remakes the copy).
+//     weights (every write remakes the copy);
+//   * the same after an asynchronous write (ggml_backend_tensor_set_async on the plugin's backend,
+//     reference ggml-backend.cpp:234), after an upload in three chunks, and while an upload is
+//     incomplete (the first chunk only: MUL_MAT must then read the ggml bytes, not the stale copy).
 // usage: repack_check PLUGIN   (exit 0 = all cases pass)
 #include "ggml-alloc.h"
 #include "ggml-backend.h"
@@ -100,12 +103,27 @@ int main(int argc, char **argv) {
         for (auto &v : x) v = u(rng);
         Weight wg = make_weight(rbt, cs.t, cs.K, cs.N), wc = make_weight(ggml_backend_cpu_buffer_type(), cs.t, cs.K, cs.N);
         bool ok_all = true;
-        for (int pass = 0; pass < 2; ++pass) {   // pass 1: new weights written into the same tensors
+        for (int pass = 0; pass < 5; ++pass) {   // 1: rewrite, 2: async, 3: in chunks, 4: first chunk only
             std::vector<float> w((size_t)cs.N * cs.K);
             for (auto &v : w) v = u(rng);
             std::vector<uint8_t> q(ggml_row_size(cs.t, cs.K) * cs.N);
             ggml_quantize_chunk(cs.t, w.data(), q.data(), 0, cs.N, cs.K, nullptr);
-            ggml_backend_tensor_set(wg.a, q.data(), 0, q.size());
+            const size_t rb = ggml_row_size(cs.t, cs.K), c1 = rb * (cs.N / 3), c2 = rb * (2 * cs.N / 3);
+            if (pass == 2) {
+                ggml_backend_tensor_set_async(gpu, wg.a, q.data(), 0, q.size());
+                ggml_backend_synchronize(gpu);
+            } else if (pass == 3) {
+                ggml_backend_tensor_set(wg.a, q.data(), 0, c1);
+                ggml_backend_tensor_set(wg.a, q.data() + c1, c1, c2 - c1);
+                ggml_backend_tensor_set(wg.a, q.data() + c2, c2, q.size() - c2);
+            } else if (pass == 4) {   // only the first rows change: the rest keep pass 3's bytes
+                std::vector<uint8_t> prev(q.size());
+                ggml_backend_tensor_get(wg.a, prev.data(), 0, prev.size());
+                ggml_backend_tensor_set(wg.a, q.data(), 0, c1);
+                memcpy(q.data() + c1, prev.data() + c1, q.size() - c1);
+            } else {
+                ggml_backend_tensor_set(wg.a, q.data(), 0, q.size());
+            }
             ggml_backend_tensor_set(wc.a, q.data(), 0, q.size());
             std::vector<uint8_t> back(q.size());
             ggml_backend_tensor_get(wg.a, back.data(), 0, back.size());

@@ -32,6 +32,11 @@ for step in "$@"; do
         tbocpy) run tbocpy 900 env GGML_BACKEND_PATH=$PWD/ggml-gfx906_amd/libggml-hip-mi355x.so ./oracle/_ref/test-backend-ops test -o CPY -b MI355X0 ;;
         tbo-*) op=${step#tbo-}; run "tbo_$op" 900 env GGML_BACKEND_PATH=$PWD/ggml-gfx906_amd/libggml-hip-mi355x.so ./oracle/_ref/test-backend-ops test -o "$op" -b MI355X0 ;;
         bench) run bench 600 python bench.py ;;
+        ringpar) run ringpar 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "k11008 or k14336 or k14368 or k12288 or k9216 or k8192 or k131072 or k4096 or k1024" ;;
+        ringb) run ringb 600 bash -c 'S="q4_0:14336:4096:1:8 q4_0:14336:4096:2:8 q4_0:14336:4096:3:8 q4_0:14336:4096:4:8 q4_0:14336:4096:5:8 q4_0:14336:4096:8:8 q4_K:14336:4096:1:8 q4_K:14336:4096:8:8 q6_K:14336:4096:8:8 q8_0:14336:4096:8:8 q4_0:4096:11008:8:8 q4_0:11008:4096:4:8"; python scripts/mmvq_bench.py $S && GGML_MI355X_RING=0 python scripts/mmvq_bench.py $S' ;;
+        tboperf) run tboperf 900 env GGML_BACKEND_PATH=$PWD/ggml-gfx906_amd/libggml-hip-mi355x.so ./oracle/_ref/test-backend-ops perf -o MUL_MAT -b MI355X0 ;;
+        cpychk) run cpychk 600 ./oracle/_ref/cpy_check $PWD/ggml-gfx906_amd/libggml-hip-mi355x.so 100 ;;
+        repchk) run repchk 300 ./oracle/_ref/repack_check $PWD/ggml-gfx906_amd/libggml-hip-mi355x.so ;;
         prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --no-extra --cpu-seconds 1 ;;
         pmc)   run pmc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/pmc -o pmc -- python bench.py --no-extra --cpu-seconds 1 --steps 5 --warmup 1 ;;
         pmcw)  run pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/pmcw -o pmcw -- python bench.py --no-extra --cpu-seconds 1 --steps 5 --warmup 1 ;;

@@ -6,6 +6,9 @@
   failed cases, and at least the executed hot-type f32 case counts of SURVEY Appendix A
   (MUL_MAT 139, MUL_MAT_ID 114) — so the suite cannot pass by declining everything.
 * repack_check (oracle/repack_check.cpp) does the same for the repacked-weight extra buffer type.
+* cpy_check (oracle/cpy_check.cpp) replays test-backend-ops' CPY cases on fixed seeds (test-backend-ops
+  draws its inputs from std::random_device, so one run sees one input per case): 100 inputs per case,
+  NMSE <= 1e-6 on every one.
 * split_check (oracle/split_check.cpp) runs MUL_MAT with src0 in our row-split buffer type
   (ggml_backend_split_buffer_type from the plugin's proc table) through the reference's backend
   API, against ggml-cpu, for 1, 2 and 3 shards (GGML_MI355X_SPLIT_SHARDS; on a one-GPU box the
@@ -23,6 +26,7 @@ LIB = os.path.join(ROOT, "ggml-gfx906_amd", "libggml-hip-mi355x.so")
 TBO = os.path.join(REF, "test-backend-ops")
 SPLIT = os.path.join(REF, "split_check")
 REPACK = os.path.join(REF, "repack_check")
+CPYCHK = os.path.join(REF, "cpy_check")
 HOT = ("q4_0", "q8_0", "q4_K", "q5_K", "q6_K")
 ANSI = re.compile(r"\x1b\[[0-9;]*m")
 
@@ -112,3 +116,15 @@ def test_repack_buffer_type_matches_cpu():
         pytest.skip("oracle/_ref/repack_check not built")
     r = subprocess.run([REPACK, LIB], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "REPACK_CHECK_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+def test_cpy_seeded_sweep():
+    """every CPY case of test-backend-ops that runs on MI355X0, 100 fixed-seed inputs each,
+    NMSE <= 1e-6 (tests/test-backend-ops.cpp:2396-2398) against ggml-cpu on every input"""
+    if not os.path.exists(CPYCHK):
+        pytest.skip("oracle/_ref/cpy_check not built")
+    r = subprocess.run([CPYCHK, LIB, "100"], capture_output=True, text=True, timeout=600)
+    bad = [l for l in r.stdout.splitlines() if "FAIL" in l][:40]
+    assert r.returncode == 0 and "CPY_CHECK_OK" in r.stdout, "\n".join(bad) + r.stdout[-2000:] + r.stderr[-2000:]
+    m = re.search(r"(\d+) cases run on the plugin", r.stdout)
+    assert m and int(m.group(1)) >= 90, r.stdout[-2000:]
