@@ -54,16 +54,13 @@ sys.path.insert(0, os.path.join(ROOT, "ggml-gfx906_amd"))
 
 import mi355x_qmm as M  # noqa: E402
 
-MFMA_F16_PEAK_TFLOPS = 2500.0   # dense f16/bf16 MFMA peak, MI355X_MICROARCH.md (no sparsity)
-MFMA_I8_PEAK_TOPS = 5000.0      # dense int8 MFMA peak (2x the bf16 rate, MI355X_MICROARCH.md MFMA table)
+MFMA_I8_PEAK_TOPS = 5000.0      # dense int8 MFMA peak (2x the bf16 rate, MI355X_MICROARCH.md MFMA table, no sparsity)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 HBM_MEASURED_GBS = 6290.0      # float4 copy measured on MI355X (same guide)
-I8_PEAK_TOPS = 5000.0          # dense int8 / fp8 MFMA (no sparsity)
 # BENCH_ONE_GPU_REHEARSAL=1 with --gpus N: all N ranks share GPU 0 and exchange over gloo through
 # host memory — the N > 1 code paths (rank plumbing, row-split all-gather, pipeline ring,
 # timing reduction) on a one-GPU box. Its numbers are not scaling numbers.
 REHEARSAL = os.environ.get("BENCH_ONE_GPU_REHEARSAL") == "1"
-F16_PEAK_TFLOPS = 2500.0       # dense f16/bf16 MFMA
 
 
 def synthetic_weights(t: int, N: int, K: int, seed: int) -> np.ndarray:
@@ -168,9 +165,8 @@ def config_row(s: MatVecSet, us: float) -> dict:
     tf = s.flops / (us * 1e-6) / 1e12
     row = {"us": round(us, 3), "GB/s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
            "TFLOP/s": round(tf, 3)}
-    if s.Mc > 8:   # mat-mat path: f16 MFMA tiles, priced against the dense f16 peak
-        # the default mat-mat path is the int8 tile (v_mfma_i32_32x32x32_i8): priced against the
-        # dense int8 peak
+    if s.Mc > 8:   # mat-mat path: the int8 tile (v_mfma_i32_32x32x32_i8), priced
+        # against the dense int8 peak
         row.update(bound="mfma", mfma_frac_i8=round(tf / MFMA_I8_PEAK_TOPS, 4),
                    graph_period_us=round(s.graph_period_us(16), 3))
     return row

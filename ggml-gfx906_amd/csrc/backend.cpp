@@ -144,6 +144,7 @@ struct LayerRun {
     int64_t nb_qkv = 0, nb_o = 0, nb_fc = 0, nb_mp = 0;
     const float *b_qkv = nullptr, *b_o = nullptr, *b_fc = nullptr, *b_mp = nullptr;
     float *kc = nullptr, *vc = nullptr;        // this layer's key / value rows (row p at p * E)
+    int64_t cap = 0;                           // rows from kc / vc to the end of their cache buffers
     const struct ggml_tensor *out_t = nullptr;
     bool chain_in = false, chain_out = false;  // residual from / to the neighbouring fused layer
     const float *b_in = nullptr;               // chain_in: the previous layer's MLP-projection bias
@@ -152,6 +153,11 @@ struct FusePlan {
     std::vector<int8_t> skip;
     std::map<int, AttnView> attn;
     std::map<int, LayerRun> layers;   // by the graph index of the layer's first node
+    // every fused layer at one position (a decode step): the layer launches read it from the
+    // backend's device word (lf_pos, set before each run) instead of a kernel argument, so the
+    // launch sequence, and a hipGraph of it, is the same for every token
+    bool pos_word = false;
+    int n_past = 0;
 };
 
 // hipGraph of the last graph_compute (cf. the reference's CUDA graphs, ggml-cuda.cu:2757-2998):
@@ -1661,6 +1667,13 @@ bool match_layer(const struct ggml_cgraph *g, int n, int i, LayerRun &r) {
     r.b_mp = static_cast<const float *>(pb->src[1]->data);
     r.kc = kc;
     r.vc = vc;
+    {   // rows of K / V storage from the layer's first row to the end of the cache tensors
+        const struct ggml_tensor *kb = K->view_src, *vb = P->view_src;
+        const int64_t ck = ((const uint8_t *)kb->data + ggml_base().nbytes(kb) - (const uint8_t *)kc) / (4 * E);
+        const int64_t cv2 = ((const uint8_t *)vb->data + ggml_base().nbytes(vb) - (const uint8_t *)vc) / (4 * E);
+        r.cap = std::min(ck, cv2);
+        if (r.cap <= n_past) return false;
+    }
     return true;
 }
 
@@ -1686,6 +1699,9 @@ void plan_layers(BackendCtx *c, const struct ggml_cgraph *g, int n, FusePlan &pl
              r.chain_in ? ", residual from the previous layer" : "");
         i = r.last;
     }
+    plan.pos_word = !plan.layers.empty();
+    plan.n_past = plan.pos_word ? plan.layers.begin()->second.n_past : 0;
+    for (const auto &kv : plan.layers) plan.pos_word = plan.pos_word && kv.second.n_past == plan.n_past;
 }
 
 int run_layer(BackendCtx *c, const LayerRun &r) {
@@ -1697,9 +1713,13 @@ int run_layer(BackendCtx *c, const LayerRun &r) {
     auto ok = [](hipError_t e) { return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP; };
     int rc;
     const float *base = r.chain_in ? c->lf_y : r.x;
+    // the kernels take the position as min(pos, n_ctx - 1): with the position word set to n_past
+    // (plan.pos_word) n_ctx is the cache capacity, a bound only; otherwise the word holds
+    // INT32_MAX and n_ctx = n_past + 1 carries the position
+    const int n_ctx = c->plan.pos_word ? (int)std::min<int64_t>(r.cap, INT32_MAX) : r.n_past + 1;
     rc = ok(gpt2_attn_block_launch(0, r.type, base, r.b_in, r.chain_in ? c->lf_mlp : nullptr,
                                    r.chain_in ? n_sl : 0, c->lf_x, r.ln1_g, r.ln1_b, r.eps1, r.w_qkv, r.nb_qkv, r.b_qkv, r.kc,
-                                   r.vc, c->lf_pos, r.scale, r.n_past + 1, w_o, r.nb_o, c->lf_attn, r.E, r.n_head, 1, nullptr, 0,
+                                   r.vc, c->lf_pos, r.scale, n_ctx, w_o, r.nb_o, c->lf_attn, r.E, r.n_head, 1, nullptr, 0,
                                    nullptr, nullptr, 0, c->stream));
     if (rc) return rc;
     rc = ok(gpt2_mlp_block_launch(0, r.type, c->lf_x, r.b_o, c->lf_attn, r.n_head, c->lf_y, r.ln2_g, r.ln2_b, r.eps2, r.w_fc, r.nb_fc,
@@ -1721,11 +1741,21 @@ void plan_fusion(BackendCtx *c, const struct ggml_cgraph *g, int n, FusePlan &pl
 
 // queue every node of g on the backend stream (fused runs as planned); quiet: a failure is
 // expected to be retried (inside a hipGraph capture) and is only logged in debug mode
-enum ggml_status run_nodes(BackendCtx *c, struct ggml_cgraph *g, bool quiet) {
+// (planned: c->plan already holds this graph's plan and its position word is set)
+void set_pos_word(BackendCtx *c) {
+    if (c->lf_pos == nullptr) return;
+    const int v = c->plan.pos_word ? c->plan.n_past : 0x7fffffff;
+    HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->lf_pos), v, 1, c->stream));
+}
+
+enum ggml_status run_nodes(BackendCtx *c, struct ggml_cgraph *g, bool quiet, bool planned = false) {
     const GgmlBase &gb = ggml_base();
     const int n = gb.graph_n_nodes(g);
     FusePlan &plan = c->plan;
-    plan_fusion(c, g, n, plan);
+    if (!planned) {
+        plan_fusion(c, g, n, plan);
+        if (!plan.layers.empty()) set_pos_word(c);
+    }
     for (int i = 0; i < n; ++i) {
         struct ggml_tensor *node = gb.graph_node(g, i);
         if (is_empty(node) || is_view_op(node->op) || plan.skip[i]) continue;
@@ -1813,18 +1843,49 @@ void node_props(const struct ggml_tensor *t, NodeProps &p) {
     }
 }
 
-// true when g has the nodes the cached graph was captured from; refreshes the cache either way
-bool graph_unchanged(GraphCache &hg, struct ggml_cgraph *g) {
+// a fused decode layer as one record of what its launches read (run_layer): everything but the
+// position, which moves every token (the cache views, the mask's n_past, the score shapes) and
+// reaches the kernels through the backend's position word instead (FusePlan::pos_word)
+void layer_props(const struct ggml_tensor *first, const LayerRun &r, NodeProps &p) {
+    std::memset(&p, 0, sizeof p);
+    p.node = first;
+    p.data = r.out;
+    p.op = -1;                                   // (no ggml op has this id)
+    p.type = r.type;
+    p.ne[0] = r.E; p.ne[1] = r.n_head; p.ne[2] = r.last; p.ne[3] = (r.chain_in ? 1 : 0) | (r.chain_out ? 2 : 0);
+    p.nb[0] = (size_t)r.nb_qkv; p.nb[1] = (size_t)r.nb_o; p.nb[2] = (size_t)r.nb_fc; p.nb[3] = (size_t)r.nb_mp;
+    std::memcpy(&p.op_params[0], &r.eps1, 4);
+    std::memcpy(&p.op_params[1], &r.eps2, 4);
+    std::memcpy(&p.op_params[2], &r.scale, 4);
+    std::memcpy(&p.op_params[3], &r.cap, 8);
+    const void *ptrs[] = {r.x, r.ln1_g, r.ln1_b, r.ln2_g, r.ln2_b, r.w_qkv, r.w_o, r.w_fc, r.w_mp, r.b_qkv,
+                          r.b_o, r.b_fc, r.b_mp, r.kc, r.vc, r.b_in};
+    static_assert(sizeof ptrs / sizeof ptrs[0] <= 2 * GGMLABI_MAX_SRC, "room for the layer's pointers");
+    for (size_t i = 0; i < sizeof ptrs / sizeof ptrs[0]; ++i) (i < GGMLABI_MAX_SRC ? p.src[i] : p.src_data[i - GGMLABI_MAX_SRC]) = ptrs[i];
+}
+
+// true when g (as planned) queues the launches the cached graph was captured from; refreshes the
+// cache either way. Nodes compare by their properties; a fused decode layer by layer_props when
+// its position comes from the position word, so a decode graph that differs from the last one
+// only in its position is replayed, not re-captured.
+bool graph_unchanged(GraphCache &hg, struct ggml_cgraph *g, const FusePlan &plan) {
     const GgmlBase &gb = ggml_base();
     const int n = gb.graph_n_nodes(g);
-    bool same = (int)hg.props.size() == n;
-    if (!same) hg.props.resize(n);
+    thread_local std::vector<NodeProps> cur;
+    cur.clear();
     for (int i = 0; i < n; ++i) {
         NodeProps p;
-        node_props(gb.graph_node(g, i), p);
-        if (same && std::memcmp(&p, &hg.props[i], sizeof p) != 0) same = false;
-        hg.props[i] = p;
+        const auto lr = plan.pos_word ? plan.layers.find(i) : plan.layers.end();
+        if (lr != plan.layers.end()) {
+            layer_props(gb.graph_node(g, i), lr->second, p);
+            i = lr->second.last;
+        } else {
+            node_props(gb.graph_node(g, i), p);
+        }
+        cur.push_back(p);
     }
+    const bool same = cur.size() == hg.props.size() && std::memcmp(cur.data(), hg.props.data(), cur.size() * sizeof(NodeProps)) == 0;
+    hg.props.swap(cur);
     return same;
 }
 
@@ -1848,9 +1909,14 @@ enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
         // generation check below then refuses to replay it
         return run_nodes(c, g, false);
     }
-    const bool same = graph_unchanged(hg, g) && hg.scratch_gen == c->scratch.gen && hg.lr_gen == g_lr_gen.load();
+    plan_fusion(c, g, ggml_base().graph_n_nodes(g), c->plan);
+    // the position word is written outside the captured launches, before every run of them
+    if (!c->plan.layers.empty()) set_pos_word(c);
+    const bool same = graph_unchanged(hg, g, c->plan) && hg.scratch_gen == c->scratch.gen && hg.lr_gen == g_lr_gen.load();
     if (same && hg.exec) {
         hg.updates = 0;
+        logf("hipGraph replayed on %s (%d nodes%s)\n", c->name.c_str(), ggml_base().graph_n_nodes(g),
+             c->plan.pos_word ? ", position word" : "");
         HIP_OK(hipGraphLaunch(hg.exec, c->stream));
         return GGML_STATUS_SUCCESS;
     }
@@ -1862,7 +1928,7 @@ enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
         return run_nodes(c, g, false);
     }
     HIP_OK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed));
-    const enum ggml_status st = run_nodes(c, g, true);
+    const enum ggml_status st = run_nodes(c, g, true, true);
     hipGraph_t graph = nullptr;
     const hipError_t ec = hipStreamEndCapture(c->stream, &graph);
     if (st != GGML_STATUS_SUCCESS || ec != hipSuccess || graph == nullptr) {
@@ -1870,7 +1936,7 @@ enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
         (void)hipGetLastError();
         if (graph) (void)hipGraphDestroy(graph);
         hg.props.clear();
-        return run_nodes(c, g, false);
+        return run_nodes(c, g, false, true);   // (planned, position word set above)
     }
     if (hg.exec) {
         hipGraphNode_t err_node = nullptr;

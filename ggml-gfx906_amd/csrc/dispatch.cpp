@@ -29,7 +29,6 @@ int mmvq_max_k_for_nc(int nc);
 bool mmvq_bigk(int K);
 hipError_t mmvq_ring_launch(int type, const MmArgs &a, int nc, int rpw, hipStream_t st);
 hipError_t dequant_launch(int type, const void *src, float *dst, int64_t n, hipStream_t st);
-hipError_t mmq_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
 struct RowsArgs {
     const uint8_t *src; int64_t nb01, nb02, nb03, ne01;
     const uint8_t *idx; int64_t nb10, nb11, nb12, ne10, ne11;
@@ -51,9 +50,6 @@ struct CpyQArgs {
     int64_t n;
 };
 hipError_t cpy_q_launch(int type, bool to_f32, const CpyQArgs &a, hipStream_t st);
-bool mmq_supported(int type, const MmArgs &a);
-bool mmq_id_supported(int type, const MmArgs &a);
-hipError_t mmq_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
 bool mmq8_supported(int type, const MmArgs &a);
 bool mmq8_images_fit(int type, const MmArgs &a);
 hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
@@ -64,16 +60,11 @@ bool mmq8_id_supported(int type, const MmArgs &a);
 hipError_t mmq8_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
 
 // mat-mat kernel family: the int8 MFMA tile (csrc/mmq8.hip). It takes every K and every
-// 2-byte-aligned Q4_0 / Q8_0 / Q6_K layout (16-B aligned Q4_K / Q5_K), is exact in the block
-// scales (no f16 range to overflow) and measured as fast or faster than the f16 tiles for Q4_0 /
-// Q8_0 / Q4_K / Q5_K from 9 to 2048 tokens (scripts/mmq8_sweep.sh, profiles/r03_mmq_sweep.txt).
-// What it refuses (a K-quant view at an offset finer than 16 B, > 4 GiB spans) takes the
-// mat-vec, which is exact too. The f16 kernels (csrc/mmq.hip) run only when GGML_MI355X_MMQ = f16
-// asks for them (A/B measurements): their LDS-staged tiles overflow f16 past d > 511 (Q8_0).
-static bool mmq_f16_forced() {
-    const char *env = getenv("GGML_MI355X_MMQ");   // read per call: tests switch it
-    return env && !strcmp(env, "f16");
-}
+// 2-byte-aligned Q4_0 / Q8_0 / Q6_K layout (16-B aligned Q4_K / Q5_K) and is exact in the block
+// scales. What it refuses (a K-quant view at an offset finer than 16 B, > 4 GiB spans) takes the
+// mat-vec, which is exact too. (Rounds 1-4 also shipped f16 MFMA tiles, behind
+// GGML_MI355X_MMQ=f16 for A/B only; with a known f16 range hole past d > 511 and no default
+// shape using them they were removed in round 5)
 
 static constexpr size_t LDS_LIMIT = 159 * 1024;   // 160 KB per CU, less the kernels' static arrays
 
@@ -247,7 +238,6 @@ int mul_mat_rp(const TensorView &a, const void *rp, const TensorView &b, const T
     MmArgs m = base_args(a, b, d);
     std::lock_guard<std::mutex> hold(scratch.mu);   // until the scratch users are queued
     hipError_t e;
-    const bool f16 = mmq_f16_forced();
     const int n_mat = (int)(a.ne[2] * a.ne[3]);
     const int rmin = repack_min_tokens();
     // a caller's repacked copy (a 64-token tile) against the in-place tile: the copy wins while the
@@ -261,11 +251,10 @@ int mul_mat_rp(const TensorView &a, const void *rp, const TensorView &b, const T
     static const bool rp_all = getenv("GGML_MI355X_MMQ_RP_ALL") && atoi(getenv("GGML_MI355X_MMQ_RP_ALL")) == 1;
     const bool wide = !rp_all && mmq8_supported(a.type, m) && mmq8_tile_tokens(m) == 128 &&
                       (m.M >= 1024 || mmq8_tiles128(m) < 256);
-    const bool use_rp = m.M > 8 && !f16 && ((rp != nullptr && !wide) || (rmin > 0 && m.M >= rmin)) &&
+    const bool use_rp = m.M > 8 && ((rp != nullptr && !wide) || (rmin > 0 && m.M >= rmin)) &&
                         repack_size(a) != 0 && mmq8_images_fit(a.type, m);
     if (use_rp) e = mmq8r_launch(a.type, m, rp, (int)a.ne[2], n_mat, st, scratch);
-    else if (m.M > 8 && !f16 && mmq8_supported(a.type, m)) e = mmq8_launch(a.type, m, st, scratch);
-    else if (m.M > 8 && f16 && mmq_supported(a.type, m)) e = mmq_launch(a.type, m, st, scratch);
+    else if (m.M > 8 && mmq8_supported(a.type, m)) e = mmq8_launch(a.type, m, st, scratch);
     else e = run_mmvq(a.type, m, 0, m.M, st);
     if (e == hipErrorOutOfMemory) return GGML_MI355X_ENOMEM;
     return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
@@ -311,13 +300,9 @@ int mul_mat_id(const TensorView &as, const TensorView &b, const TensorView &ids,
     m.x_aligned16 = aligned16(b.data, m.nb11, m.nb12, m.nb13);
     static const int min_pairs = getenv("GGML_MI355X_MMQ_ID_MIN") ? atoi(getenv("GGML_MI355X_MMQ_ID_MIN")) : MMQ_ID_MIN_PAIRS;
     const bool grouped = m.n_used * m.n_tok >= min_pairs;
-    // the grouped int8 tile; the f16 one only when GGML_MI355X_MMQ=f16 asks (as for MUL_MAT)
-    const bool f16 = mmq_f16_forced();
-    const bool i8 = grouped && !f16 && mmq8_id_supported(as.type, m);
+    const bool i8 = grouped && mmq8_id_supported(as.type, m);
     std::lock_guard<std::mutex> hold(scratch.mu);
-    const hipError_t e = i8 ? mmq8_id_launch(as.type, m, st, scratch)
-                         : grouped && f16 && mmq_id_supported(as.type, m) ? mmq_id_launch(as.type, m, st, scratch)
-                                                                          : mmvq_id_launch(as.type, m, 1, st);
+    const hipError_t e = i8 ? mmq8_id_launch(as.type, m, st, scratch) : mmvq_id_launch(as.type, m, 1, st);
     if (e == hipErrorOutOfMemory) return GGML_MI355X_ENOMEM;
     return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
 }

@@ -16,8 +16,10 @@
 //      tiles that share the token (A) fragment. Per super-block the weight rows are loaded with
 //      16-B buffer loads into registers one stage ahead, decoded to int8 codes (Q4_0: q-8,
 //      Q4_K: q, Q5_K: q | qh<<4, Q6_K: q-32, Q8_0 as is) and written to LDS in MFMA-fragment
-//      order with an XOR swizzle that keeps both the staging writes and the fragment reads free
-//      of bank conflicts. K-group g takes blocks 4g..4g+3 of every super-block.
+//      order with an XOR swizzle meant to spread the staging writes and fragment reads over the
+//      banks (the counters still show 0.14 M SQ_LDS_BANK_CONFLICT cycles per Q8_0 4096 x 4096 x
+//      512 call, profiles/r04_mmq8_pmc.txt; the repacked tile below has none). K-group g takes
+//      blocks 4g..4g+3 of every super-block.
 //        Q8_0 / Q4_0: v_mfma_i32_32x32x32_i8 per 32-k block with C = 0x4B400000: the int32
 //          result R + 0x4B400000 IS the f32 bit pattern of 12582912 + R (|R| < 2^22), so one
 //          fma per output and block applies the weight scale: p += (12582912 + R) * d_w; the
@@ -87,7 +89,7 @@ constexpr float Q8_MAGIC_F = 12582912.0f;
 constexpr int XI_DX = 16384, XI_BS = 16640;
 template <int T> constexpr bool q8_has_min() { return T == T_Q4_K || T == T_Q5_K; }
 template <int T> constexpr int ximg_bytes() { return q8_has_min<T>() ? 19456 : 17408; }
-// ---- MUL_MAT_ID: expert-sorted (slot, token) pairs (moe_prep in mmq.hip), 64-pair token tiles
+// ---- MUL_MAT_ID: expert-sorted (slot, token) pairs (moe_prep below), 64-pair token tiles
 //   offsets[e] .. offsets[e+1]: sorted positions of expert e's pairs; tile_off[e]: first tile of
 //   expert e (prefix sum of ceil(count / 64)); pos_pair[q]: pair t * n_used + slot at position q
 struct Moe8 {
@@ -1401,8 +1403,44 @@ hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scrat
 // exit at once, so nothing waits on the host. (Reference: ggml_cuda_mul_mat_id,
 // src/ggml-cuda/ggml-cuda.cu:2092-2230, which runs its int8 MMQ per expert.)
 // ------------------------------------------------------------------------------------------
-hipError_t moe_prep_launch(const MmArgs &a, int *offsets, int *tile_off, int *pos_pair, hipStream_t st);
 constexpr int MOE8_MAX_EXPERTS = 1024;   // moe_prep's LDS counters
+
+// counting sort of the (slot, token) pairs by expert in LDS (one 1024-thread workgroup): per
+// expert the offset of its pairs and of its 64-pair token tiles, and the sorted pair list — the
+// expert grouping of ggml_compute_forward_mul_mat_id (src/ggml-cpu/ggml-cpu.c:1564-1579)
+__global__ __launch_bounds__(1024) void moe_prep(const MmArgs a, int *offsets, int *tile_off, int *pos_pair) {
+    __shared__ int cnt[MOE8_MAX_EXPERTS], cur[MOE8_MAX_EXPERTS];
+    const int E = a.n_expert, P = a.n_used * a.n_tok;
+    for (int e = threadIdx.x; e < E; e += 1024) cnt[e] = 0;
+    __syncthreads();
+    auto expert_of = [&](int p) {
+        const int slot = p % a.n_used, t = p / a.n_used;
+        const int ex = *reinterpret_cast<const int32_t *>(reinterpret_cast<const uint8_t *>(a.ids) + slot * a.ids_nb0 +
+                                                          (int64_t)t * a.ids_nb1);
+        return min(max(ex, 0), E - 1);     // host validates ids; never index out of bounds
+    };
+    for (int p = threadIdx.x; p < P; p += 1024) atomicAdd(&cnt[expert_of(p)], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int o = 0, tl = 0;
+        for (int e = 0; e < E; ++e) {
+            offsets[e] = o;
+            tile_off[e] = tl;
+            cur[e] = o;
+            o += cnt[e];
+            tl += (cnt[e] + Q8_TOK - 1) / Q8_TOK;
+        }
+        offsets[E] = o;
+        tile_off[E] = tl;
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < P; p += 1024) pos_pair[atomicAdd(&cur[expert_of(p)], 1)] = p;
+}
+
+static hipError_t moe_prep_launch(const MmArgs &a, int *offsets, int *tile_off, int *pos_pair, hipStream_t st) {
+    hipLaunchKernelGGL(moe_prep, dim3(1), dim3(1024), 0, st, a, offsets, tile_off, pos_pair);
+    return hipGetLastError();
+}
 
 static int64_t moe8_tiles(const MmArgs &a) { return ((int64_t)a.n_used * a.n_tok + 63) / 64 + a.n_expert; }
 

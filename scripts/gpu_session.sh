@@ -43,6 +43,13 @@ for step in "$@"; do
         profsingles) run profsingles 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsingles -o run -- python scripts/prof_singles.py ;;
         profgpt2) run profgpt2 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profgpt2 -o run -- python scripts/gpt2_bench.py 1 256 1 ;;
         gpt2b) run gpt2b 300 python scripts/gpt2_bench.py 1 256 1 ;;
+        gpt2tests) run gpt2tests 900 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpt2.py tests/test_gpt2_example.py tests/test_graph_fusion.py tests/test_gpt2_pipeline.py -m gpu ;;
+        plugab) run plugab 600 bash scripts/plugin_gpt2_ab.sh ;;
+        pmcring) run pmcring 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/pmcring -o pmc -- python scripts/mmvq_bench.py q4_0:14336:4096:1:8 q4_0:14336:4096:8:8 q4_K:14336:4096:8:8
+                 python scripts/pmc_summary.py $OUT/pmcring > $OUT/pmcring_summary.txt; find $OUT/pmcring -name '*.csv' -size +2M -delete ;;
+        floor) run floor_stream 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/floor_stream -o run -- scripts/hbm_probe s
+               run floor_mv 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/floor_mv -o run -- python scripts/prof_singles.py 128 q4_K:4096:64
+               for d in floor_stream floor_mv; do for t in $(find $OUT/$d -name '*kernel_trace.csv'); do python scripts/trace_summary.py $t 2 > $OUT/${d}_summary.txt; rm -f $t; done; done ;;
         mmq)   run mmq 300 python scripts/mmq_bench.py ;;
         profmmq) run profmmq 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profmmq -o run -- python scripts/mmq_bench.py q8_0:4096:4096:512 q4_K:4096:4096:512 ;;
         *) echo "unknown step $step" ;;

@@ -107,7 +107,50 @@ __global__ void empty_kernel(uint32_t *out) {
     if (threadIdx.x == 12345) out[0] = 1;
 }
 
+// the bare stream under a per-grid kernel name, so a rocprofv3 kernel trace separates the grids
+template <int TAG>
+__global__ void stream_read_tag(const uint4 *__restrict__ p, size_t per_wg_vec, uint32_t *out) {
+    const uint4 *base = p + (size_t)blockIdx.x * per_wg_vec;
+    uint32_t acc = 0;
+    for (size_t i = threadIdx.x; i < per_wg_vec; i += (size_t)blockDim.x * 4) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const size_t j = i + (size_t)u * blockDim.x;
+            v[u] = j < per_wg_vec ? base[j] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    if (acc == 0x12345678u) out[blockIdx.x] = acc;
+}
+
 int main(int argc, char **argv) {
+    if (argc > 1 && argv[1][0] == 's') {
+        // single launches of a bare 9,469,952-B stream (one Q4_K 4096 x 4096 matrix), 64 rotated
+        // copies (HBM-cold, > the 256 MiB Infinity Cache), 128 launches per grid, one sync each:
+        // for rocprofv3 --kernel-trace --stats, the floor beside the mat-vec's single launches
+        // (scripts/prof_singles.py) on the same basis
+        const size_t bytes = 9469952 / 16 * 16;
+        const int copies = 64;
+        std::vector<uint4 *> bufs(copies);
+        for (auto &b : bufs) { CK(hipMalloc(&b, bytes)); CK(hipMemset(b, 1, bytes)); }
+        uint32_t *o;
+        CK(hipMalloc(&o, 1 << 20));
+        auto go = [&](auto kern, int wgs) {
+            const size_t per = bytes / 16 / wgs;
+            for (int i = 0; i < 128 + copies; ++i) {
+                hipLaunchKernelGGL(kern, dim3(wgs), dim3(512), 0, 0, bufs[i % copies], per, o);
+                CK(hipDeviceSynchronize());
+            }
+        };
+        go(stream_read_tag<256>, 256);
+        go(stream_read_tag<512>, 512);
+        go(stream_read_tag<1024>, 1024);
+        go(stream_read_tag<2048>, 2048);
+        printf("done\n");
+        return 0;
+    }
     {
         uint32_t *o;
         CK(hipMalloc(&o, 64));

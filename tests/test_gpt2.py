@@ -388,6 +388,10 @@ def test_reference_scheduler_layer_fusion(name):
             # every decode graph (positions 1 .. n-1) fuses all its layers, chained
             assert len(fused) >= (n - 1) * SMALL["n_layer"], (len(fused), [ln for ln in r.stderr.splitlines() if "not fused" in ln][:8])
             assert any("residual from the previous layer" in ln for ln in fused) or SMALL["n_layer"] == 1
+            # the decode graphs differ only in their position, which the fused layers read from the
+            # backend's position word: after the first decode step's capture every step replays it
+            replays = [ln for ln in r.stderr.splitlines() if "hipGraph replayed" in ln and "position word" in ln]
+            assert len(replays) >= n - 4, (len(replays), r.stderr[-1500:])
         else:
             assert not fused
         got[fuse] = np.fromfile(out, np.float32).reshape(n, -1)

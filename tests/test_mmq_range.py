@@ -1,12 +1,8 @@
-"""Huge block scales on the mat-mat path.
-  * f16 kernels (csrc/mmq.hip, run only when GGML_MI355X_MMQ=f16 forces them): weights are
-    decoded to f16 inside the register-decode tile, so rows whose block scales reach 1.0 (|w| in
-    the hundreds or more, far outside what quantized LLM weights hold) take an exact fp32
-    recomputation instead of overflowing (M <= 64);
-  * the default int8 tile (csrc/mmq8.hip, every K and 2-byte-aligned layout) converts every scale
-    to f32: exact at any M, including the K = 96 k shapes that used to take the f16 tiles
-    (tests/test_mmq8.py covers M = 200 and 512 for all five types).
-Checked against the CPU oracle on rows mixing ordinary and huge scales."""
+"""Huge block scales on the mat-mat path: the int8 tile (csrc/mmq8.hip, every K and 2-byte-aligned
+layout) converts every scale to f32, so it is exact at any M, including the K = 96 k shapes
+(tests/test_mmq8.py covers M = 200 and 512 for all five types). (The f16 tiles that overflowed
+past d > 511 were removed in round 5.) Checked against the CPU oracle on rows mixing ordinary and
+huge scales."""
 import os
 
 import numpy as np
@@ -29,7 +25,7 @@ def mm():
     return M
 
 
-@pytest.fixture(params=["f16", "i8", "default"])
+@pytest.fixture(params=["i8", "default"])
 def path(request):
     old = os.environ.get("GGML_MI355X_MMQ")
     if request.param == "default":
@@ -46,8 +42,6 @@ def path(request):
 @pytest.mark.parametrize("t,big", [(qref.Q8_0, 7.0e4), (qref.Q4_K, 2.0e3), (qref.Q4_0, 1.0e5)])
 @pytest.mark.parametrize("M,K", [(16, 512), (40, 512), (200, 96 * 3), (512, 96 * 5)])
 def test_huge_scales_match_oracle(mm, path, t, big, M, K):
-    if path == "f16" and M > 64:
-        pytest.skip("the f16 LDS-staged tiles overflow past d > 511: why they are not the default")
     if qref.BLCK[t] == 256 and K % 256:
         K = 768
     N = 160
