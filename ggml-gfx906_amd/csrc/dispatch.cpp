@@ -27,7 +27,8 @@ size_t mmvq_lds_bytes(int K, int nc);
 bool mmvq_has_nc(int nc);
 int mmvq_max_k_for_nc(int nc);
 bool mmvq_bigk(int K);
-hipError_t mmvq_ring_launch(int type, const MmArgs &a, int nc, int rpw, hipStream_t st);
+hipError_t mmvq_ring_launch(int type, const MmArgs &a, int nc, int rpw, uint8_t *img, hipStream_t st);
+size_t mmvq_ring_img_bytes(const MmArgs &a, int nc);
 hipError_t dequant_launch(int type, const void *src, float *dst, int64_t n, hipStream_t st);
 struct RowsArgs {
     const uint8_t *src; int64_t nb01, nb02, nb03, ne01;
@@ -170,8 +171,17 @@ static bool use_ring(int K, int ncols) {
     return ncols >= 2 || ring_policy() == 2 || mmvq_bigk(K);
 }
 
-// mat-vec over columns [c0, c0 + ncols) in groups of at most 8
-static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st) {
+// column groups of at least ring_pre_min() columns at K > 4096 are quantized once per call into
+// scratch (mmvq_prequant) instead of by every workgroup; GGML_MI355X_RING_PRE=0: in the
+// workgroups (A/B), =2: from 2 columns on (default 4)
+static int ring_pre_min() {
+    static const int v = getenv("GGML_MI355X_RING_PRE") ? atoi(getenv("GGML_MI355X_RING_PRE")) : 1;
+    return v == 0 ? 1 << 30 : v == 2 ? 2 : 4;
+}
+
+// mat-vec over columns [c0, c0 + ncols) in groups of at most 8 (scratch: the caller holds its
+// mutex; nullptr = no pre-quantized images)
+static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st, Scratch *scratch = nullptr) {
     const int rpw = pick_rpw(type, (int64_t)m.N * m.ne12 * m.ne13);
     while (ncols > 0) {
         MmArgs g = m;
@@ -183,7 +193,10 @@ static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st
             const int take = std::min(ncols, 8);   // one launch: the last column group may be partial
             nc = take <= 1 ? 1 : take <= 2 ? 2 : take <= 4 ? 4 : 8;
             g.M = take;
-            e = mmvq_ring_launch(type, g, nc, rpw, st);
+            uint8_t *img = nullptr;
+            if (nc >= ring_pre_min() && scratch != nullptr)   // (nullptr inside a capture that would grow it)
+                img = static_cast<uint8_t *>(scratch->get(mmvq_ring_img_bytes(g, nc), st));
+            e = mmvq_ring_launch(type, g, nc, rpw, img, st);
             nc = take;
         } else {
             nc = mmvq_bigk(m.K) ? 1 : std::min(ncols, 8);
@@ -255,7 +268,7 @@ int mul_mat_rp(const TensorView &a, const void *rp, const TensorView &b, const T
                         repack_size(a) != 0 && mmq8_images_fit(a.type, m);
     if (use_rp) e = mmq8r_launch(a.type, m, rp, (int)a.ne[2], n_mat, st, scratch);
     else if (m.M > 8 && mmq8_supported(a.type, m)) e = mmq8_launch(a.type, m, st, scratch);
-    else e = run_mmvq(a.type, m, 0, m.M, st);
+    else e = run_mmvq(a.type, m, 0, m.M, st, &scratch);
     if (e == hipErrorOutOfMemory) return GGML_MI355X_ENOMEM;
     return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
 }
@@ -530,11 +543,35 @@ void *Scratch::get(size_t bytes, hipStream_t st) {
     return ptr;
 }
 
+int *Scratch::counters(hipStream_t st) {
+    if (cnt) return cnt;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess) {
+        (void)hipGetLastError();
+        cs = hipStreamCaptureStatusNone;
+    }
+    if (cs != hipStreamCaptureStatusNone) return nullptr;   // (the caller takes its other path)
+    void *p = nullptr;
+    if (hipMalloc(&p, COUNTERS * sizeof(int)) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (hipMemset(p, 0, COUNTERS * sizeof(int)) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFree(p);
+        return nullptr;
+    }
+    cnt = static_cast<int *>(p);
+    return cnt;
+}
+
 void Scratch::release() {
     if (ptr) (void)hipFree(ptr);
     ptr = nullptr;
     cap = 0;
     ++gen;
+    if (cnt) (void)hipFree(cnt);
+    cnt = nullptr;
 }
 
 Scratch::~Scratch() { release(); }

@@ -39,6 +39,11 @@ struct Scratch {
     int device = -1;
     uint64_t gen = 0;
     void *get(size_t bytes, hipStream_t st);
+    // stream-K tile counters (mmq8.hip): a separate zeroed allocation of COUNTERS ints, made once
+    // (outside any capture) and never moved; every launch leaves them zero
+    static constexpr int COUNTERS = 16384;
+    int *cnt = nullptr;
+    int *counters(hipStream_t st);
     void release();                   // free now (on the current device)
     ~Scratch();
 };

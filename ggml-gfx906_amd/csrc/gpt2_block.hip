@@ -389,19 +389,6 @@ __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
     const int p = min(max(a.pos[s], 0), a.n_ctx - 1);
     RowsDot<T, 16, 6, QNIT> qd;
     qd.load([&](int vr) { return a.w_qkv + (int64_t)((vr >> 6) * E + h * HD + (vr & 63)) * a.nb_qkv; }, 3 * HD, 0, 0, E / 64);
-    // c_proj K-split weights: the slots holding head h's 64 columns (Q6_K: halves of two slots).
-    // Q4_0 / Q8_0: the engine's head-major copy [head][row][one slot] (gpt2.cpp), a contiguous
-    // stream; K-quants read the ggml rows in place. The first pass is issued here, behind the
-    // q/k/v stream, so it has landed by the time the attention output is ready.
-    constexpr int OLPR = T == T_Q6_K ? 2 : 1;
-    const int os0 = T == T_Q6_K ? 4 * (h >> 2) + 2 * ((h & 3) >> 1) : h;
-    const int ows0 = REPACK<T> ? 0 : -1;
-    auto orow = [&](int r) {
-        return REPACK<T> ? a.w_o + ((int64_t)h * E + r) * (2 * QT<T>::bytes) : a.w_o + (int64_t)r * a.nb_o;
-    };
-    RowsDot<T, OLPR, 2, 1> od0;
-    constexpr bool OD_EARLY = T != T_Q6_K;   // (Q6_K's 23-register fragments would spill: issued after the keys)
-    if constexpr (OD_EARLY) od0.load(orow, E, 0, os0, OLPR, ows0);
     __builtin_amdgcn_sched_barrier(0);
     stamp(a, 0, 8);
     if (a.stamps != nullptr) {   // diagnostics: when this wave's first residual row has landed
@@ -489,47 +476,40 @@ __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
             m = mn;
         }
     }
-    // merge the wave's 4 key groups (lanes 16 g .. 16 g + 15) in registers: the partial of the
-    // wave, (max, sum, o[64]) with lane d4 holding dims 4 d4 .. 4 d4 + 3, then one LDS record per
-    // wave (the cross-wave merge below reads 8 records instead of 32)
-    {
-        const float mg = l > 0.f ? m : -INFINITY;
-        float mw = fmaxf(mg, xchg<16>(mg));
-        mw = fmaxf(mw, xchg<32>(mw));
-        const float cw = mw > -INFINITY && l > 0.f ? expf(m - mw) : 0.f;
-        float lw = l * cw;
-        float4 ow = make_float4(o4.x * cw, o4.y * cw, o4.z * cw, o4.w * cw);
-        lw += xchg<16>(lw);
-        lw += xchg<32>(lw);
-        ow.x += xchg<16>(ow.x); ow.y += xchg<16>(ow.y); ow.z += xchg<16>(ow.z); ow.w += xchg<16>(ow.w);
-        ow.x += xchg<32>(ow.x); ow.y += xchg<32>(ow.y); ow.z += xchg<32>(ow.z); ow.w += xchg<32>(ow.w);
-        if (lane < 16) reinterpret_cast<float4 *>(go[wave])[d4] = ow;
-        if (lane == 0) { gm[wave] = mw; gl[wave] = lw; }
-    }
-    if constexpr (!OD_EARLY) od0.load(orow, E, 0, os0, OLPR, ows0);
+    reinterpret_cast<float4 *>(go[grp])[d4] = o4;
+    if (d4 == 0) { gm[grp] = m; gl[grp] = l; }
+
+    // c_proj K-split weights: the slots holding head h's 64 columns (Q6_K: halves of two slots).
+    // Q4_0 / Q8_0: the engine's head-major copy [head][row][one slot] (gpt2.cpp), a contiguous
+    // stream; K-quants read the ggml rows in place
+    constexpr int OLPR = T == T_Q6_K ? 2 : 1;
+    const int os0 = T == T_Q6_K ? 4 * (h >> 2) + 2 * ((h & 3) >> 1) : h;
+    const int ows0 = REPACK<T> ? 0 : -1;
+    auto orow = [&](int r) {
+        return REPACK<T> ? a.w_o + ((int64_t)h * E + r) * (2 * QT<T>::bytes) : a.w_o + (int64_t)r * a.nb_o;
+    };
+    RowsDot<T, OLPR, 2, 1> od0;
+    od0.load(orow, E, 0, os0, OLPR, ows0);
     stamp(a, 0, 4);
     lds_barrier();
 
-    // ---- merge the 8 wave partials and key p (wave 0: lane w < 8 scores wave w's partial, then
-    // lane d owns o[d]); straight-line, every LDS read of a step issued together
+    // ---- merge the key groups and key p (wave 0: lane g < 32 scores group g, then lane d
+    // owns o[d]); straight-line, every LDS read of a step issued together
     if (wave == 0) {
         const float sp = wave_sum(qkv_s[lane] * qkv_s[HD + lane]) * a.scale;
-        const int g = lane & (NW - 1);
+        const int g = lane & (AGROUPS - 1);
         const float gmv = gm[g], glv = gl[g];
         float mx = glv > 0.f ? gmv : -INFINITY;
         mx = fmaxf(mx, xchg<1>(mx)); mx = fmaxf(mx, xchg<2>(mx)); mx = fmaxf(mx, xchg<4>(mx));
+        mx = fmaxf(mx, xchg<8>(mx)); mx = fmaxf(mx, xchg<16>(mx)); mx = fmaxf(mx, xchg<32>(mx));
         const float MX = fmaxf(mx, sp);
         const float wg = glv > 0.f ? expf(gmv - MX) : 0.f;
         const float ep = expf(sp - MX);
-        float lsum = wg * glv;                    // (every 8 lanes hold the 8 partials: the butterfly
-        lsum += xchg<1>(lsum);                    //  over 1, 2, 4 gives every lane the sum)
-        lsum += xchg<2>(lsum);
-        lsum += xchg<4>(lsum);
-        const float L = lsum + ep;
-        if (lane < NW) gw_s[lane] = wg;
+        const float L = wave_sum(lane < AGROUPS ? wg * glv : 0.f) + ep;
+        if (lane < AGROUPS) gw_s[lane] = wg;
         float O = ep * qkv_s[2 * HD + lane];
 #pragma unroll
-        for (int w = 0; w < NW; ++w) O += gw_s[w] * go[w][lane];
+        for (int w = 0; w < AGROUPS; ++w) O += gw_s[w] * go[w][lane];
         o_s[lane] = O / L;
         // quantize o (blocks 2h, 2h+1) in the same wave: its LDS accesses run in order
         if (lane < 8) {
@@ -577,18 +557,6 @@ __global__ __launch_bounds__(BT) void mlp_block_kernel(const BlockArgs a) {
     const float fb = a.b_fc[j * MLP_SLICE + min(tid, MLP_SLICE - 1)];
     RowsDot<T, 16, MLP_SLICE / 32, FNIT> fd;
     fd.load([&](int r) { return a.w_fc + (int64_t)(j * MLP_SLICE + r) * a.nb_fc; }, MLP_SLICE, 0, 0, E / 64);
-    // mlp proj K-split weights: slots [SL j, SL j + SL) of every row (the slice's columns); one
-    // pass covers 8 waves x 32 x 3 = 768 rows. The first pass is issued here, behind the fc
-    // stream, so it has landed when h is ready.
-    constexpr int SL = MLP_SLICE / 64;
-    using MD = RowsDot<T, SL, 3, 1>;
-    MD md0;
-    // Q4_0 / Q8_0: the engine's slice-major copy [slice][row][SL slots] (a contiguous stream)
-    const int mws0 = REPACK<T> ? 0 : -1;
-    auto mrow = [&](int r) {
-        return REPACK<T> ? a.w_mp + ((int64_t)j * E + r) * (SL * 2 * QT<T>::bytes) : a.w_mp + (int64_t)r * a.nb_mp;
-    };
-    md0.load(mrow, E, 0, SL * j, SL, mws0);
     __builtin_amdgcn_sched_barrier(0);
     stamp(a, 1, 8);
 
@@ -609,6 +577,17 @@ __global__ __launch_bounds__(BT) void mlp_block_kernel(const BlockArgs a) {
     fd.compute(sx, E, MLP_SLICE, [&](int r, float v) { h_s[r] = gelu_ggml(v + fb_s[r]); });
     stamp(a, 1, 11);
 
+    // mlp proj K-split weights: slots [SL j, SL j + SL) of every row (the slice's columns); one
+    // pass covers 8 waves x 32 x 3 = 768 rows
+    constexpr int SL = MLP_SLICE / 64;
+    using MD = RowsDot<T, SL, 3, 1>;
+    MD md0;
+    // Q4_0 / Q8_0: the engine's slice-major copy [slice][row][SL slots] (a contiguous stream)
+    const int mws0 = REPACK<T> ? 0 : -1;
+    auto mrow = [&](int r) {
+        return REPACK<T> ? a.w_mp + ((int64_t)j * E + r) * (SL * 2 * QT<T>::bytes) : a.w_mp + (int64_t)r * a.nb_mp;
+    };
+    md0.load(mrow, E, 0, SL * j, SL, mws0);
     stamp(a, 1, 3);
     lds_barrier();
     if (tid < MLP_SLICE / 8) {

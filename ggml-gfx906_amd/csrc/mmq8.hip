@@ -659,36 +659,30 @@ __device__ __forceinline__ void q8_x_dma(__amdgpu_buffer_rsrc_t xr, uint32_t img
     }
 }
 
-// grid.x = n_rt * ksplit * n_tt (token tiles fastest; XCD-remapped when a multiple of 8),
-// grid.y = slices. TR weight rows x TT tokens per workgroup, TR / 16 waves of 64 rows x 32
-// tokens:
-//   TT = 64:  two K-groups of waves split every super-block (blocks 0-3 / 4-7), reduced through
-//             LDS at the end;
-//   TT = 128: every wave takes whole super-blocks (the weight stage serves twice the tokens).
-//   TR = 64 halves the workgroup (4 waves, ~70 KB of LDS) so that two run on one CU and their
-//   load / compute phases interleave.
-template <int T, int TT, int TR, bool MOE = false>
-__global__ __launch_bounds__(4 * TR) void mmq8_kernel(const MmArgs a, const uint8_t *__restrict__ ximg, int n_tt,
-                                                      int ksplit, int sb_per, uint32_t w_extent,
-                                                      float *__restrict__ part, int xcd_remap, const Moe8 moe) {
+// stream-K state (SK kernels): per-tile arrival counters (zero between launches: the second
+// arrival re-arms its tile's), two partial slots per tile, the tile count of one slice
+struct StreamK {
+    int *cnt;
+    float *part;
+    int n_tiles;
+};
+constexpr int MMQ8_SK_WGS = 256;   // stream-K grid: one workgroup per CU (the 128-row tiles hold ~136 KB of LDS)
+
+// one (row tile, token tile, super-block range) of mmq8_kernel: stages, steps, K-group
+// reduction and the epilogue (plain store, the 2-way split-K atomic add, the split-K partial, or
+// the stream-K hand-off)
+template <int T, int TT, int TR, bool MOE, bool SK>
+__device__ __forceinline__ void mmq8_job(const MmArgs &a, const uint8_t *__restrict__ ximg, int n_tt, uint32_t w_extent,
+                                         float *__restrict__ part, int xcd_remap, const Moe8 &moe, const StreamK &sk,
+                                         uint8_t *lds, int rt, int tt, int sb0, int sb1, int ksplit, int ks, int slice) {
     constexpr int NW = TR / 16;                    // waves
     constexpr int WB = wi_bytes<TR>();
     constexpr int XB = ximg_bytes<T>();
     constexpr int NI = TT / Q8_TOK;                // activation images per stage
     constexpr int N_XS = (TT == 64 && TR == 128) ? 3 : 2;   // activation stage ring
     constexpr int DX = N_XS - 1;                   // activation DMA distance (super-blocks ahead)
-    // LDS: two weight stages (decoded one super-block ahead from registers loaded two ahead) and
-    // the activation ring (LDS-DMA DX super-blocks ahead)
-    __shared__ __align__(16) uint8_t lds[2 * WB + N_XS * NI * XB];
     uint8_t *const Xs = lds + 2 * WB;
     const int n_sb = (a.K + Q8_QK - 1) / Q8_QK;
-    int v = blockIdx.x;
-    if (xcd_remap & 1) v = (v & 7) * (int)(gridDim.x >> 3) + (v >> 3);
-    const int tt = v % n_tt;
-    v /= n_tt;
-    const int ks = v % ksplit, rt = v / ksplit;
-    const int sb0 = ks * sb_per, sb1 = min(n_sb, sb0 + sb_per);
-    const int slice = blockIdx.y;   // MOE: the token tile
     const int i12 = slice % a.ne12, i13 = slice / a.ne12;
     int ex = 0, q0 = 0, n_tok = a.M;   // MOE: expert, first sorted pair, pairs of the tile
     if constexpr (MOE)
@@ -778,20 +772,68 @@ __global__ __launch_bounds__(4 * TR) void mmq8_kernel(const MmArgs a, const uint
             }
         }
         lds_barrier();
-        if (kg == 1) return;
+        if (kg == 0) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            acc0[i] += red[((wl * 2 + 0) * 16 + i) * 64 + lane];
-            acc1[i] += red[((wl * 2 + 1) * 16 + i) * 64 + lane];
+            for (int i = 0; i < 16; ++i) {
+                acc0[i] += red[((wl * 2 + 0) * 16 + i) * 64 + lane];
+                acc1[i] += red[((wl * 2 + 1) * 16 + i) * 64 + lane];
+            }
         }
     }
+    const bool out_wave = NKG == 1 || kg == 0;   // the waves holding the sums
+    if constexpr (SK) {
+        // a tile shared by two workgroups: each stores its partial write-through (sc1, one
+        // 256-B wave row per register), drains, and one lane adds to the tile's counter (agent
+        // scope); the workgroup whose add returns 1 came second: it loads the other partial with
+        // sc1 loads, adds it (two operands: the same sum in either order) and stores dst; it
+        // also re-arms the counter (MI355X_MICROARCH.md inter-workgroup visibility, first form)
+        const int n_sb2 = (a.K + Q8_QK - 1) / Q8_QK;
+        if (sb0 != 0 || sb1 != n_sb2) {
+            const int tile = rt * n_tt + tt;
+            const int me = sb0 == 0 ? 0 : 1;
+            constexpr int OW = NW / NKG;           // output waves
+            const int ow = NKG == 1 ? wave : wave % OW;
+            auto slot = [&](int who) {
+                return reinterpret_cast<uint32_t *>(sk.part) + (((int64_t)tile * 2 + who) * OW + ow) * 32 * 64;
+            };
+            if (out_wave) {
+                // (f32 values, no bit_cast: ROCm 7.2's clang lowers __builtin_bit_cast of an
+                // ext_vector element, acc0[i], to element 0 for every i, or to an undefined value:
+                // scripts/bitcast_vec_elem.hip)
+                float *mine = reinterpret_cast<float *>(slot(me));
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float v0 = acc0[i], v1 = acc1[i];
+                    __hip_atomic_store(mine + i * 64 + lane, v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(mine + (16 + i) * 64 + lane, v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+            __shared__ int sk_order;
+            lds_barrier();
+            if (threadIdx.x == 0)
+                sk_order = __hip_atomic_fetch_add(sk.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lds_barrier();
+            if (sk_order == 0) return;             // (uniform) the other half finishes the tile
+            if (out_wave) {
+                const float *other = reinterpret_cast<const float *>(slot(me ^ 1));
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    acc0[i] += __hip_atomic_load(other + i * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    acc1[i] += __hip_atomic_load(other + (16 + i) * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            if (threadIdx.x == 0) __hip_atomic_store(sk.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (!out_wave) return;
     const int r = lane & 31, hl = lane >> 5;
     const int tok0 = tt * TT + 32 * tg + 4 * hl;
     const int rowA = rt * TR + 64 * rg + r, rowB = rowA + 32;
     uint8_t *dbase;
     int64_t ldd;
-    const bool atomic = (xcd_remap & 4) != 0;   // 2-way split-K: both halves add into dst (zeroed)
-    if (ksplit > 1 && !atomic) {   // part[ks][slice][token][row]
+    const bool atomic = !SK && (xcd_remap & 4) != 0;   // 2-way split-K: both halves add into dst (zeroed)
+    if (!SK && ksplit > 1 && !atomic) {   // part[ks][slice][token][row]
         dbase = reinterpret_cast<uint8_t *>(part + ((int64_t)ks * gridDim.y + slice) * a.M * a.N);
         ldd = (int64_t)a.N * 4;
     } else {
@@ -819,6 +861,56 @@ __global__ __launch_bounds__(4 * TR) void mmq8_kernel(const MmArgs a, const uint
             if (rowB < a.N) drow[rowB] = acc1[i];
         }
     }
+}
+
+// grid.x = n_rt * ksplit * n_tt (token tiles fastest; XCD-remapped when a multiple of 8),
+// grid.y = slices. TR weight rows x TT tokens per workgroup, TR / 16 waves of 64 rows x 32
+// tokens:
+//   TT = 64:  two K-groups of waves split every super-block (blocks 0-3 / 4-7), reduced through
+//             LDS at the end;
+//   TT = 128: every wave takes whole super-blocks (the weight stage serves twice the tokens).
+//   TR = 64 halves the workgroup (4 waves, ~70 KB of LDS) so that two run on one CU and their
+//   load / compute phases interleave.
+// SK (stream-K, the reference's CDNA decomposition, src/ggml-cuda/mmq.cu:115 / mmq.cuh:3374):
+// grid.x workgroups split the (tile, super-block) units evenly, a tile's two halves meet
+// through a write-through partial and a counter (mmq8_job).
+template <int T, int TT, int TR, bool MOE = false, bool SK = false>
+__global__ __launch_bounds__(4 * TR) void mmq8_kernel(const MmArgs a, const uint8_t *__restrict__ ximg, int n_tt,
+                                                      int ksplit, int sb_per, uint32_t w_extent,
+                                                      float *__restrict__ part, int xcd_remap, const Moe8 moe,
+                                                      const StreamK sk) {
+    constexpr int WB = wi_bytes<TR>();
+    constexpr int XB = ximg_bytes<T>();
+    constexpr int NI = TT / Q8_TOK;                // activation images per stage
+    constexpr int N_XS = (TT == 64 && TR == 128) ? 3 : 2;   // activation stage ring
+    // LDS: two weight stages (decoded one super-block ahead from registers loaded two ahead) and
+    // the activation ring (LDS-DMA DX super-blocks ahead)
+    __shared__ __align__(16) uint8_t lds[2 * WB + N_XS * NI * XB];
+    const int n_sb = (a.K + Q8_QK - 1) / Q8_QK;
+    int v = blockIdx.x;
+    if (xcd_remap & 1) v = (v & 7) * (int)(gridDim.x >> 3) + (v >> 3);
+    const int slice = blockIdx.y;   // MOE: the token tile
+    if constexpr (SK) {
+        // stream-K: this workgroup's share [u0, u1) of the (tile, super-block) units, tiles in
+        // (row tile, token tile) order, token tiles fastest (neighbours share weights and, after
+        // the XCD remap, an L2); at most two workgroups share a tile (host: units per workgroup
+        // >= super-blocks per tile)
+        const int64_t U = (int64_t)sk.n_tiles * n_sb;
+        const int u0 = (int)((int64_t)v * U / gridDim.x), u1 = (int)((int64_t)(v + 1) * U / gridDim.x);
+        for (int u = u0; u < u1;) {
+            const int tile = u / n_sb, k0 = u - tile * n_sb, k1 = min(n_sb, k0 + (u1 - u));
+            mmq8_job<T, TT, TR, MOE, SK>(a, ximg, n_tt, w_extent, part, xcd_remap, moe, sk, lds, tile / n_tt, tile % n_tt,
+                                         k0, k1, 1, 0, slice);
+            u += k1 - k0;
+            lds_barrier();   // (the next job's stages overwrite the reduction / stage LDS)
+        }
+        return;
+    }
+    const int tt = v % n_tt;
+    v /= n_tt;
+    const int ks = v % ksplit, rt = v / ksplit;
+    const int sb0 = ks * sb_per, sb1 = min(n_sb, sb0 + sb_per);
+    mmq8_job<T, TT, TR, MOE, SK>(a, ximg, n_tt, w_extent, part, xcd_remap, moe, sk, lds, rt, tt, sb0, sb1, ksplit, ks, slice);
 }
 
 // dst[slice][token][row] = sum over s of part[s][slice][token][row], in s order
@@ -1323,7 +1415,7 @@ bool mmq8_images_fit(int type, const MmArgs &a) {
 
 template <int T>
 static void launch8(const MmArgs &a, uint8_t *ximg, int tr_rows, int tt_tok, int n_tt, int slices, int ksplit,
-                    int sb_per, float *part, bool atomic, hipStream_t st) {
+                    int sb_per, float *part, bool atomic, const StreamK &sk, hipStream_t st) {
     const int n_sb = (a.K + Q8_QK - 1) / Q8_QK;
     const int n_img = n_tt * (tt_tok / Q8_TOK);   // 64-token images per slice (tokens past M: zeros)
     hipLaunchKernelGGL(mmq8_quant_x<T>, dim3((unsigned)(n_img * (Q8_TOK / 4) * n_sb), slices), dim3(256), 0, st, a, ximg,
@@ -1331,12 +1423,22 @@ static void launch8(const MmArgs &a, uint8_t *ximg, int tr_rows, int tt_tok, int
     const int64_t row_b = (int64_t)a.K / QT<T>::blck * QT<T>::bytes;
     const uint32_t w_extent = (uint32_t)((int64_t)(a.N - 1) * a.nb01 + row_b);   // (the kernel rounds it up)
     const int n_rt = (a.N + tr_rows - 1) / tr_rows;
+    if (sk.cnt != nullptr) {   // stream-K: one workgroup per CU, the units split evenly
+        const unsigned gx = MMQ8_SK_WGS;
+        if (tt_tok == 128)
+            hipLaunchKernelGGL((mmq8_kernel<T, 128, 128, false, true>), dim3(gx, 1), dim3(512), 0, st, a, (const uint8_t *)ximg,
+                               n_tt, 1, n_sb, w_extent, part, 1, Moe8{}, sk);
+        else
+            hipLaunchKernelGGL((mmq8_kernel<T, 64, 128, false, true>), dim3(gx, 1), dim3(512), 0, st, a, (const uint8_t *)ximg,
+                               n_tt, 1, n_sb, w_extent, part, 1, Moe8{}, sk);
+        return;
+    }
     const unsigned gx = (unsigned)(n_rt * ksplit * n_tt);
     const int remap = ((gx % 8 == 0) ? 1 : 0) | (atomic ? 4 : 0);
     const dim3 grid(gx, slices);
 #define Q8_LAUNCH(TTv, TRv)                                                                                          \
     hipLaunchKernelGGL((mmq8_kernel<T, TTv, TRv>), grid, dim3(4 * TRv), 0, st, a, (const uint8_t *)ximg, n_tt, ksplit, \
-                       sb_per, w_extent, part, remap, Moe8{})
+                       sb_per, w_extent, part, remap, Moe8{}, StreamK{})
     if (tt_tok == 128) Q8_LAUNCH(128, 128);
     else if (tr_rows == 128) Q8_LAUNCH(64, 128);
     else Q8_LAUNCH(64, 64);   // measured slower than 128 rows at every shape; kept for A/B
@@ -1380,16 +1482,34 @@ hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scrat
     // exactly two halves add into dst atomically (order-independent); more go through part[]
     static const bool no_atomic = getenv("GGML_MI355X_MMQ8_ATOMIC") && atoi(getenv("GGML_MI355X_MMQ8_ATOMIC")) == 0;
     const bool atomic = ksplit == 2 && !no_atomic;
-    const size_t part_bytes = ksplit > 1 && !atomic ? (size_t)ksplit * slices * a.M * a.N * sizeof(float) : 0;
+    size_t part_bytes = ksplit > 1 && !atomic ? (size_t)ksplit * slices * a.M * a.N * sizeof(float) : 0;
+    // stream-K (one slice, no split-K, 128-row tiles) where whole rounds of one tile per CU would
+    // leave the last round mostly idle: e.g. 4096 x 11008 x 512, 344 128-token tiles = 1.34
+    // rounds. A tile's units are then split between at most two workgroups (units per
+    // workgroup >= super-blocks per tile, since tiles > workgroups). GGML_MI355X_MMQ8_SK: 0 never
+    // (A/B), 1 whenever the tiles outnumber the workgroups
+    const char *sk_env = getenv("GGML_MI355X_MMQ8_SK");   // per call: tests switch it
+    const int64_t rounds = (tiles + MMQ8_SK_WGS - 1) / MMQ8_SK_WGS;
+    bool use_sk = slices == 1 && ksplit == 1 && tr_rows == 128 && tiles > MMQ8_SK_WGS && tiles <= Scratch::COUNTERS &&
+                  (double)tiles / (double)(rounds * MMQ8_SK_WGS) < 0.85;
+    if (sk_env) use_sk = atoi(sk_env) == 1 && slices == 1 && ksplit == 1 && tr_rows == 128 && tiles > MMQ8_SK_WGS &&
+                         tiles <= Scratch::COUNTERS;
+    StreamK sk{};
+    if (use_sk) {
+        sk.cnt = scratch.counters(st);
+        sk.n_tiles = (int)tiles;
+        if (sk.cnt) part_bytes = (size_t)tiles * 2 * (tt_tok == 128 ? 8 : 4) * 32 * 64 * sizeof(float);
+    }
     uint8_t *buf = static_cast<uint8_t *>(scratch.get(img_bytes + part_bytes, st));
     if (!buf) return hipErrorOutOfMemory;
     float *part = reinterpret_cast<float *>(buf + img_bytes);
+    sk.part = part;
     switch (type) {
-        case T_Q4_0: launch8<T_Q4_0>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, atomic, st); break;
-        case T_Q8_0: launch8<T_Q8_0>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, atomic, st); break;
-        case T_Q4_K: launch8<T_Q4_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, atomic, st); break;
-        case T_Q5_K: launch8<T_Q5_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, atomic, st); break;
-        case T_Q6_K: launch8<T_Q6_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, atomic, st); break;
+        case T_Q4_0: launch8<T_Q4_0>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, atomic, sk, st); break;
+        case T_Q8_0: launch8<T_Q8_0>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, atomic, sk, st); break;
+        case T_Q4_K: launch8<T_Q4_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, atomic, sk, st); break;
+        case T_Q5_K: launch8<T_Q5_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, atomic, sk, st); break;
+        case T_Q6_K: launch8<T_Q6_K>(a, buf, tr_rows, tt_tok, n_tt, slices, ksplit, sb_per, part, atomic, sk, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1463,7 +1583,7 @@ static void launch8_id(const MmArgs &a, uint8_t *ximg, int n_tiles, const Moe8 &
     const unsigned gx = (unsigned)((a.N + 127) / 128);
     const int remap = (gx % 8 == 0) ? 1 : 0;
     hipLaunchKernelGGL((mmq8_kernel<T, 64, 128, true>), dim3(gx, (unsigned)n_tiles), dim3(512), 0, st, a,
-                       (const uint8_t *)ximg, 1, 1, n_sb, w_extent, (float *)nullptr, remap, moe);
+                       (const uint8_t *)ximg, 1, 1, n_sb, w_extent, (float *)nullptr, remap, moe, StreamK{});
 }
 
 hipError_t mmq8_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch) {

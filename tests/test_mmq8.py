@@ -50,11 +50,13 @@ def exact(t, w, N, K, x, M_):
     return (x.reshape(M_, K).astype(np.float64) @ wd.T).astype(np.float64).ravel()
 
 
-def case(mm, t, N, M_, K, seed=1, ksplit=None, tt=None):
+def case(mm, t, N, M_, K, seed=1, ksplit=None, tt=None, sk=None, ret_got=False):
     if ksplit is not None:
         os.environ["GGML_MI355X_MMQ8_KSPLIT"] = str(ksplit)
     if tt is not None:
         os.environ["GGML_MI355X_MMQ8_TT"] = str(tt)
+    if sk is not None:
+        os.environ["GGML_MI355X_MMQ8_SK"] = str(sk)
     try:
         w = qref.quantize(t, qref.fill_uniform(N * K, seed), n_per_row=K)
         x = qref.fill_uniform(M_ * K, seed + 1)
@@ -64,6 +66,7 @@ def case(mm, t, N, M_, K, seed=1, ksplit=None, tt=None):
     finally:
         os.environ.pop("GGML_MI355X_MMQ8_KSPLIT", None)
         os.environ.pop("GGML_MI355X_MMQ8_TT", None)
+        os.environ.pop("GGML_MI355X_MMQ8_SK", None)
     assert np.all(np.isfinite(got))
     want = G.oracle_mul_mat(a, b, [N, M_, 1, 1])
     err = qref.nmse(got, want)
@@ -71,7 +74,7 @@ def case(mm, t, N, M_, K, seed=1, ksplit=None, tt=None):
     ex = exact(t, w, N, K, x, M_)
     err_x = float(np.sum((got - ex) ** 2) / np.sum(ex ** 2))
     assert err_x <= 2e-4, f"{qref.NAMES[t]} N={N} M={M_} K={K}: nmse vs exact {err_x:.3e}"
-    return err
+    return got if ret_got else err
 
 
 @pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])
@@ -89,6 +92,28 @@ def test_mmq8_ksplit(mm, t, ksplit):
     """split-K over workgroups (fixed-order reduce), with a super-block count the splits do not
     divide evenly"""
     case(mm, t, 192, 96, 256 * 5, seed=7, ksplit=ksplit)
+
+
+@pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])
+@pytest.mark.parametrize("shape", [(4224, 1024, 768, None), (8192, 640, 512, None), (4160, 1152, 1024, None),
+                                   (8320, 520, 256, None), (4224, 1024, 768, 64)],
+                         ids=lambda s: "x".join(map(str, s[:3])) + (f"_tt{s[3]}" if s[3] else ""))
+def test_mmq8_stream_k(mm, t, shape, force_i8):
+    """stream-K (GGML_MI355X_MMQ8_SK=1): more 128-row tiles than the 256 workgroups, so the
+    (tile, super-block) units split unevenly and tiles are finished by a second workgroup through
+    the write-through partial + counter hand-off; against the oracle, bit-identical on a second
+    run (two operands per tile: the order of arrival does not change the sum) and within the
+    fp32 scale-sum order of the plain tiles (SK=0)"""
+    if force_i8 == "repack":
+        pytest.skip("stream-K is the in-place tile's")
+    N, M_, K, tt = shape
+    if qref.BLCK[t] == 256 and K % 256:
+        K = 768
+    g1 = case(mm, t, N, M_, K, seed=13, sk=1, tt=tt, ret_got=True)
+    g2 = case(mm, t, N, M_, K, seed=13, sk=1, tt=tt, ret_got=True)
+    assert np.array_equal(g1.view(np.uint32), g2.view(np.uint32)), "stream-K result not repeatable"
+    g0 = case(mm, t, N, M_, K, seed=13, sk=0, tt=tt, ret_got=True)
+    assert qref.nmse(g1, g0) <= 1e-9
 
 
 @pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])
