@@ -28,6 +28,8 @@ bool mmvq_has_nc(int nc);
 int mmvq_max_k_for_nc(int nc);
 bool mmvq_bigk(int K);
 hipError_t mmvq_ring_launch(int type, const MmArgs &a, int nc, int rpw, uint8_t *img, hipStream_t st);
+hipError_t mmvq_mma_launch(int type, const MmArgs &a, uint8_t *img, hipStream_t st);
+size_t mmvq_mma_img_bytes(int type, const MmArgs &a);
 size_t mmvq_ring_img_bytes(const MmArgs &a, int nc);
 hipError_t dequant_launch(int type, const void *src, float *dst, int64_t n, hipStream_t st);
 struct RowsArgs {
@@ -179,10 +181,28 @@ static int ring_pre_min() {
     return v == 0 ? 1 << 30 : v == 2 ? 2 : 4;
 }
 
+// the int8 MFMA mat-vec (mmvq_mma.hip: the columns are the N side of a 16 x 16 tile, so the
+// weights are read once and the per-column cost is one MFMA column), for 2..8 columns.
+// GGML_MI355X_MMA=N: from N columns on; unset or 0: the per-column VALU kernels (the MFMA form
+// does not beat them yet: profiles/r05_mma_matvec_ab.txt)
+static int mma_min_cols() {
+    const char *e = getenv("GGML_MI355X_MMA");   // per call: tests switch it
+    const int v = e ? atoi(e) : 0;
+    return v <= 0 ? 1 << 30 : std::max(v, 1);
+}
+
 // mat-vec over columns [c0, c0 + ncols) in groups of at most 8 (scratch: the caller holds its
 // mutex; nullptr = no pre-quantized images)
 static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st, Scratch *scratch = nullptr) {
     const int rpw = pick_rpw(type, (int64_t)m.N * m.ne12 * m.ne13);
+    if (scratch != nullptr && ncols >= mma_min_cols() && ncols <= 8) {
+        MmArgs g = m;
+        g.x = m.x + (int64_t)c0 * m.nb11;
+        g.dst = m.dst + (int64_t)c0 * m.nb1;
+        g.M = ncols;
+        // (nullptr inside a capture that would grow the scratch: the kernels below take it)
+        if (uint8_t *img = static_cast<uint8_t *>(scratch->get(mmvq_mma_img_bytes(type, g), st))) return mmvq_mma_launch(type, g, img, st);
+    }
     while (ncols > 0) {
         MmArgs g = m;
         g.x = m.x + (int64_t)c0 * m.nb11;

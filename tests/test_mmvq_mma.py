@@ -1,0 +1,120 @@
+"""GPU parity of the int8-MFMA mat-vec for 2..8 src1 columns (csrc/mmvq_mma.hip).
+
+The path quantizes every src1 column per 32-block exactly as the VALU mat-vec kernels do
+(d = amax/127, round-to-nearest-even: mmvq_impl.h xblock_store) and sums the integer block dots
+in int32 on v_mfma_i32_16x16x32_i8, so against the VALU path (GGML_MI355X_MMA=0, the same
+activation bytes) only the fp32 order of the per-block scale sums differs: NMSE <= 1e-10. Against
+the CPU oracle (ggml-cpu's vec_dot on its own src1 quantization) the reference's MUL_MAT bar
+5e-4 (tests/test-backend-ops.cpp:3106-3108) applies, as for every mat-vec case.
+
+Covered: all five types; 2, 3, 5 and 8 columns; ragged rows (N % 16 != 0); Q4_0 / Q8_0 K that
+ends inside a 128-step (K % 128 = 32, 64, 96), K-quants at odd super-block counts; the reference's
+perf shapes (K = 14336, bs 2..8); broadcast batch slices (ne12 = 2 * ne02); a Q6_K row stride
+that leaves every other super-block 2-byte aligned; the wave-count override (4 / 8 / 16 waves).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import golden_cases as G
+import qref
+from test_gpu_parity import mm, run_mul_mat  # noqa: F401  (fixture)
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+TYPES = [qref.Q4_0, qref.Q8_0, qref.Q4_K, qref.Q5_K, qref.Q6_K]
+
+
+def operands(t, N, M_, K, seed, ne2=(1, 1)):
+    """src0 [K, N, ne02] and src1 [K, M, ne12] (ne12 = 2 * ne02: broadcast)"""
+    ne02, ne12 = ne2
+    w = qref.quantize(t, qref.fill_uniform(N * K * ne02, seed), n_per_row=K)
+    x = qref.fill_uniform(M_ * K * ne12, seed + 1)
+    a = G.Operand(t, w, [K, N, ne02, 1], qref.contiguous_nb(t, [K, N, ne02, 1]))
+    b = G.Operand(qref.F32, x, [K, M_, ne12, 1], qref.contiguous_nb(qref.F32, [K, M_, ne12, 1]))
+    return a, b, [N, M_, ne12, 1]
+
+
+def run_with(mm, a, b, out_ne, env):
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return run_mul_mat(mm, a, b, out_ne)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def check(mm, t, N, M_, K, seed=3, ne2=(1, 1), ks=None, oracle=True):
+    a, b, out_ne = operands(t, N, M_, K, seed, ne2)
+    env = {"GGML_MI355X_MMA": 2}
+    if ks is not None:
+        env["GGML_MI355X_MMA_KS"] = ks
+    got = run_with(mm, a, b, out_ne, env)
+    assert np.all(np.isfinite(got))
+    valu = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 0})
+    e_valu = qref.nmse(got, valu)
+    assert e_valu <= 1e-10, f"{qref.NAMES[t]} N={N} M={M_} K={K}: nmse vs the VALU mat-vec {e_valu:.3e}"
+    if oracle:
+        e = qref.nmse(got, G.oracle_mul_mat(a, b, out_ne, threads=16))
+        assert e <= 5e-4, f"{qref.NAMES[t]} N={N} M={M_} K={K}: nmse vs oracle {e:.3e}"
+    return got
+
+
+@pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])
+@pytest.mark.parametrize("M_", [2, 3, 5, 8])
+def test_mma_columns(mm, t, M_):
+    K = 512 if qref.BLCK[t] == 256 else 448   # (Q4_0 / Q8_0: 3.5 steps of 128)
+    check(mm, t, 200, M_, K)
+
+
+@pytest.mark.parametrize("t", [qref.Q4_0, qref.Q8_0], ids=lambda t: qref.NAMES[t])
+@pytest.mark.parametrize("K", [32, 64, 96, 160, 4160])
+def test_mma_partial_step(mm, t, K):
+    """the last 128-step holds 1..3 live blocks: activation codes past K are zero, the weight
+    loads clamp to the row's last block"""
+    check(mm, t, 37, 4, K)
+
+
+@pytest.mark.parametrize("t", [qref.Q4_K, qref.Q5_K, qref.Q6_K], ids=lambda t: qref.NAMES[t])
+@pytest.mark.parametrize("K", [256, 768, 2304])
+def test_mma_kquant_k(mm, t, K):
+    """odd super-block counts (the steps are half super-blocks: odd step pairs per wave)"""
+    check(mm, t, 48, 6, K)
+
+
+@pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])
+@pytest.mark.parametrize("M_", [2, 8])
+def test_mma_reference_perf_shape(mm, t, M_):
+    """test-backend-ops perf's mat-vec shape, K = 14336, N = 4096, against the VALU path (the
+    oracle at this size takes minutes; the smaller cases above hold the oracle check)"""
+    a, b, out_ne = operands(t, 4096, M_, 14336, 7)
+    got = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 2})
+    valu = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 0})
+    assert np.all(np.isfinite(got))
+    assert qref.nmse(got, valu) <= 1e-10
+
+
+@pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])
+def test_mma_broadcast_slices(mm, t):
+    check(mm, t, 64, 3, 256 if qref.BLCK[t] == 256 else 128, ne2=(2, 4))
+
+
+@pytest.mark.parametrize("ks", [4, 8, 16])
+@pytest.mark.parametrize("t", [qref.Q4_0, qref.Q4_K, qref.Q6_K], ids=lambda t: qref.NAMES[t])
+def test_mma_wave_counts(mm, t, ks):
+    """the K split over 4, 8 or 16 waves (Q6_K caps at 8) sums in a fixed order: the same bits
+    whatever the split, up to the fp32 order of the partial sums"""
+    check(mm, t, 96, 5, 4096, ks=ks, oracle=False)
+
+
+def test_mma_q6k_odd_row_alignment(mm):
+    """Q6_K rows of 3 super-blocks (630 B): every other row starts 2-byte aligned, so the
+    windows of the fragment loads are funnel-shifted by 2 on those rows"""
+    check(mm, qref.Q6_K, 33, 7, 768)
