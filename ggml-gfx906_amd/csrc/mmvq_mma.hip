@@ -46,24 +46,30 @@ template <int T> __device__ __forceinline__ int mma_elem(int g, int i) {
     else return 8 * g + i;
 }
 
-// grid (steps, slices), TOK * 16 threads: thread (t, j, g) quantizes k-group g of block j of
-// column t; the quad of a block shares amax and sum(q) through DPP
-template <int T, int TOK>
-__global__ __launch_bounds__(TOK * 16) void mma_prequant(const MmArgs a, uint8_t *__restrict__ img) {
-    const int s = blockIdx.x, z = blockIdx.y;
-    const int i12 = z % a.ne12, i13 = z / a.ne12;
-    const int g = threadIdx.x & 3, j = (threadIdx.x >> 2) & 3, t = threadIdx.x >> 4;
+// k-group g of block j of step s of column t (zeros past K or M), loaded, then quantized into
+// its record `rec` (the record of (s, t)); the 4 threads of a block (g = 0..3) are consecutive
+// lanes and share amax and sum(q) through DPP. The arithmetic of mmvq_impl.h's xblock_store,
+// bit for bit.
+// (the loads only: the zeroing past K / M is applied by mma_quant once every load of the batch
+// is issued; a select right behind a load makes the compiler wait for it before the next load)
+template <int T, bool XA>
+__device__ __forceinline__ void mma_xload(const MmArgs &a, const float *col, int s, int j, int g, float (&v)[8]) {
     const int kb = s * MMA_STEP_K + 32 * j;   // first element of the block
-    const float *col = reinterpret_cast<const float *>(a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13 +
-                                                       (int64_t)min(t, a.M - 1) * a.nb11);
-    float v[8];
+    if constexpr (XA) {   // rows 16-B aligned, K % 4 == 0 (runs of 4 clamped as a whole)
+        const float4 lo = *reinterpret_cast<const float4 *>(col + min(kb + mma_elem<T>(g, 0), a.K - 4));
+        const float4 hi = *reinterpret_cast<const float4 *>(col + min(kb + mma_elem<T>(g, 4), a.K - 4));
+        v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+        v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    } else {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int k = kb + mma_elem<T>(g, i);
-        const float x = col[min(k, a.K - 1)];
-        v[i] = (k < a.K && t < a.M) ? x : 0.f;
+        for (int i = 0; i < 8; ++i) v[i] = col[min(kb + mma_elem<T>(g, i), a.K - 1)];
     }
-    // the quantization of mmvq_impl.h's xblock_store, bit for bit
+}
+template <int T, bool SX>
+__device__ __forceinline__ void mma_quant(const MmArgs &a, float (&v)[8], int s, int j, int t, int g, uint8_t *rec, bool store) {
+    const int kb = s * MMA_STEP_K + 32 * j;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (kb + mma_elem<T>(g, i) < a.K && t < a.M) ? v[i] : 0.f;
     float amax = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[i]));
@@ -77,16 +83,18 @@ __global__ __launch_bounds__(TOK * 16) void mma_prequant(const MmArgs a, uint8_t
     for (int i = 0; i < 8; ++i) b[i] = __float_as_uint(__builtin_fmaf(v[i], id, MAGIC));
     const uint32_t w0 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(b[3], b[2], 0x0c0c0400u), __builtin_amdgcn_perm(b[1], b[0], 0x0c0c0400u), 0x05040100u);
     const uint32_t w1 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(b[7], b[6], 0x0c0c0400u), __builtin_amdgcn_perm(b[5], b[4], 0x0c0c0400u), 0x05040100u);
-    const int qs = (int)__builtin_amdgcn_udot4(w0, 0x01010101u, __builtin_amdgcn_udot4(w1, 0x01010101u, 0u, false), false) - 1024;
-    float fs = (float)qs;
-    fs += dpp_f<DPP_XOR1>(fs);
-    fs += dpp_f<DPP_XOR2>(fs);
-    uint8_t *rec = img + ((int64_t)z * gridDim.x + s) * mma_step_bytes<T, TOK>() + t * mma_rec_bytes<T>();
-    *reinterpret_cast<uint2 *>(rec + g * 32 + j * 8) = make_uint2(w0 ^ 0x80808080u, w1 ^ 0x80808080u);
-    if (g == 0) {
+    if (store) *reinterpret_cast<uint2 *>(rec + g * 32 + j * 8) = make_uint2(w0 ^ 0x80808080u, w1 ^ 0x80808080u);
+    float fs = 0.f;
+    if constexpr (SX) {
+        const int qs = (int)__builtin_amdgcn_udot4(w0, 0x01010101u, __builtin_amdgcn_udot4(w1, 0x01010101u, 0u, false), false) - 1024;
+        fs = (float)qs;
+        fs += dpp_f<DPP_XOR1>(fs);
+        fs += dpp_f<DPP_XOR2>(fs);
+    }
+    if (g == 0 && store) {
         float *ds = reinterpret_cast<float *>(rec + 128);
         ds[j] = d;
-        if constexpr (mma_rec_bytes<T>() == 160) ds[4 + j] = d * fs;
+        if constexpr (SX) ds[4 + j] = d * fs;
     }
 }
 
@@ -324,87 +332,108 @@ template <> struct MmaW<T_Q6_K> {
 };
 
 // ------------------------------------------------------------------------------------------
-// weight sets per wave (DEPTH - 1 steps in flight). XL (the slice's activation image copied to
-// LDS once per workgroup): the sets hold only weights, so they go deep; otherwise the sets hold
-// the activation fragments too, 2 deep.
-template <int T, bool XL> __host__ __device__ constexpr int mma_depth() {
-    if constexpr (!XL) return 2;
-    else return T == T_Q4_0 ? 6 : (T == T_Q8_0 || T == T_Q4_K) ? 4 : T == T_Q5_K ? 3 : 2;
+// weight sets per wave (DEPTH - 1 steps in flight; the activations come from LDS): as deep as
+// the register budget of 16 waves per CU allows without spills
+template <int T> __host__ __device__ constexpr int mma_depth() {
+    return T == T_Q4_0 ? 5 : (T == T_Q8_0 || T == T_Q4_K) ? 3 : 2;
 }
 
-// Workgroup = KS waves on one 16-row tile at a time, each wave a contiguous K range of it
-// (persistent over tiles when XL: the image is copied once); the row scales reach the output
-// lanes through a per-wave LDS slot; the K ranges are summed through LDS in a fixed order.
-template <int T, int TOK, int KS, bool XL>
-__global__ __launch_bounds__(KS * WAVE) void mmvq_mma_kernel(const MmArgs a, const uint8_t *__restrict__ img, int n_steps,
-                                                           int n_tiles) {
+// One launch, no pre-pass. Workgroup (row group rg, K part kp, slice z) = 8 waves, wave w on the
+// 16-row tile 8 rg + w, all waves over the same K part:
+//  1. the workgroup quantizes its K part of the src1 columns into LDS (records of mma_quant),
+//     while the first weight steps of every wave are already in flight;
+//  2. each wave streams its tile's weights over the K part, DEPTH - 1 steps ahead in registers,
+//     one MFMA per 32-block against the LDS records;
+//  3. with one K part the wave stores its tile; otherwise it stores a partial (write-through
+//     sc1 stores), the workgroup adds one to its row group's counter (agent scope) and the
+//     workgroup that arrives last sums the parts in K order and stores dst
+//     (MI355X_MICROARCH.md inter-workgroup visibility, the counter row), then re-arms it.
+template <int D, typename F, int... Is>
+__device__ __forceinline__ void mma_run_steps(F &&f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is % D>{}, Is), ...);
+}
+
+template <int T, int TOK, int D, int NSTEP, bool XA>
+__global__ __launch_bounds__(8 * WAVE) void mmvq_mma_kernel(const MmArgs a, int n_steps, int n_kp, float *__restrict__ part,
+                                                          int *__restrict__ cnt) {
     constexpr int NMF = MmaW<T>::NMF;
     constexpr int NSC = MmaW<T>::NSC;
     constexpr int RB = mma_rec_bytes<T>();
     constexpr int SB = mma_step_bytes<T, TOK>();
-    constexpr int D = mma_depth<T, XL>();
     constexpr bool SX = RB == 160;
-    extern __shared__ __align__(16) uint8_t xsm[];   // XL: n_steps * SB bytes
-    // per wave: the row scales of the step being finished, [row 16][4 j][NSC] floats; the K-split
-    // partial sums of the live lanes (column < TOK) [wave][g 4][t TOK][4]
-    __shared__ __align__(16) float wsc[KS][16 * 4 * NSC];
-    __shared__ __align__(16) float red[KS][4 * TOK * 4];
+    extern __shared__ __align__(16) uint8_t xsm[];   // the K part's records: steps * SB bytes
+    __shared__ __align__(16) float wsc[8][16 * 4 * NSC];
+    __shared__ int order;
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int r = lane & 15, g = lane >> 4;
-    const int z = blockIdx.y;
+    const int rg = blockIdx.x, kp = blockIdx.y, z = blockIdx.z;
     const int i12 = z % a.ne12, i13 = z / a.ne12;
-    const uint8_t *wmat = a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03;
+    const int k0 = kp * NSTEP, k1 = min(n_steps, k0 + NSTEP);   // this K part's steps (NSTEP per part)
+    const int tile = rg * 8 + wave;
+    const int row0 = tile * 16;
+    const uint8_t *wrow = a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03 +
+                          (int64_t)min(row0 + r, a.N - 1) * a.nb01;
     const int nblk = a.K / QT<T>::blck;
-    const uint8_t *xs = img + (int64_t)z * n_steps * SB;
     const int tl = r & (TOK - 1);   // this lane's column (lanes past TOK repeat a column)
-    const int s0 = (int)((int64_t)wave * n_steps / KS), s1 = (int)((int64_t)(wave + 1) * n_steps / KS);
-    const uint8_t *xsrc = XL ? xsm : xs;   // (generic pointer: global or LDS)
 
-    struct Xf {
-        uint4 c0, c1;   // codes of 4 blocks (8 B each)
-        float4 d, sx;   // d and d * sum(q) of the 4 blocks, this lane's column
-    };
-    auto read_x = [&](Xf &x, int s) __attribute__((always_inline)) {
-        if constexpr (XL) {
-            const uint8_t *rec = xsm + s * SB + tl * RB;
-            x.c0 = *reinterpret_cast<const uint4 *>(rec + g * 32);
-            x.c1 = *reinterpret_cast<const uint4 *>(rec + g * 32 + 16);
-            x.d = *reinterpret_cast<const float4 *>(rec + 128);
-            if constexpr (SX) x.sx = *reinterpret_cast<const float4 *>(rec + 144);
-        } else {
-            const uint8_t *rec = xs + (int64_t)s * SB + tl * RB;
-            x.c0 = *reinterpret_cast<const uint4 *>(rec + g * 32);
-            x.c1 = *reinterpret_cast<const uint4 *>(rec + g * 32 + 16);
-            x.d = *reinterpret_cast<const float4 *>(rec + 128);
-            if constexpr (SX) x.sx = *reinterpret_cast<const float4 *>(rec + 144);
+    // 1. weight prologue, then the K part's activations into LDS (16-B loads: the 8 values of a
+    // unit are two runs of 4 consecutive floats in either element order)
+    MmaW<T> F[D];
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) F[d].load(wrow, min(k0 + d, k1 - 1), g, nblk);
+    {
+        const float *xz = reinterpret_cast<const float *>(a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13);
+        const int units = (k1 - k0) * 4 * TOK * 4;   // (step, t, j, g), g fastest
+        constexpr int QU = 4;   // units per thread whose loads are issued together
+        for (int u0 = threadIdx.x; u0 < units; u0 += QU * 8 * WAVE) {
+            float v[QU][8];
+#pragma unroll
+            for (int q = 0; q < QU; ++q) {
+                const int u = min(u0 + q * 8 * WAVE, units - 1);
+                const int j = (u >> 2) & 3, t = (u >> 4) % TOK, sl = (u >> 4) / TOK;
+                const float *col = reinterpret_cast<const float *>(reinterpret_cast<const uint8_t *>(xz) + (int64_t)min(t, a.M - 1) * a.nb11);
+                mma_xload<T, XA>(a, col, k0 + sl, j, u & 3, v[q]);
+            }
+#pragma unroll
+            for (int q = 0; q < QU; ++q) {
+                // (units past the end, whole quads since units % 4 == 0, quantize the clamped
+                // repeat without storing it: a quad of repeats has the wrong amax)
+                const int u = min(u0 + q * 8 * WAVE, units - 1);
+                const int j = (u >> 2) & 3, t = (u >> 4) % TOK, sl = (u >> 4) / TOK;
+                mma_quant<T, SX>(a, v[q], k0 + sl, j, t, u & 3, xsm + sl * SB + t * RB, u0 + q * 8 * WAVE < units);
+            }
         }
-    };
-    (void)xsrc;
-    float acc[4];
-    auto compute = [&](MmaW<T> &w, Xf &x, float live) __attribute__((always_inline)) {
+    }
+    lds_barrier();
+
+    // 2. the weight stream: step s computes from set s % D while the loads of s + D - 1 go into
+    // the set step s - 1 used (clamped repeats past k1 - 1); the step count is padded to a
+    // multiple of D with repeats that add nothing (live = 0). The scheduling barriers keep each
+    // step's loads ahead of the previous step's arithmetic, pin() keeps that arithmetic behind.
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](MmaW<T> &w, int s, float live) __attribute__((always_inline)) {
         long A[NMF];
         w.frags(A);
-        pin(x.c0);
-        pin(x.c1);
-        pin(x.d);
-        if constexpr (SX) pin(x.sx);
-        const long xb[4] = {pack2(x.c0.x, x.c0.y), pack2(x.c0.z, x.c0.w), pack2(x.c1.x, x.c1.y), pack2(x.c1.z, x.c1.w)};
+        const uint8_t *rec = xsm + (s - k0) * SB + tl * RB;
+        const uint4 c0 = *reinterpret_cast<const uint4 *>(rec + g * 32);
+        const uint4 c1 = *reinterpret_cast<const uint4 *>(rec + g * 32 + 16);
+        const float4 xdv = *reinterpret_cast<const float4 *>(rec + 128);
+        float4 sxv = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (SX) sxv = *reinterpret_cast<const float4 *>(rec + 144);
+        const long xb[4] = {pack2(c0.x, c0.y), pack2(c0.z, c0.w), pack2(c1.x, c1.y), pack2(c1.z, c1.w)};
         i32x4_t R[NMF];
         const i32x4_t zero = {0, 0, 0, 0};
 #pragma unroll
         for (int m = 0; m < NMF; ++m) R[m] = __builtin_amdgcn_mfma_i32_16x16x32_i8(A[m], xb[NMF == 8 ? m >> 1 : m], zero, 0, 0, 0);
-        // publish this lane's row scales: [r][j = g][NSC]
+        // publish this lane's row scales [r][j = g][NSC]; read those of rows 4G + i (G = g)
         float o[NSC];
         if constexpr (NSC == 1) w.sc(o);
         else w.sc(o, g);
         float *ws = wsc[wave];
 #pragma unroll
         for (int k = 0; k < NSC; ++k) ws[(r * 4 + g) * NSC + k] = o[k];
-        // read the scales of rows 4G + i (G = g): 4 * NSC floats per row
-        const float xd[4] = {x.d.x, x.d.y, x.d.z, x.d.w};
-        // (the padding step's live = 0 is applied to its finished sums: a factor on the loaded
-        // scales would be hoisted next to their loads, and its wait would drain the prefetch)
+        const float xd[4] = {xdv.x, xdv.y, xdv.z, xdv.w};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             float c;
@@ -423,98 +452,71 @@ __global__ __launch_bounds__(KS * WAVE) void mmvq_mma_kernel(const MmArgs a, con
             } else {
                 const float4 lo = *reinterpret_cast<const float4 *>(rs), hi = *reinterpret_cast<const float4 *>(rs + 4);
                 // [j][sc, m]: lo = sc0 m0 sc1 m1, hi = sc2 m2 sc3 m3
-                const float sx[4] = {x.sx.x, x.sx.y, x.sx.z, x.sx.w};
-                c = (lo.x * (xd[0] * (float)R[0][i]) - lo.y * sx[0]) + (lo.z * (xd[1] * (float)R[1][i]) - lo.w * sx[1]) +
-                    (hi.x * (xd[2] * (float)R[2][i]) - hi.y * sx[2]) + (hi.z * (xd[3] * (float)R[3][i]) - hi.w * sx[3]);
+                c = (lo.x * (xd[0] * (float)R[0][i]) - lo.y * sxv.x) + (lo.z * (xd[1] * (float)R[1][i]) - lo.w * sxv.y) +
+                    (hi.x * (xd[2] * (float)R[2][i]) - hi.y * sxv.z) + (hi.z * (xd[3] * (float)R[3][i]) - hi.w * sxv.w);
             }
             acc[i] = __builtin_fmaf(live, c, acc[i]);
         }
     };
+    // straight-line: NSTEP steps (the last part's steps past k1 are clamped repeats with
+    // live = 0), no loop, so no register set crosses a back-edge (the copies the register
+    // allocator puts on a back-edge move sets whose loads are still in flight, and each copy
+    // waits for its load: one memory latency per step)
+    auto step = [&](auto k_c, int i) __attribute__((always_inline)) {
+        constexpr int k = decltype(k_c)::value;
+        const int s = k0 + i;
+        if (i + D - 1 < NSTEP) F[(k + D - 1) % D].load(wrow, min(s + D - 1, k1 - 1), g, nblk);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(F[k], min(s, k1 - 1), s < k1 ? 1.f : 0.f);
+    };
+    mma_run_steps<D>(step, std::make_integer_sequence<int, NSTEP>{});
 
-    bool copied = !XL;
-    for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-        const int row0 = tile * 16;
-        const uint8_t *wrow = wmat + (int64_t)min(row0 + r, a.N - 1) * a.nb01;
+    // 3. store (live lanes: column t < TOK, rows 4G + i)
+    const bool live_lane = r < TOK;
+    float *dcol = reinterpret_cast<float *>(a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3 + (int64_t)r * a.nb1);
+    if (n_kp == 1) {
+        if (live_lane && r < a.M)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i] = 0.f;
-        // DEPTH - 1 steps in flight per wave: step s computes from set s % DEPTH while the loads
-        // of s + DEPTH - 1 go into the set step s - 1 used (clamped repeats past s1 - 1). A CU's
-        // whole weight stream is the steps its waves hold in flight (a wave owns a few steps of
-        // ~1 KiB each), so the depth sets the bandwidth. The step count is padded to a multiple
-        // of DEPTH with repeats that add nothing (live = 0): no exit inside the unrolled body.
-        // The scheduling barriers keep each step's loads ahead of the previous step's
-        // arithmetic, with pin() (see there) keeping that arithmetic behind them.
-        MmaW<T> F[D];
-        Xf X[D];
-        const bool work = s1 > s0;
-        if (work) {
-#pragma unroll
-            for (int d = 0; d < D - 1; ++d) {
-                F[d].load(wrow, min(s0 + d, s1 - 1), g, nblk);
-                if constexpr (!XL) read_x(X[d], min(s0 + d, s1 - 1));
-            }
-        }
-        if (!copied) {   // XL, first tile: the slice's image into LDS behind the weight prologue
-            const uint4 *src = reinterpret_cast<const uint4 *>(xs);
-            uint4 *dst = reinterpret_cast<uint4 *>(xsm);
-            const int n16 = n_steps * SB / 16;
-            constexpr int B = 8;   // loads issued before the writes that wait for them
-            for (int i0 = threadIdx.x; i0 < n16; i0 += B * KS * WAVE) {
-                uint4 v[B];
-#pragma unroll
-                for (int b = 0; b < B; ++b) v[b] = src[min(i0 + b * KS * WAVE, n16 - 1)];
-#pragma unroll
-                for (int b = 0; b < B; ++b) dst[min(i0 + b * KS * WAVE, n16 - 1)] = v[b];   // (clamped: a repeat of the last)
-            }
-            lds_barrier();
-            copied = true;
-        }
-        if (work) {
-            const int n_pad = (s1 - s0 + D - 1) / D * D;
-            auto step = [&](auto k_c, int s) __attribute__((always_inline)) {
-                constexpr int k = decltype(k_c)::value;
-                const int sl = min(s + D - 1, s1 - 1);
-                F[(k + D - 1) % D].load(wrow, sl, g, nblk);
-                if constexpr (!XL) read_x(X[(k + D - 1) % D], sl);
-                __builtin_amdgcn_sched_barrier(0);
-                if constexpr (XL) read_x(X[k], min(s, s1 - 1));
-                compute(F[k], X[k], s < s1 ? 1.f : 0.f);
-            };
-            for (int it = 0; it < n_pad; it += D) {
-                const int s = s0 + it;
-                step(std::integral_constant<int, 0>{}, s);
-                if constexpr (D > 1) step(std::integral_constant<int, 1 % D>{}, s + 1);
-                if constexpr (D > 2) step(std::integral_constant<int, 2 % D>{}, s + 2);
-                if constexpr (D > 3) step(std::integral_constant<int, 3 % D>{}, s + 3);
-                if constexpr (D > 4) step(std::integral_constant<int, 4 % D>{}, s + 4);
-                if constexpr (D > 5) step(std::integral_constant<int, 5 % D>{}, s + 5);
-            }
-        }
-        // K-split reduction over the waves, fixed order (live lanes: column t < TOK)
-        if (r < TOK) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) red[wave][(g * TOK + r) * 4 + i] = acc[i];
-        }
-        lds_barrier();
-        if (wave == 0 && r < TOK) {
-            float v[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = red[0][(g * TOK + r) * 4 + i];
-#pragma unroll
-            for (int w = 1; w < KS; ++w)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) v[i] += red[w][(g * TOK + r) * 4 + i];
-            if (r < a.M) {
-                float *dst = reinterpret_cast<float *>(a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3 + (int64_t)r * a.nb1);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int row = row0 + 4 * g + i;
-                    if (row < a.N) dst[row] = v[i];
-                }
-            }
-        }
-        lds_barrier();   // (red is rewritten by the next tile)
+            for (int i = 0; i < 4; ++i)
+                if (row0 + 4 * g + i < a.N) dcol[row0 + 4 * g + i] = acc[i];
+        return;
     }
+    // partial of (slice, K part, tile): [lane (g, t < TOK)][4] floats
+    const int n_tiles8 = gridDim.x * 8;
+    auto slot = [&](int k) { return part + (((int64_t)z * n_kp + k) * n_tiles8 + tile) * (TOK * 4 * 4) + (g * TOK + tl) * 4; };
+    if (live_lane) {
+        float *p = slot(kp);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) __hip_atomic_store(p + i, acc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+    lds_barrier();
+    int *c = cnt + (int64_t)z * gridDim.x + rg;
+    if (threadIdx.x == 0) order = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    lds_barrier();
+    if (order != n_kp - 1) return;   // (uniform) a later workgroup finishes the row group
+    if (live_lane) {
+        // the parts in K order, loads of 8 parts issued before their sums (one latency per 8)
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int k0p = 0; k0p < n_kp; k0p += 8) {
+            float pv[8][4];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float *p = slot(min(k0p + k, n_kp - 1));
+#pragma unroll
+                for (int i = 0; i < 4; ++i) pv[k][i] = __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] += k0p + k < n_kp ? pv[k][i] : 0.f;
+        }
+        if (r < a.M)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (row0 + 4 * g + i < a.N) dcol[row0 + 4 * g + i] = v[i];
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -522,87 +524,82 @@ __global__ __launch_bounds__(KS * WAVE) void mmvq_mma_kernel(const MmArgs a, con
 // ------------------------------------------------------------------------------------------
 static int mma_steps(const MmArgs &a) { return (a.K + MMA_STEP_K - 1) / MMA_STEP_K; }
 
-template <int T> static size_t img_bytes_t(const MmArgs &a) {
-    return (size_t)mma_steps(a) * (a.M <= 8 ? mma_step_bytes<T, 8>() : mma_step_bytes<T, 16>()) * a.ne12 * a.ne13;
+// K parts of NSTEP steps: 8 (1024 K) when that still gives ~2 workgroups per CU over the grid
+// (row groups x slices x parts), else 4
+static int mma_nstep(const MmArgs &a) {
+    const int S = mma_steps(a);
+    const int64_t groups = (a.N + 127) / 128, slices = (int64_t)a.ne12 * a.ne13;
+    const char *e = getenv("GGML_MI355X_MMA_NSTEP");   // per call: tests switch it
+    if (e) return atoi(e) <= 4 ? 4 : 8;
+    return groups * slices * ((S + 7) / 8) >= 384 ? 8 : 4;
 }
 
-size_t mmvq_mma_img_bytes(int type, const MmArgs &a) {
+template <int T, int TOK> static void mma_geometry(const MmArgs &a, int &groups, int &n_kp, size_t &lds) {
+    const int S = mma_steps(a);
+    const int ns = mma_nstep(a);
+    groups = (a.N + 127) / 128;
+    n_kp = (S + ns - 1) / ns;
+    lds = (size_t)ns * mma_step_bytes<T, TOK>();
+}
+
+size_t mmvq_mma_part_bytes(int type, const MmArgs &a) {
+    int groups = 0, n_kp = 1;
+    size_t lds = 0;
+    const bool t8 = a.M <= 8;
     switch (type) {
-        case T_Q4_0: return img_bytes_t<T_Q4_0>(a);
-        case T_Q8_0: return img_bytes_t<T_Q8_0>(a);
-        case T_Q4_K: return img_bytes_t<T_Q4_K>(a);
-        case T_Q5_K: return img_bytes_t<T_Q5_K>(a);
-        case T_Q6_K: return img_bytes_t<T_Q6_K>(a);
+        case T_Q4_0: t8 ? mma_geometry<T_Q4_0, 8>(a, groups, n_kp, lds) : mma_geometry<T_Q4_0, 16>(a, groups, n_kp, lds); break;
+        case T_Q8_0: t8 ? mma_geometry<T_Q8_0, 8>(a, groups, n_kp, lds) : mma_geometry<T_Q8_0, 16>(a, groups, n_kp, lds); break;
+        case T_Q4_K: t8 ? mma_geometry<T_Q4_K, 8>(a, groups, n_kp, lds) : mma_geometry<T_Q4_K, 16>(a, groups, n_kp, lds); break;
+        case T_Q5_K: t8 ? mma_geometry<T_Q5_K, 8>(a, groups, n_kp, lds) : mma_geometry<T_Q5_K, 16>(a, groups, n_kp, lds); break;
         default: return 0;
     }
-}
-
-template <int T, int TOK, int KS, bool XL>
-static hipError_t mma_launch_k(const MmArgs &a, uint8_t *img, int S, int tiles, int slices, size_t xl_bytes, hipStream_t st) {
-    const void *kern = reinterpret_cast<const void *>(mmvq_mma_kernel<T, TOK, KS, XL>);
-    if constexpr (XL) {
-        static bool attr_set = false;   // per instantiation; set only once the call succeeded
-        if (!attr_set) {
-            hipFuncAttributes fa{};
-            hipError_t e = hipFuncGetAttributes(&fa, kern);
-            if (e == hipSuccess) e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(160 * 1024 - fa.sharedSizeBytes));
-            if (e != hipSuccess) {
-                (void)hipGetLastError();
-                return e;
-            }
-            attr_set = true;
-        }
-    }
-    // XL: one workgroup per CU, persistent over the slice's tiles (the image copy is paid once)
-    const int gx = XL ? std::max(1, std::min(tiles, 256 / std::max(1, slices))) : tiles;
-    hipLaunchKernelGGL((mmvq_mma_kernel<T, TOK, KS, XL>), dim3(gx, slices), dim3(KS * WAVE), XL ? xl_bytes : 0, st, a,
-                       (const uint8_t *)img, S, tiles);
-    return hipGetLastError();
+    if (n_kp == 1) return 0;
+    // [slice][part][tile][g 4][t TOK][4] floats
+    return (size_t)a.ne12 * a.ne13 * n_kp * groups * 8 * (t8 ? 8 : 16) * 16 * sizeof(float);
 }
 
 template <int T, int TOK>
-static hipError_t mma_tok(const MmArgs &a, uint8_t *img, hipStream_t st) {
-    const int S = mma_steps(a);
+static hipError_t mma_tok(const MmArgs &a, float *part, int *cnt, hipStream_t st) {
+    int groups = 0, n_kp = 1;
+    size_t lds = 0;
+    mma_geometry<T, TOK>(a, groups, n_kp, lds);
     const int slices = a.ne12 * a.ne13;
-    const int tiles = (a.N + 15) / 16;
-    hipLaunchKernelGGL((mma_prequant<T, TOK>), dim3(S, slices), dim3(TOK * 16), 0, st, a, img);
-    // ~16 waves per CU over the whole grid; never more waves than steps
-    const char *kse = getenv("GGML_MI355X_MMA_KS");   // per call: tests switch it
-    const int ks_env = kse ? atoi(kse) : 0;
-    const int64_t waves_per_tile = std::max<int64_t>(1, (256 * 16) / ((int64_t)tiles * slices));
-    int ks = ks_env > 0 ? ks_env : waves_per_tile >= 16 ? 16 : waves_per_tile >= 8 ? 8 : 4;
-    while (ks > 4 && ks > S) ks >>= 1;
-    if (T == T_Q6_K && ks > 8) ks = 8;   // (its fragments need more than the 128 VGPRs of 16 waves)
-    // the image in LDS when it fits beside the static arrays (<= 16 KiB); GGML_MI355X_MMA_XL=0: never
-    const char *xle = getenv("GGML_MI355X_MMA_XL");
-    const size_t xl_bytes = (size_t)S * mma_step_bytes<T, TOK>();
-    // (not Q6_K: its deeper fragment sets spill)
-    const bool xl = T != T_Q6_K && !(xle && atoi(xle) == 0) && xl_bytes <= 144 * 1024;
-    // XL: 8 waves per workgroup (one per CU, persistent): the deep weight sets need the 256
-    // VGPRs of 2 waves per SIMD; 16 waves would spill them
-    if (xl) return ks >= 8 ? mma_launch_k<T, TOK, 8, true>(a, img, S, tiles, slices, xl_bytes, st)
-                           : mma_launch_k<T, TOK, 4, true>(a, img, S, tiles, slices, xl_bytes, st);
-    if (ks >= 16 && (T == T_Q4_0 || T == T_Q8_0))   // (the K-quants' sets spill at 16 waves)
-        return mma_launch_k<T, TOK, 16, false>(a, img, S, tiles, slices, xl_bytes, st);
-    if (ks >= 8) return mma_launch_k<T, TOK, 8, false>(a, img, S, tiles, slices, xl_bytes, st);
-    return mma_launch_k<T, TOK, 4, false>(a, img, S, tiles, slices, xl_bytes, st);
+    if (n_kp > 1 && (part == nullptr || cnt == nullptr || (int64_t)groups * slices > 16384)) return hipErrorInvalidValue;
+    const char *de = getenv("GGML_MI355X_MMA_D");   // measurements: 2 = one step ahead
+    const bool d2 = de && atoi(de) == 2;
+    const bool n8 = mma_nstep(a) == 8;
+    const dim3 grid(groups, n_kp, slices);
+    const int S = mma_steps(a);
+    // (16-B activation loads when the rows are 16-B aligned; K is a multiple of 32 for every type)
+#define MMA_GO(DV, NS)                                                                                                \
+    if (a.x_aligned16) hipLaunchKernelGGL((mmvq_mma_kernel<T, TOK, DV, NS, true>), grid, dim3(8 * WAVE), lds, st, a, S, n_kp, part, cnt); \
+    else hipLaunchKernelGGL((mmvq_mma_kernel<T, TOK, DV, NS, false>), grid, dim3(8 * WAVE), lds, st, a, S, n_kp, part, cnt)
+    if (d2) {
+        if (n8) MMA_GO(2, 8);
+        else MMA_GO(2, 4);
+    } else {
+        if (n8) MMA_GO(mma_depth<T>(), 8);
+        else MMA_GO(mma_depth<T>(), 4);
+    }
+#undef MMA_GO
+    return hipGetLastError();
 }
 
 template <int T>
-static hipError_t mma_type(const MmArgs &a, uint8_t *img, hipStream_t st) {
-    return a.M <= 8 ? mma_tok<T, 8>(a, img, st) : mma_tok<T, 16>(a, img, st);
+static hipError_t mma_type(const MmArgs &a, float *part, int *cnt, hipStream_t st) {
+    return a.M <= 8 ? mma_tok<T, 8>(a, part, cnt, st) : mma_tok<T, 16>(a, part, cnt, st);
 }
 
-// plain MUL_MAT with 1 <= M <= 16 columns, img = mmvq_mma_img_bytes(type, a) of scratch
-hipError_t mmvq_mma_launch(int type, const MmArgs &a, uint8_t *img, hipStream_t st) {
-    if (a.M < 1 || a.M > 16 || img == nullptr) return hipErrorInvalidValue;
+// plain MUL_MAT with 1 <= M <= 16 columns. part: mmvq_mma_part_bytes(type, a) bytes of scratch
+// (nullptr when that is 0), cnt: zeroed counters (Scratch::counters) when part is set
+hipError_t mmvq_mma_launch(int type, const MmArgs &a, float *part, int *cnt, hipStream_t st) {
+    if (a.M < 1 || a.M > 16) return hipErrorInvalidValue;
     switch (type) {
-        case T_Q4_0: return mma_type<T_Q4_0>(a, img, st);
-        case T_Q8_0: return mma_type<T_Q8_0>(a, img, st);
-        case T_Q4_K: return mma_type<T_Q4_K>(a, img, st);
-        case T_Q5_K: return mma_type<T_Q5_K>(a, img, st);
-        case T_Q6_K: return mma_type<T_Q6_K>(a, img, st);
-        default: return hipErrorInvalidValue;
+        case T_Q4_0: return mma_type<T_Q4_0>(a, part, cnt, st);
+        case T_Q8_0: return mma_type<T_Q8_0>(a, part, cnt, st);
+        case T_Q4_K: return mma_type<T_Q4_K>(a, part, cnt, st);
+        case T_Q5_K: return mma_type<T_Q5_K>(a, part, cnt, st);
+        default: return hipErrorInvalidValue;   // (Q6_K: its eight MFMAs per step spill; the VALU kernels take it)
     }
 }
 

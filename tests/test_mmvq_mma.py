@@ -9,8 +9,8 @@ the CPU oracle (ggml-cpu's vec_dot on its own src1 quantization) the reference's
 
 Covered: all five types; 2, 3, 5 and 8 columns; ragged rows (N % 16 != 0); Q4_0 / Q8_0 K that
 ends inside a 128-step (K % 128 = 32, 64, 96), K-quants at odd super-block counts; the reference's
-perf shapes (K = 14336, bs 2..8); broadcast batch slices (ne12 = 2 * ne02); a Q6_K row stride
-that leaves every other super-block 2-byte aligned; the wave-count override (4 / 8 / 16 waves).
+perf shapes (K = 14336, bs 2..8); broadcast batch slices (ne12 = 2 * ne02); K parts of 4 and 8
+steps over workgroups. Q6_K stays on the VALU kernels.
 """
 import os
 
@@ -25,7 +25,7 @@ torch = pytest.importorskip("torch")
 
 pytestmark = pytest.mark.gpu
 
-TYPES = [qref.Q4_0, qref.Q8_0, qref.Q4_K, qref.Q5_K, qref.Q6_K]
+TYPES = [qref.Q4_0, qref.Q8_0, qref.Q4_K, qref.Q5_K]   # (Q6_K stays on the VALU kernels)
 
 
 def operands(t, N, M_, K, seed, ne2=(1, 1)):
@@ -51,11 +51,9 @@ def run_with(mm, a, b, out_ne, env):
                 os.environ[k] = v
 
 
-def check(mm, t, N, M_, K, seed=3, ne2=(1, 1), ks=None, oracle=True):
+def check(mm, t, N, M_, K, seed=3, ne2=(1, 1), oracle=True):
     a, b, out_ne = operands(t, N, M_, K, seed, ne2)
     env = {"GGML_MI355X_MMA": 2}
-    if ks is not None:
-        env["GGML_MI355X_MMA_KS"] = ks
     got = run_with(mm, a, b, out_ne, env)
     assert np.all(np.isfinite(got))
     valu = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 0})
@@ -82,7 +80,7 @@ def test_mma_partial_step(mm, t, K):
     check(mm, t, 37, 4, K)
 
 
-@pytest.mark.parametrize("t", [qref.Q4_K, qref.Q5_K, qref.Q6_K], ids=lambda t: qref.NAMES[t])
+@pytest.mark.parametrize("t", [qref.Q4_K, qref.Q5_K], ids=lambda t: qref.NAMES[t])
 @pytest.mark.parametrize("K", [256, 768, 2304])
 def test_mma_kquant_k(mm, t, K):
     """odd super-block counts (the steps are half super-blocks: odd step pairs per wave)"""
@@ -106,15 +104,25 @@ def test_mma_broadcast_slices(mm, t):
     check(mm, t, 64, 3, 256 if qref.BLCK[t] == 256 else 128, ne2=(2, 4))
 
 
-@pytest.mark.parametrize("ks", [4, 8, 16])
-@pytest.mark.parametrize("t", [qref.Q4_0, qref.Q4_K, qref.Q6_K], ids=lambda t: qref.NAMES[t])
-def test_mma_wave_counts(mm, t, ks):
-    """the K split over 4, 8 or 16 waves (Q6_K caps at 8) sums in a fixed order: the same bits
-    whatever the split, up to the fp32 order of the partial sums"""
-    check(mm, t, 96, 5, 4096, ks=ks, oracle=False)
+@pytest.mark.parametrize("nstep", [4, 8])
+@pytest.mark.parametrize("t", [qref.Q4_0, qref.Q4_K], ids=lambda t: qref.NAMES[t])
+def test_mma_k_parts(mm, t, nstep):
+    """the K split into parts of 4 or 8 steps over workgroups (partials through write-through
+    stores and a counter; the last workgroup sums them in K order); run twice for the counters'
+    re-arming"""
+    a, b, out_ne = operands(t, 300, 5, 4096, 5)
+    env = {"GGML_MI355X_MMA": 2, "GGML_MI355X_MMA_NSTEP": nstep}
+    g1 = run_with(mm, a, b, out_ne, env)
+    g2 = run_with(mm, a, b, out_ne, env)
+    assert np.array_equal(g1.view(np.uint32), g2.view(np.uint32)), "K-split result not repeatable"
+    valu = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 0})
+    assert qref.nmse(g1, valu) <= 1e-10
 
 
-def test_mma_q6k_odd_row_alignment(mm):
-    """Q6_K rows of 3 super-blocks (630 B): every other row starts 2-byte aligned, so the
-    windows of the fragment loads are funnel-shifted by 2 on those rows"""
-    check(mm, qref.Q6_K, 33, 7, 768)
+@pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])
+def test_mma_depth2(mm, t):
+    """one weight step ahead (GGML_MI355X_MMA_D=2) instead of the default depth"""
+    a, b, out_ne = operands(t, 100, 7, 2048, 9)
+    got = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 2, "GGML_MI355X_MMA_D": 2})
+    valu = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 0})
+    assert qref.nmse(got, valu) <= 1e-10
