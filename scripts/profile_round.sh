@@ -25,6 +25,8 @@ squash() {  # squash <dir>
     for t in $(find $d -name '*kernel_trace.csv'); do python scripts/trace_summary.py $t 2 > ${t%.csv}_summary.txt; rm -f $t; done
     find $d -name '*counter_collection.csv' -size +2M -delete
 }
+# the HBM floor probe (built here when the tree does not carry the binary)
+[ -x scripts/hbm_probe ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o scripts/hbm_probe scripts/hbm_probe.hip || exit 1
 [ -s $O/bench.log ] || step bench 600 python bench.py
 step prof_bench 600 $RP -d $O/bench -o run -- python bench.py --no-extra --cpu-seconds 1
 squash $O/bench
@@ -45,5 +47,11 @@ step prof_gpt2 300 $RP -d $O/gpt2 -o run -- python scripts/gpt2_bench.py 1 256 1
 squash $O/gpt2
 step block_stamps 200 bash -c 'python scripts/block_stamps.py 24 64 && python scripts/block_stamps.py 24 600'
 step hbm_floor 120 scripts/hbm_probe
+# the single-launch floor on one basis: rocprofv3 durations of a bare stream of one Q4_K 4096^2
+# matrix's bytes (hbm_probe s) and of the mat-vec on the same bytes
+step floor_stream 120 $RP -d $O/floor_stream -o run -- scripts/hbm_probe s
+squash $O/floor_stream
+step floor_mv 120 $RP -d $O/floor_mv -o run -- python scripts/prof_singles.py 128 q4_K:4096:64
+squash $O/floor_mv
 du -sh $O
 echo "=== done"
