@@ -25,6 +25,12 @@
 // waves per CU at any N); MUL_MAT batch slices on grid.y.
 #include <type_traits>
 
+// measurement builds only (scripts/mma_exp.sh; results wrong by design): bit 1 = no activation
+// loads (the records quantize zeros), bit 2 = no weight loads, bit 4 = no K-part hand-off
+#ifndef MMA_EXP
+#define MMA_EXP 0
+#endif
+
 #include "mmvq_impl.h"
 
 namespace mi355x {
@@ -381,7 +387,8 @@ __global__ __launch_bounds__(8 * WAVE) void mmvq_mma_kernel(const MmArgs a, int 
     // unit are two runs of 4 consecutive floats in either element order)
     MmaW<T> F[D];
 #pragma unroll
-    for (int d = 0; d < D - 1; ++d) F[d].load(wrow, min(k0 + d, k1 - 1), g, nblk);
+    for (int d = 0; d < D - 1; ++d)
+        if constexpr (!(MMA_EXP & 2)) F[d].load(wrow, min(k0 + d, k1 - 1), g, nblk);
     {
         const float *xz = reinterpret_cast<const float *>(a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13);
         const int units = (k1 - k0) * 4 * TOK * 4;   // (step, t, j, g), g fastest
@@ -393,7 +400,12 @@ __global__ __launch_bounds__(8 * WAVE) void mmvq_mma_kernel(const MmArgs a, int 
                 const int u = min(u0 + q * 8 * WAVE, units - 1);
                 const int j = (u >> 2) & 3, t = (u >> 4) % TOK, sl = (u >> 4) / TOK;
                 const float *col = reinterpret_cast<const float *>(reinterpret_cast<const uint8_t *>(xz) + (int64_t)min(t, a.M - 1) * a.nb11);
-                mma_xload<T, XA>(a, col, k0 + sl, j, u & 3, v[q]);
+                if constexpr (MMA_EXP & 1) {
+                    for (int c = 0; c < 8; ++c) v[q][c] = 0.f;
+                    (void)col;
+                } else {
+                    mma_xload<T, XA>(a, col, k0 + sl, j, u & 3, v[q]);
+                }
             }
 #pragma unroll
             for (int q = 0; q < QU; ++q) {
@@ -465,7 +477,8 @@ __global__ __launch_bounds__(8 * WAVE) void mmvq_mma_kernel(const MmArgs a, int 
     auto step = [&](auto k_c, int i) __attribute__((always_inline)) {
         constexpr int k = decltype(k_c)::value;
         const int s = k0 + i;
-        if (i + D - 1 < NSTEP) F[(k + D - 1) % D].load(wrow, min(s + D - 1, k1 - 1), g, nblk);
+        if constexpr (!(MMA_EXP & 2))
+            if (i + D - 1 < NSTEP) F[(k + D - 1) % D].load(wrow, min(s + D - 1, k1 - 1), g, nblk);
         __builtin_amdgcn_sched_barrier(0);
         compute(F[k], min(s, k1 - 1), s < k1 ? 1.f : 0.f);
     };
@@ -474,7 +487,7 @@ __global__ __launch_bounds__(8 * WAVE) void mmvq_mma_kernel(const MmArgs a, int 
     // 3. store (live lanes: column t < TOK, rows 4G + i)
     const bool live_lane = r < TOK;
     float *dcol = reinterpret_cast<float *>(a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3 + (int64_t)r * a.nb1);
-    if (n_kp == 1) {
+    if (n_kp == 1 || (MMA_EXP & 4)) {
         if (live_lane && r < a.M)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
