@@ -28,8 +28,9 @@ bool mmvq_has_nc(int nc);
 int mmvq_max_k_for_nc(int nc);
 bool mmvq_bigk(int K);
 hipError_t mmvq_ring_launch(int type, const MmArgs &a, int nc, int rpw, uint8_t *img, hipStream_t st);
-hipError_t mmvq_mma_launch(int type, const MmArgs &a, float *part, int *cnt, hipStream_t st);
-size_t mmvq_mma_part_bytes(int type, const MmArgs &a);
+hipError_t mmvq_mma_launch(int type, const MmArgs &a, uint8_t *img, hipStream_t st);
+size_t mmvq_mma_img_bytes(int type, const MmArgs &a);
+bool mmvq_mma_supported(int type, const MmArgs &a);
 size_t mmvq_ring_img_bytes(const MmArgs &a, int nc);
 hipError_t dequant_launch(int type, const void *src, float *dst, int64_t n, hipStream_t st);
 struct RowsArgs {
@@ -195,16 +196,14 @@ static int mma_min_cols() {
 // mutex; nullptr = no pre-quantized images)
 static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st, Scratch *scratch = nullptr) {
     const int rpw = pick_rpw(type, (int64_t)m.N * m.ne12 * m.ne13);
-    if (scratch != nullptr && type != T_Q6_K && ncols >= mma_min_cols() && ncols <= 8) {
+    if (scratch != nullptr && ncols >= mma_min_cols() && ncols <= 8) {
         MmArgs g = m;
         g.x = m.x + (int64_t)c0 * m.nb11;
         g.dst = m.dst + (int64_t)c0 * m.nb1;
         g.M = ncols;
         // (nullptr inside a capture that would grow the scratch: the kernels below take it)
-        const size_t pb = mmvq_mma_part_bytes(type, g);
-        float *part = pb ? static_cast<float *>(scratch->get(pb, st)) : nullptr;
-        int *cnt = pb ? scratch->counters(st) : nullptr;
-        if (pb == 0 || (part != nullptr && cnt != nullptr)) return mmvq_mma_launch(type, g, part, cnt, st);
+        if (mmvq_mma_supported(type, g))
+            if (uint8_t *img = static_cast<uint8_t *>(scratch->get(mmvq_mma_img_bytes(type, g), st))) return mmvq_mma_launch(type, g, img, st);
     }
     while (ncols > 0) {
         MmArgs g = m;

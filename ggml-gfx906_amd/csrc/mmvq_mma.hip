@@ -1,32 +1,37 @@
-// mmvq_mma.hip — the quantized mat-vec for 2..16 src1 columns on the int8 matrix cores.
+// mmvq_mma.hip — the quantized mat-vec for 1..8 src1 columns on the int8 matrix cores.
 //
 // The reference streams the weights once for up to 8 columns with per-column dp4a dot products
 // (mul_mat_vec_q<type, ncols_dst>, src/ggml-cuda/mmvq.cu:139-226). On gfx950 the per-column VALU
-// dots (mmvq_impl.h / mmvq_ring.hip) grow with the column count, and so do the LDS reads of the
-// quantized columns, which every wave re-reads: at 8 columns a CU spends as long on them as on
-// its share of the weight stream, and the two do not overlap (profiles/r05_ring_depth_ab.txt:
-// 8 columns take 2.2x one column at K = 14336). Here the columns are the N side of
-// v_mfma_i32_16x16x32_i8 and the weight rows its M side:
+// dots (mmvq_impl.h / mmvq_ring.hip) grow with the column count: at 8 columns a CU spends as
+// long on them as on its share of the weight stream (profiles/r05_ring_depth_ab.txt: 8 columns
+// take 2.2x one column at K = 14336). Here the dots run on v_mfma_i32_16x16x32_i8, weight rows
+// on its M side, and the VALU only unpacks weights and applies the block scales.
 //
-//  * one 32-weight block (Q4_0 / Q8_0) or 32-weight sub-block (K-quants) = one MFMA K step;
-//    the integer dot of 16 rows x 16 columns is one instruction, the block scales are applied
-//    to its int32 results in fp32 (per block, as ggml-cpu's vec_dot does);
-//  * a wave owns 16 weight rows and a contiguous range of K; lane (r = l & 15, g = l >> 4)
-//    loads row r's bytes for k-group g, straight to registers (no LDS staging of weights);
-//    Q4_0 / Q8_0 lanes load one whole block each and a 4 x 4 transpose across the lanes of a
-//    row (two permlane swaps) hands every lane its k-group of all four blocks;
-//  * the columns were quantized once per call by mma_prequant into the B-fragment order
-//    (int8 per 32-block, d = amax/127, round-to-nearest-even, exactly as the other mat-vec
-//    kernels), so lane (t, g) reads its 4 blocks of column t as 32 contiguous bytes;
-//  * the row scales reach the output lanes (column t, rows 4G..4G+3) through a 256-B per-wave
-//    LDS slot; the K ranges of a workgroup's waves are summed through LDS in a fixed order.
+// An MFMA's 16 columns would leave most of the scale work on padding columns (a lane owns 4
+// outputs of one column; at 4 tokens 12 of 16 columns are empty). So the columns are packed
+// block-diagonally: with TOK tokens, column c holds token c % TOK of block group c / TOK, and
+// the 32-wide contraction is split into 16 / TOK ranges, one per block group; each lane's
+// B fragment is zero outside its group's range. Every output is then a (row, token, block)
+// dot, and the scale epilogue does no padding work:
 //
-// A workgroup = KS waves on the same 16 rows (KS = 4, 8 or 16, so that the grid holds ~16
-// waves per CU at any N); MUL_MAT batch slices on grid.y.
+//  * TOK = 4 (1..4 columns): 4 blocks per MFMA, 8 K of each; 4 MFMAs make a step of 4 blocks
+//    (128 K) and lane (row r, k-group g) owns block g of row r for the whole step;
+//  * TOK = 8 (5..8 columns): 2 blocks per MFMA, 16 K of each; two pairs of MFMAs per step,
+//    lane g holds half g & 1 of block g >> 1 of the pair (Q4_0 / Q8_0: a permlane exchange of
+//    the halves of the blocks the lanes loaded whole);
+//  * the B fragments come from the columns' records, quantized once per call by mma_prequant
+//    (int8 per 32-block, d = amax / 127, round-to-nearest-even, exactly as the other mat-vec
+//    kernels); a lane outside its group's range loads from an offset past the buffer's end,
+//    which returns zeros without a memory access;
+//  * the row scales reach the output lanes through a per-wave LDS slot; Q4_0 codes stay
+//    unsigned (0..15) and the - 8 comes back through d * sum(q) of the column block;
+//  * a workgroup = 16 waves on one 16-row tile, wave w a straight-line run of K steps; the
+//    block groups are summed across lanes (DPP) and the waves through LDS in a fixed order,
+//    so no workgroup depends on another and results repeat bit for bit.
 #include <type_traits>
 
 // measurement builds only (scripts/mma_exp.sh; results wrong by design): bit 1 = no activation
-// loads (the records quantize zeros), bit 2 = no weight loads, bit 4 = no K-part hand-off
+// loads (pre-pass and records), bit 2 = no weight loads
 #ifndef MMA_EXP
 #define MMA_EXP 0
 #endif
@@ -37,45 +42,43 @@ namespace mi355x {
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
-constexpr int MMA_STEP_K = 128;   // K per step: 4 MFMA K steps of 32
+constexpr int MMA_STEP_K = 128;   // K per step: 4 blocks of 32
+constexpr int MMA_KS = 16;        // waves per workgroup
+constexpr uint32_t MMA_RSRC_W3 = 0x00020000u;   // raw buffer descriptor dword 3 (as mmq8.hip)
+constexpr uint32_t MMA_OOB = 0x80000000u;       // an offset past any image: loads return zeros
 
-// activation image of one (slice, step), one record per column t: codes [g 4][j 4][8 B] (int8,
-// the B-fragment byte order of the type), d [4] f32, and for Q4_K / Q5_K d * sum(q) [4] f32.
-// The record stride (144 / 160 B) also spreads the columns' 16-B LDS reads over distinct banks.
-template <int T> __host__ __device__ constexpr int mma_rec_bytes() { return (T == T_Q4_K || T == T_Q5_K) ? 160 : 144; }
-template <int T, int TOK> __host__ __device__ constexpr int mma_step_bytes() { return TOK * mma_rec_bytes<T>(); }
+// activation image of one (slice, step): codes [t TOK][block 4][32 B] in chunk order, then
+// [t][block] {d, d * sum(q)} f32
+template <int TOK> __host__ __device__ constexpr int mma_step_bytes() { return TOK * 160; }
 
-// element of a 32-block held by byte i (0..7) of k-group g: Q4_0 pairs each nibble byte's low
-// and high halves (byte 4g + i holds elements 4g + i and 4g + i + 16), the others are in order
-template <int T> __device__ __forceinline__ int mma_elem(int g, int i) {
-    if constexpr (T == T_Q4_0) return i < 4 ? 4 * g + i : 4 * g + 12 + i;
-    else return 8 * g + i;
-}
+// element of a 32-block at byte i (0..7) of chunk m (0..3): chunks 0 / 1 are elements 0..7 /
+// 16..23, chunks 2 / 3 are 8..15 / 24..31, so a chunk pair {2a, 2a + 1} is the low and high
+// nibbles of Q4_0 qs bytes 8a .. 8a + 7 (and of a K-quant's 32-byte qs run)
+__host__ __device__ constexpr int mma_elem(int m, int i) { return 8 * (m >> 1) + 16 * (m & 1) + i; }
 
-// k-group g of block j of step s of column t (zeros past K or M), loaded, then quantized into
-// its record `rec` (the record of (s, t)); the 4 threads of a block (g = 0..3) are consecutive
-// lanes and share amax and sum(q) through DPP. The arithmetic of mmvq_impl.h's xblock_store,
-// bit for bit.
+// chunk m of block j of step s of column t (zeros past K or M), loaded, quantized and stored into
+// the step's image; the 4 threads of a block are consecutive lanes and share amax and sum(q)
+// through DPP. The arithmetic of mmvq_impl.h's xblock_store, bit for bit.
 // (the loads only: the zeroing past K / M is applied by mma_quant once every load of the batch
 // is issued; a select right behind a load makes the compiler wait for it before the next load)
-template <int T, bool XA>
-__device__ __forceinline__ void mma_xload(const MmArgs &a, const float *col, int s, int j, int g, float (&v)[8]) {
-    const int kb = s * MMA_STEP_K + 32 * j;   // first element of the block
+template <bool XA>
+__device__ __forceinline__ void mma_xload(const MmArgs &a, const float *col, int s, int j, int m, float (&v)[8]) {
+    const int k0 = s * MMA_STEP_K + 32 * j + mma_elem(m, 0);   // 8 consecutive elements
     if constexpr (XA) {   // rows 16-B aligned, K % 4 == 0 (runs of 4 clamped as a whole)
-        const float4 lo = *reinterpret_cast<const float4 *>(col + min(kb + mma_elem<T>(g, 0), a.K - 4));
-        const float4 hi = *reinterpret_cast<const float4 *>(col + min(kb + mma_elem<T>(g, 4), a.K - 4));
+        const float4 lo = *reinterpret_cast<const float4 *>(col + min(k0, a.K - 4));
+        const float4 hi = *reinterpret_cast<const float4 *>(col + min(k0 + 4, a.K - 4));
         v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
         v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
     } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = col[min(kb + mma_elem<T>(g, i), a.K - 1)];
+        for (int i = 0; i < 8; ++i) v[i] = col[min(k0 + i, a.K - 1)];
     }
 }
-template <int T, bool SX>
-__device__ __forceinline__ void mma_quant(const MmArgs &a, float (&v)[8], int s, int j, int t, int g, uint8_t *rec, bool store) {
-    const int kb = s * MMA_STEP_K + 32 * j;
+template <int TOK>
+__device__ __forceinline__ void mma_quant(const MmArgs &a, float (&v)[8], int s, int j, int t, int m, uint8_t *step) {
+    const int k0 = s * MMA_STEP_K + 32 * j + mma_elem(m, 0);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = (kb + mma_elem<T>(g, i) < a.K && t < a.M) ? v[i] : 0.f;
+    for (int i = 0; i < 8; ++i) v[i] = (k0 + i < a.K && t < a.M) ? v[i] : 0.f;
     float amax = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[i]));
@@ -89,26 +92,16 @@ __device__ __forceinline__ void mma_quant(const MmArgs &a, float (&v)[8], int s,
     for (int i = 0; i < 8; ++i) b[i] = __float_as_uint(__builtin_fmaf(v[i], id, MAGIC));
     const uint32_t w0 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(b[3], b[2], 0x0c0c0400u), __builtin_amdgcn_perm(b[1], b[0], 0x0c0c0400u), 0x05040100u);
     const uint32_t w1 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(b[7], b[6], 0x0c0c0400u), __builtin_amdgcn_perm(b[5], b[4], 0x0c0c0400u), 0x05040100u);
-    if (store) *reinterpret_cast<uint2 *>(rec + g * 32 + j * 8) = make_uint2(w0 ^ 0x80808080u, w1 ^ 0x80808080u);
-    float fs = 0.f;
-    if constexpr (SX) {
-        const int qs = (int)__builtin_amdgcn_udot4(w0, 0x01010101u, __builtin_amdgcn_udot4(w1, 0x01010101u, 0u, false), false) - 1024;
-        fs = (float)qs;
-        fs += dpp_f<DPP_XOR1>(fs);
-        fs += dpp_f<DPP_XOR2>(fs);
-    }
-    if (g == 0 && store) {
-        float *ds = reinterpret_cast<float *>(rec + 128);
-        ds[j] = d;
-        if constexpr (SX) ds[4 + j] = d * fs;
-    }
+    *reinterpret_cast<uint2 *>(step + (t * 4 + j) * 32 + m * 8) = make_uint2(w0 ^ 0x80808080u, w1 ^ 0x80808080u);
+    const int qs = (int)__builtin_amdgcn_udot4(w0, 0x01010101u, __builtin_amdgcn_udot4(w1, 0x01010101u, 0u, false), false) - 1024;
+    float fs = (float)qs;
+    fs += dpp_f<DPP_XOR1>(fs);
+    fs += dpp_f<DPP_XOR2>(fs);
+    if (m == 0) *reinterpret_cast<float2 *>(step + TOK * 128 + (t * 4 + j) * 8) = make_float2(d, d * fs);
 }
 
 // ------------------------------------------------------------------------------------------
-// per-type weight fragment of one step for lane (row r, k-group g)
-//   load  : issue the loads (no use of the data: the next step's loads stay in flight)
-//   frags : the 8 int8 weights of k-group g of every MFMA of the step
-//   sc   : the row scale(s) this lane publishes for the epilogue
+// helpers
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ void swap32(uint32_t &lo_src, uint32_t &hi_dst) {
     // upper 32 lanes of hi_dst <-> lower 32 lanes of lo_src
@@ -142,86 +135,173 @@ template <typename V> __device__ __forceinline__ void pin(V &v) {
     for (int i = 0; i < (int)(sizeof(V) / 4); ++i) asm volatile("" : "+v"(u[i]));
 }
 
-template <int T> struct MmaW;
+constexpr uint32_t NIB = 0x0f0f0f0fu;
 
-// Q4_0: lane g loads block 4s + g of its row (a 20-byte window from the dword floor)
-template <> struct MmaW<T_Q4_0> {
-    static constexpr int NMF = 4, NSC = 1;
-    uint32_t W[5];
-    uint32_t sh;
-    __device__ inline void load(const uint8_t *row, int s, int g, int nblk) {
-        const uint8_t *p = row + (size_t)min(4 * s + g, nblk - 1) * 18;
-        sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
-        const uint8_t *pa = p - sh;
-        const uint4 w = *reinterpret_cast<const uint4 *>(pa);
-        W[0] = w.x; W[1] = w.y; W[2] = w.z; W[3] = w.w;
-        W[4] = *reinterpret_cast<const uint32_t *>(pa + 16);
-    }
-    __device__ inline void frags(long (&A)[NMF]) {
-        pin(W);
-        uint32_t q[4];
+// Q4_0 / Q8_0 with 8 tokens: lane g loaded block g whole; lane g needs half g & 1 of block
+// 2p + (g >> 1) for pair p. With X = the lane's lower half and Y = its upper half (n dwords
+// each), two swaps leave pair 0's half in X and pair 1's in Y:
+//   X = L0 L1 L2 L3, Y = H0 H1 H2 H3  --swap16-->  X = L0 H0 L2 H2, Y = L1 H1 L3 H3
+//                                     --swap32-->  X = L0 H0 L1 H1, Y = L2 H2 L3 H3
+template <int n> __device__ __forceinline__ void halves_to_pairs(uint32_t (&X)[n], uint32_t (&Y)[n]) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) q[k] = sh ? W[k + 1] : align2(W[k + 1], W[k]);
-        transpose4(q);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) A[j] = pack2(sub8_bytes(q[j] & 0x0f0f0f0fu), sub8_bytes((q[j] >> 4) & 0x0f0f0f0fu));
+    for (int k = 0; k < n; ++k) {
+        swap16(Y[k], X[k]);
+        swap32(Y[k], X[k]);
     }
-    __device__ inline void sc(float *o) const { o[0] = h2f((uint16_t)(W[0] >> (8 * sh))); }
+}
+
+typedef uint32_t mma_u4 __attribute__((ext_vector_type(4)));
+typedef uint32_t mma_u2 __attribute__((ext_vector_type(2)));
+typedef float mma_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void bl16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t *o) {
+    const mma_u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = v[3];
+}
+__device__ __forceinline__ void bl8(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t *o) {
+    const mma_u2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    o[0] = v[0]; o[1] = v[1];
+}
+
+// ------------------------------------------------------------------------------------------
+// per-type weights of one step for lane (row r, k-group g), loaded through a per-step buffer
+// descriptor (base = the tile at the step's first byte; no records at all for a step past K,
+// so those loads return zeros) at offsets fixed per lane:
+//   lanes : the lane's offsets in the tile (row r, k-group g, half h of a K-quant super-block)
+//   load  : issue the loads (no use of the data: the next steps' loads stay in flight)
+//   frags : A[p][q], the int8 weights of MFMA q of pair p (TOK 4: p = 0, q = chunk of the
+//           lane's block; TOK 8: q = chunk 2 (g & 1) + q of block 2p + (g >> 1))
+//   sc    : the scale(s) of block g of the step (sub-block 4h + g for the K-quants)
+// Q4_0 / Q8_0 blocks are 2-byte aligned: their qs come from a dword-aligned window and a
+// per-lane funnel shift (unaligned 16-byte loads cost about twice the memory-pipeline time).
+// ------------------------------------------------------------------------------------------
+struct MmaLanes {
+    uint32_t a, b, c;
 };
+template <int T, int TOK> struct MmaW;
 
-// Q8_0: lane g loads block 4s + g (a 36-byte window); k-group g' = qs dwords 2g', 2g'+1
-template <> struct MmaW<T_Q8_0> {
-    static constexpr int NMF = 4, NSC = 1;
-    uint32_t W[9];
-    uint32_t sh;
-    __device__ inline void load(const uint8_t *row, int s, int g, int nblk) {
-        const uint8_t *p = row + (size_t)min(4 * s + g, nblk - 1) * 34;
-        sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
-        const uint8_t *pa = p - sh;
-        const uint4 w0 = *reinterpret_cast<const uint4 *>(pa);
-        const uint4 w1 = *reinterpret_cast<const uint4 *>(pa + 16);
-        W[0] = w0.x; W[1] = w0.y; W[2] = w0.z; W[3] = w0.w;
-        W[4] = w1.x; W[5] = w1.y; W[6] = w1.z; W[7] = w1.w;
-        W[8] = *reinterpret_cast<const uint32_t *>(pa + 32);
+template <int TOK> struct MmaW<T_Q4_0, TOK> {
+    static constexpr int NSC = 1;
+    uint32_t V[5], d;
+    int h;   // (unused)
+    __device__ static uint32_t step_off(int s) { return 72u * s; }
+    // a = the block, b = the dword floor of its qs (a 20-byte window), c = the qs offset in it
+    __device__ static MmaLanes lanes(int r, int g, int, uint32_t nb01, uint32_t mis) {
+        const uint32_t blk = r * nb01 + 18u * g, o = (mis + blk + 2) & 3;
+        return {blk, blk + 2 - o, o};
     }
-    __device__ inline void frags(long (&A)[NMF]) {
-        pin(W);
-        uint32_t qe[4], qo[4];
+    __device__ inline void load(__amdgpu_buffer_rsrc_t rs, const MmaLanes &lo) {
+        bl16(rs, lo.b, V);
+        V[4] = __builtin_amdgcn_raw_buffer_load_b32(rs, lo.b + 16, 0, 0);
+        d = __builtin_amdgcn_raw_buffer_load_b16(rs, lo.a, 0, 0);
+    }
+    __device__ inline void frags(long (&A)[4], int, const MmaLanes &lo) {
+        pin(V);
+        uint32_t q[4];   // qs dwords
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            qe[k] = sh ? W[2 * k + 1] : align2(W[2 * k + 1], W[2 * k]);
-            qo[k] = sh ? W[2 * k + 2] : align2(W[2 * k + 2], W[2 * k + 1]);
+        for (int k = 0; k < 4; ++k) q[k] = __builtin_amdgcn_alignbyte(V[k + 1], V[k], lo.c);
+        if constexpr (TOK == 4) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int a = m >> 1, sft = 4 * (m & 1);
+                A[m] = pack2((q[2 * a] >> sft) & NIB, (q[2 * a + 1] >> sft) & NIB);
+            }
+        } else {
+            uint32_t X[2] = {q[0], q[1]}, Y[2] = {q[2], q[3]};
+            halves_to_pairs(X, Y);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                A[h] = pack2((X[0] >> (4 * h)) & NIB, (X[1] >> (4 * h)) & NIB);
+                A[2 + h] = pack2((Y[0] >> (4 * h)) & NIB, (Y[1] >> (4 * h)) & NIB);
+            }
         }
-        transpose4(qe);
-        transpose4(qo);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) A[j] = pack2(qe[j], qo[j]);
     }
-    __device__ inline void sc(float *o) const { o[0] = h2f((uint16_t)(W[0] >> (8 * sh))); }
+    __device__ inline void sc(float *o, int) {
+        pin(d);
+        o[0] = h2f((uint16_t)d);
+    }
 };
 
-// Q4_K: step s = half h = s & 1 of super-block s >> 1: sub-blocks 4h .. 4h+3 are the low / high
-// nibbles of qs chunks 2h and 2h+1; lane g loads its 8 bytes of each chunk and the 16-B header
-template <> struct MmaW<T_Q4_K> {
-    static constexpr int NMF = 4, NSC = 2;
-    uint32_t H[4], QA[2], QB[2];
-    int h;
-    __device__ inline void load(const uint8_t *row, int s, int g, int) {
-        const uint8_t *p = row + (size_t)(s >> 1) * 144;
-        h = s & 1;
-        ld16(p, H);
-        ld8(p + 16 + 64 * h + 8 * g, QA);
-        ld8(p + 48 + 64 * h + 8 * g, QB);
+// Q8_0: chunk m = qs dwords 2 (m >> 1) + 4 (m & 1)
+template <int TOK> struct MmaW<T_Q8_0, TOK> {
+    static constexpr int NSC = 1;
+    uint32_t V[9], d;
+    int h;   // (unused)
+    __device__ static uint32_t step_off(int s) { return 136u * s; }
+    __device__ static MmaLanes lanes(int r, int g, int, uint32_t nb01, uint32_t mis) {
+        const uint32_t blk = r * nb01 + 34u * g, o = (mis + blk + 2) & 3;
+        return {blk, blk + 2 - o, o};
     }
-    __device__ inline void frags(long (&A)[NMF]) {
-        pin(H);
-        pin(QA);
-        pin(QB);
+    __device__ inline void load(__amdgpu_buffer_rsrc_t rs, const MmaLanes &lo) {
+        bl16(rs, lo.b, V);
+        bl16(rs, lo.b + 16, V + 4);
+        V[8] = __builtin_amdgcn_raw_buffer_load_b32(rs, lo.b + 32, 0, 0);
+        d = __builtin_amdgcn_raw_buffer_load_b16(rs, lo.a, 0, 0);
+    }
+    __device__ inline void frags(long (&A)[4], int, const MmaLanes &lo) {
+        pin(V);
+        uint32_t q[8];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t *Q = j < 2 ? QA : QB;
-            const int shf = (j & 1) * 4;
-            A[j] = pack2((Q[0] >> shf) & 0x0f0f0f0fu, (Q[1] >> shf) & 0x0f0f0f0fu);
+        for (int k = 0; k < 8; ++k) q[k] = __builtin_amdgcn_alignbyte(V[k + 1], V[k], lo.c);
+        if constexpr (TOK == 4) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int o = 2 * (m >> 1) + 4 * (m & 1);
+                A[m] = pack2(q[o], q[o + 1]);
+            }
+        } else {
+            // half a = chunks 2a, 2a + 1 = dwords {2a, 2a + 1, 2a + 4, 2a + 5}
+            uint32_t X[4] = {q[0], q[1], q[4], q[5]}, Y[4] = {q[2], q[3], q[6], q[7]};
+            halves_to_pairs(X, Y);
+            A[0] = pack2(X[0], X[1]);
+            A[1] = pack2(X[2], X[3]);
+            A[2] = pack2(Y[0], Y[1]);
+            A[3] = pack2(Y[2], Y[3]);
+        }
+    }
+    __device__ inline void sc(float *o, int) {
+        pin(d);
+        o[0] = h2f((uint16_t)d);
+    }
+};
+
+// Q4_K: step s = half h = s & 1 of super-block s >> 1 (h is the wave's: s = wave + 16 i); sub-block
+// 4h + b is nibble b & 1 of qs run 2h + (b >> 1) (32 B at 16 + 32 (2h + (b >> 1))); every lane
+// loads the 16-B header.
+//   TOK 4: lane g loads the 32-B run of its sub-block g;
+//   TOK 8: lane g loads bytes 8 (g & 1) + 16 q .. + 8 (q = 0, 1) of run 2h + p for both pairs
+template <int TOK> struct MmaW<T_Q4_K, TOK> {
+    static constexpr int NSC = 2;
+    uint32_t H[4], Q[8];
+    int h;
+    __device__ static uint32_t step_off(int s) { return 144u * (uint32_t)(s >> 1); }
+    __device__ static MmaLanes lanes(int r, int g, int h, uint32_t nb01, uint32_t) {
+        const uint32_t row = r * nb01;
+        return {row, row + 16 + 32 * (2 * h + (TOK == 4 ? (g >> 1) : 0)) + (TOK == 4 ? 0 : 8 * (g & 1)), 0};
+    }
+    __device__ inline void load(__amdgpu_buffer_rsrc_t rs, const MmaLanes &lo) {
+        bl16(rs, lo.a, H);
+        if constexpr (TOK == 4) {
+            bl16(rs, lo.b, Q);
+            bl16(rs, lo.b + 16, Q + 4);
+        } else {
+#pragma unroll
+            for (int pq = 0; pq < 4; ++pq) bl8(rs, lo.b + 32 * (pq >> 1) + 16 * (pq & 1), Q + 2 * pq);
+        }
+    }
+    __device__ inline void frags(long (&A)[4], int g, const MmaLanes &) {
+        pin(H);
+        pin(Q);
+        if constexpr (TOK == 4) {
+            const int sft = 4 * (g & 1);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int o = 2 * (m >> 1) + 4 * (m & 1);
+                A[m] = pack2((Q[o] >> sft) & NIB, (Q[o + 1] >> sft) & NIB);
+            }
+        } else {
+            const int sft = 4 * (g >> 1);
+#pragma unroll
+            for (int pq = 0; pq < 4; ++pq) A[pq] = pack2((Q[2 * pq] >> sft) & NIB, (Q[2 * pq + 1] >> sft) & NIB);
         }
     }
     // d * sc and dmin * m of sub-block 4h + g
@@ -235,31 +315,52 @@ template <> struct MmaW<T_Q4_K> {
     }
 };
 
-// Q5_K: as Q4_K plus the 5th bits: qh byte 8g + i, bit (4h + j) for sub-block 4h + j
-template <> struct MmaW<T_Q5_K> {
-    static constexpr int NMF = 4, NSC = 2;
-    uint32_t H[4], QH[2], QA[2], QB[2];
+// Q5_K: as Q4_K (runs at 48 + 32 c) plus the 5th bits: qh byte e (32 B at 16), bit 4h + b for
+// sub-block 4h + b
+template <int TOK> struct MmaW<T_Q5_K, TOK> {
+    static constexpr int NSC = 2;
+    uint32_t H[4], Q[8], QH[TOK == 4 ? 8 : 4];
     int h;
-    __device__ inline void load(const uint8_t *row, int s, int g, int) {
-        const uint8_t *p = row + (size_t)(s >> 1) * 176;
-        h = s & 1;
-        ld16(p, H);
-        ld8(p + 16 + 8 * g, QH);
-        ld8(p + 48 + 64 * h + 8 * g, QA);
-        ld8(p + 80 + 64 * h + 8 * g, QB);
+    __device__ static uint32_t step_off(int s) { return 176u * (uint32_t)(s >> 1); }
+    __device__ static MmaLanes lanes(int r, int g, int h, uint32_t nb01, uint32_t) {
+        const uint32_t row = r * nb01;
+        return {row, row + 48 + 32 * (2 * h + (TOK == 4 ? (g >> 1) : 0)) + (TOK == 4 ? 0 : 8 * (g & 1)),
+                row + 16 + (TOK == 4 ? 0 : 8 * (g & 1))};
     }
-    __device__ inline void frags(long (&A)[NMF]) {
-        pin(H);
-        pin(QH);
-        pin(QA);
-        pin(QB);
+    __device__ inline void load(__amdgpu_buffer_rsrc_t rs, const MmaLanes &lo) {
+        bl16(rs, lo.a, H);
+        if constexpr (TOK == 4) {
+            bl16(rs, lo.b, Q);
+            bl16(rs, lo.b + 16, Q + 4);
+            bl16(rs, lo.c, QH);
+            bl16(rs, lo.c + 16, QH + 4);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t *Q = j < 2 ? QA : QB;
-            const int shf = (j & 1) * 4, hb = 4 * h + j;
-            const uint32_t lo = ((Q[0] >> shf) & 0x0f0f0f0fu) | (((QH[0] >> hb) & 0x01010101u) << 4);
-            const uint32_t hi = ((Q[1] >> shf) & 0x0f0f0f0fu) | (((QH[1] >> hb) & 0x01010101u) << 4);
-            A[j] = pack2(lo, hi);
+            for (int pq = 0; pq < 4; ++pq) bl8(rs, lo.b + 32 * (pq >> 1) + 16 * (pq & 1), Q + 2 * pq);
+            bl8(rs, lo.c, QH);
+            bl8(rs, lo.c + 16, QH + 2);
+        }
+    }
+    __device__ inline void frags(long (&A)[4], int g, const MmaLanes &) {
+        pin(H);
+        pin(Q);
+        pin(QH);
+        if constexpr (TOK == 4) {
+            const int sft = 4 * (g & 1), hb = 4 * h + g;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int o = 2 * (m >> 1) + 4 * (m & 1);
+                A[m] = pack2(((Q[o] >> sft) & NIB) | (((QH[o] >> hb) & 0x01010101u) << 4),
+                             ((Q[o + 1] >> sft) & NIB) | (((QH[o + 1] >> hb) & 0x01010101u) << 4));
+            }
+        } else {
+            const int sft = 4 * (g >> 1);
+#pragma unroll
+            for (int pq = 0; pq < 4; ++pq) {
+                const int hb = 4 * h + 2 * (pq >> 1) + (g >> 1), o = 2 * (pq & 1);
+                A[pq] = pack2(((Q[2 * pq] >> sft) & NIB) | (((QH[o] >> hb) & 0x01010101u) << 4),
+                              ((Q[2 * pq + 1] >> sft) & NIB) | (((QH[o + 1] >> hb) & 0x01010101u) << 4));
+            }
         }
     }
     __device__ inline void sc(float *o, int g) const {
@@ -272,264 +373,213 @@ template <> struct MmaW<T_Q5_K> {
     }
 };
 
-// Q6_K: step s = half h of super-block s >> 1; sub-block q of the half: low 4 bits from
-// ql[64h + 32 (q & 1) + l] (nibble q >> 1), high 2 bits from qh[32h + l] >> 2q; scales per 16
-// (k-groups 0-1 / 2-3), so each sub-block is two MFMAs with the other run's weights zeroed
-// (dequantize_row_q6_K, reference src/ggml-quants.c:1762)
-template <> struct MmaW<T_Q6_K> {
-    static constexpr int NMF = 8, NSC = 2;
-    // 4-byte-aligned windows from the dword floor of the (2-byte aligned) super-block, as
-    // mmvq_impl.h's Frag<Q6_K>: ql (two 12-B windows), qh (12 B), scales + d (20 B)
-    uint32_t L0[3], L1[3], QH[3], RS[5];
-    uint32_t sh;
-    int h, g;
-    __device__ static inline void ld12(const uint8_t *pa, uint32_t *o) {
-        const uint2 w = *reinterpret_cast<const uint2 *>(pa);
-        o[0] = w.x; o[1] = w.y;
-        o[2] = *reinterpret_cast<const uint32_t *>(pa + 8);
-    }
-    __device__ inline void load(const uint8_t *row, int s, int g_, int) {
-        const uint8_t *p = row + (size_t)(s >> 1) * 210;
-        h = s & 1;
-        g = g_;
-        sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
-        const uint8_t *pa = p - sh;
-        ld12(pa + 64 * h + 8 * g, L0);
-        ld12(pa + 64 * h + 32 + 8 * g, L1);
-        ld12(pa + 128 + 32 * h + 8 * g, QH);
-        const uint4 w = *reinterpret_cast<const uint4 *>(pa + 192);
-        RS[0] = w.x; RS[1] = w.y; RS[2] = w.z; RS[3] = w.w;
-        RS[4] = *reinterpret_cast<const uint32_t *>(pa + 208);
-    }
-    __device__ inline void frags(long (&A)[NMF]) {
-        pin(L0);
-        pin(L1);
-        pin(QH);
-        pin(RS);
-        uint32_t l0[2], l1[2], qh[2];
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            l0[k] = __builtin_amdgcn_alignbyte(L0[k + 1], L0[k], sh);
-            l1[k] = __builtin_amdgcn_alignbyte(L1[k + 1], L1[k], sh);
-            qh[k] = __builtin_amdgcn_alignbyte(QH[k + 1], QH[k], sh);
-        }
-        // MFMA m = 2 q + run; this lane's k-group belongs to run g >> 1, the other run is zero
-#pragma unroll
-        for (int m = 0; m < NMF; ++m) {
-            const int q = m >> 1, run = m & 1;
-            const uint32_t keep = 0u - (uint32_t)(run == (g >> 1));   // (a mask, not a branch)
-            const uint32_t *L = (q & 1) ? l1 : l0;
-            const int shf = (q >> 1) * 4, hs = 2 * q;
-            const uint32_t lo = ((L[0] >> shf) & 0x0f0f0f0fu) | (((qh[0] >> hs) & 0x03030303u) << 4);
-            const uint32_t hi = ((L[1] >> shf) & 0x0f0f0f0fu) | (((qh[1] >> hs) & 0x03030303u) << 4);
-            A[m] = pack2(sub32_bytes(lo) & keep, sub32_bytes(hi) & keep);
-        }
-    }
-    // d * sc[8h + 2g + run] for run 0, 1 (sub-block q = g): bytes sh + 8h + 2g of the scale window
-    __device__ inline void sc(float *o, int) const {
-        const uint32_t ob = sh + 8 * h + 2 * g;   // even, <= 16: both bytes in one dword
-        const uint32_t wi = ob >> 2;
-        const uint32_t wd = wi == 0 ? RS[0] : wi == 1 ? RS[1] : wi == 2 ? RS[2] : wi == 3 ? RS[3] : RS[4];
-        const uint32_t sc2 = wd >> (8 * (ob & 3));
-        const float d = h2f((uint16_t)(RS[4] >> (8 * sh)));
-        o[0] = d * (float)(int8_t)(sc2 & 0xff);
-        o[1] = d * (float)(int8_t)((sc2 >> 8) & 0xff);
-    }
-};
-
 // ------------------------------------------------------------------------------------------
-// weight sets per wave (DEPTH - 1 steps in flight; the activations come from LDS): as deep as
-// the register budget of 16 waves per CU allows without spills
-template <int T> __host__ __device__ constexpr int mma_depth() {
-    return T == T_Q4_0 ? 5 : (T == T_Q8_0 || T == T_Q4_K) ? 3 : 2;
-}
+// step sets in flight per wave (D - 1 steps ahead), within the 128 VGPRs of 16 waves per CU
+#ifdef MMA_D
+template <int T, int TOK> __host__ __device__ constexpr int mma_depth() { return MMA_D; }   // (measurement builds)
+#else
+template <int T, int TOK> __host__ __device__ constexpr int mma_depth() { return T == T_Q5_K && TOK == 4 ? 2 : 3; }
+#endif
 
-// One launch, no pre-pass. Workgroup (row group rg, K part kp, slice z) = 8 waves, wave w on the
-// 16-row tile 8 rg + w, all waves over the same K part:
-//  1. the workgroup quantizes its K part of the src1 columns into LDS (records of mma_quant),
-//     while the first weight steps of every wave are already in flight;
-//  2. each wave streams its tile's weights over the K part, DEPTH - 1 steps ahead in registers,
-//     one MFMA per 32-block against the LDS records;
-//  3. with one K part the wave stores its tile; otherwise it stores a partial (write-through
-//     sc1 stores), the workgroup adds one to its row group's counter (agent scope) and the
-//     workgroup that arrives last sums the parts in K order and stores dst
-//     (MI355X_MICROARCH.md inter-workgroup visibility, the counter row), then re-arms it.
 template <int D, typename F, int... Is>
 __device__ __forceinline__ void mma_run_steps(F &&f, std::integer_sequence<int, Is...>) {
     (f(std::integral_constant<int, Is % D>{}, Is), ...);
 }
 
-template <int T, int TOK, int D, int NSTEP, bool XA>
-__global__ __launch_bounds__(8 * WAVE) void mmvq_mma_kernel(const MmArgs a, int n_steps, int n_kp, float *__restrict__ part,
-                                                          int *__restrict__ cnt) {
-    constexpr int NMF = MmaW<T>::NMF;
-    constexpr int NSC = MmaW<T>::NSC;
-    constexpr int RB = mma_rec_bytes<T>();
-    constexpr int SB = mma_step_bytes<T, TOK>();
-    constexpr bool SX = RB == 160;
-    extern __shared__ __align__(16) uint8_t xsm[];   // the K part's records: steps * SB bytes
-    __shared__ __align__(16) float wsc[8][16 * 4 * NSC];
-    __shared__ int order;
-
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int r = lane & 15, g = lane >> 4;
-    const int rg = blockIdx.x, kp = blockIdx.y, z = blockIdx.z;
+// the columns' images once per call: grid (steps, slices), TOK * 16 threads, thread (t, j, m)
+// quantizes chunk m of block j of column t (zeros past K and M)
+template <int TOK, bool XA>
+__global__ __launch_bounds__(TOK * 16) void mma_prequant(const MmArgs a, uint8_t *__restrict__ img) {
+    const int s = blockIdx.x, z = blockIdx.y;
     const int i12 = z % a.ne12, i13 = z / a.ne12;
-    const int k0 = kp * NSTEP, k1 = min(n_steps, k0 + NSTEP);   // this K part's steps (NSTEP per part)
-    const int tile = rg * 8 + wave;
-    const int row0 = tile * 16;
-    const uint8_t *wrow = a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03 +
-                          (int64_t)min(row0 + r, a.N - 1) * a.nb01;
-    const int nblk = a.K / QT<T>::blck;
-    const int tl = r & (TOK - 1);   // this lane's column (lanes past TOK repeat a column)
-
-    // 1. weight prologue, then the K part's activations into LDS (16-B loads: the 8 values of a
-    // unit are two runs of 4 consecutive floats in either element order)
-    MmaW<T> F[D];
-#pragma unroll
-    for (int d = 0; d < D - 1; ++d)
-        if constexpr (!(MMA_EXP & 2)) F[d].load(wrow, min(k0 + d, k1 - 1), g, nblk);
-    {
-        const float *xz = reinterpret_cast<const float *>(a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13);
-        const int units = (k1 - k0) * 4 * TOK * 4;   // (step, t, j, g), g fastest
-        constexpr int QU = 4;   // units per thread whose loads are issued together
-        for (int u0 = threadIdx.x; u0 < units; u0 += QU * 8 * WAVE) {
-            float v[QU][8];
-#pragma unroll
-            for (int q = 0; q < QU; ++q) {
-                const int u = min(u0 + q * 8 * WAVE, units - 1);
-                const int j = (u >> 2) & 3, t = (u >> 4) % TOK, sl = (u >> 4) / TOK;
-                const float *col = reinterpret_cast<const float *>(reinterpret_cast<const uint8_t *>(xz) + (int64_t)min(t, a.M - 1) * a.nb11);
-                if constexpr (MMA_EXP & 1) {
-                    for (int c = 0; c < 8; ++c) v[q][c] = 0.f;
-                    (void)col;
-                } else {
-                    mma_xload<T, XA>(a, col, k0 + sl, j, u & 3, v[q]);
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < QU; ++q) {
-                // (units past the end, whole quads since units % 4 == 0, quantize the clamped
-                // repeat without storing it: a quad of repeats has the wrong amax)
-                const int u = min(u0 + q * 8 * WAVE, units - 1);
-                const int j = (u >> 2) & 3, t = (u >> 4) % TOK, sl = (u >> 4) / TOK;
-                mma_quant<T, SX>(a, v[q], k0 + sl, j, t, u & 3, xsm + sl * SB + t * RB, u0 + q * 8 * WAVE < units);
-            }
-        }
+    const int m = threadIdx.x & 3, j = (threadIdx.x >> 2) & 3, t = threadIdx.x >> 4;
+    const float *col = reinterpret_cast<const float *>(a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13 +
+                                                       (int64_t)min(t, a.M - 1) * a.nb11);
+    float v[8];
+    if constexpr (MMA_EXP & 1) {
+        for (int c = 0; c < 8; ++c) v[c] = 0.f;
+    } else {
+        mma_xload<XA>(a, col, s, j, m, v);
     }
-    lds_barrier();
+    mma_quant<TOK>(a, v, s, j, t, m, img + ((int64_t)z * gridDim.x + s) * mma_step_bytes<TOK>());
+}
 
-    // 2. the weight stream: step s computes from set s % D while the loads of s + D - 1 go into
-    // the set step s - 1 used (clamped repeats past k1 - 1); the step count is padded to a
-    // multiple of D with repeats that add nothing (live = 0). The scheduling barriers keep each
-    // step's loads ahead of the previous step's arithmetic, pin() keeps that arithmetic behind.
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    auto compute = [&](MmaW<T> &w, int s, float live) __attribute__((always_inline)) {
-        long A[NMF];
-        w.frags(A);
-        const uint8_t *rec = xsm + (s - k0) * SB + tl * RB;
-        const uint4 c0 = *reinterpret_cast<const uint4 *>(rec + g * 32);
-        const uint4 c1 = *reinterpret_cast<const uint4 *>(rec + g * 32 + 16);
-        const float4 xdv = *reinterpret_cast<const float4 *>(rec + 128);
-        float4 sxv = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (SX) sxv = *reinterpret_cast<const float4 *>(rec + 144);
-        const long xb[4] = {pack2(c0.x, c0.y), pack2(c0.z, c0.w), pack2(c1.x, c1.y), pack2(c1.z, c1.w)};
-        i32x4_t R[NMF];
-        const i32x4_t zero = {0, 0, 0, 0};
+// Workgroup = one 16-row tile, 16 waves, wave w the steps w, w + 16, w + 32, ... of K, so that
+// the workgroup's loads in flight are 16 consecutive steps of each row (steps past K load through
+// empty descriptors: zero weights, zero columns): straight-line code, no loop, so no register
+// set crosses a back-edge (the copies the allocator puts on a back-edge move sets whose loads
+// are still in flight, and each copy waits for its load). Each step loads its weights and its
+// column codes and scales D - 1 steps ahead; all addresses are per-lane constants plus the
+// step's descriptor base (scalar arithmetic).
+template <int T, int TOK, int NSTEP>
+__global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a, const uint8_t *__restrict__ img, int n_steps) {
+    using W = MmaW<T, TOK>;
+    constexpr int G = 16 / TOK;   // block groups per MFMA
+    constexpr int L = 4 / G;      // k-groups per block group
+    constexpr int P = 4 / G;      // MFMA outputs per step
+    constexpr int Qn = G;         // MFMAs per output
+    constexpr int NSC = W::NSC;
+    constexpr int SB = mma_step_bytes<TOK>();
+    constexpr int D = mma_depth<T, TOK>();
+    __shared__ __align__(16) float wsc[MMA_KS][4 * NSC * 16];   // [wave][block][k][row]
+    __shared__ __align__(16) float red[MMA_KS][4 * TOK * 4];
+    extern __shared__ __align__(16) uint8_t xl[];   // [steps][SB] column image, then 128 zero bytes
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int c = lane & 15, g = lane >> 4;
+    const int z = blockIdx.y;
+    const int i12 = z % a.ne12, i13 = z / a.ne12;
+    const int row0 = blockIdx.x * 16;
+    const uint8_t *wtile = a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03 + (int64_t)row0 * a.nb01;
+    const uint32_t nb01 = (uint32_t)a.nb01;
+    const uint32_t tile_bytes = (uint32_t)(min(16, a.N - row0) - 1) * nb01 + (uint32_t)(a.K / QT<T>::blck) * QT<T>::bytes;
+    const MmaLanes lo = W::lanes(c, g, wave & 1, nb01, (uint32_t)(reinterpret_cast<uintptr_t>(wtile) & 3));
+    auto wrs = [&](int s) __attribute__((always_inline)) {
+        const uint32_t so = W::step_off(s);
+        return __builtin_amdgcn_make_buffer_rsrc((void *)(wtile + so), 0, s < n_steps ? tile_bytes - so : 0u, MMA_RSRC_W3);
+    };
+    // the slice's column image, staged in LDS once: 16-B pieces, thread t the pieces t + 1024 k
+    // (issued before the weight prefetch, so the LDS writes wait for these loads only)
+    const uint32_t nbx = (uint32_t)(n_steps * SB);
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(img + (int64_t)z * nbx), 0, nbx, MMA_RSRC_W3);
+    constexpr int NP = (MMA_KS * NSTEP * SB + 16383) / 16384;
+    uint32_t stg[NP][4];
+    if constexpr (!(MMA_EXP & 1)) {
 #pragma unroll
-        for (int m = 0; m < NMF; ++m) R[m] = __builtin_amdgcn_mfma_i32_16x16x32_i8(A[m], xb[NMF == 8 ? m >> 1 : m], zero, 0, 0, 0);
-        // publish this lane's row scales [r][j = g][NSC]; read those of rows 4G + i (G = g)
-        float o[NSC];
-        if constexpr (NSC == 1) w.sc(o);
-        else w.sc(o, g);
-        float *ws = wsc[wave];
+        for (int k = 0; k < NP; ++k) bl16(xr, threadIdx.x * 16 + k * 16384, stg[k]);
+    }
+    // B role: column c = token bt of block group bg; codes only where k-group g is in bg's range
+    // (the other lanes read the zero bytes after the image, at a fixed address)
+    const int bt = c % TOK, bg = c / TOK;
+    const bool xlive = g / L == bg;
+    const uint32_t xc = xlive ? (uint32_t)((bt * 4 + bg) * 32 + (g % L) * Qn * 8) : nbx;
+    const uint32_t xstep = xlive ? (uint32_t)SB : 0u;
+    const uint32_t xsc = (uint32_t)(TOK * 128 + (bt * 4 + bg) * 8);
+    auto step_of = [&](int i) { return wave + MMA_KS * i; };
+
+    struct Xf {
+        uint32_t c[8];   // codes: TOK 4: 4 chunks of 8 B; TOK 8: pair p's 2 chunks at 4p
+        float2 s[P];     // {d, d * sum(q)} of the output lane's (token, block) per pair
+    };
+    // (steps past K read the last real step: finite values against zero weights)
+    auto load_x = [&](Xf &x, int s) __attribute__((always_inline)) {
+        const uint32_t sl = (uint32_t)min(s, n_steps - 1);
+        const uint8_t *cp = xl + xc + sl * xstep;
+        const uint8_t *sp = xl + xsc + sl * SB;
 #pragma unroll
-        for (int k = 0; k < NSC; ++k) ws[(r * 4 + g) * NSC + k] = o[k];
-        const float xd[4] = {xdv.x, xdv.y, xdv.z, xdv.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            float c;
-            const float *rs = ws + (4 * g + i) * 4 * NSC;
-            if constexpr (T == T_Q4_0 || T == T_Q8_0) {
-                const float4 dw = *reinterpret_cast<const float4 *>(rs);
-                c = (dw.x * xd[0]) * (float)R[0][i] + (dw.y * xd[1]) * (float)R[1][i] +
-                    (dw.z * xd[2]) * (float)R[2][i] + (dw.w * xd[3]) * (float)R[3][i];
-            } else if constexpr (T == T_Q6_K) {
-                const float4 lo = *reinterpret_cast<const float4 *>(rs), hi = *reinterpret_cast<const float4 *>(rs + 4);
-                // [q][run]: lo = q0r0 q0r1 q1r0 q1r1, hi = q2r0 q2r1 q3r0 q3r1
-                c = xd[0] * (lo.x * (float)R[0][i] + lo.y * (float)R[1][i]) +
-                    xd[1] * (lo.z * (float)R[2][i] + lo.w * (float)R[3][i]) +
-                    xd[2] * (hi.x * (float)R[4][i] + hi.y * (float)R[5][i]) +
-                    xd[3] * (hi.z * (float)R[6][i] + hi.w * (float)R[7][i]);
+        for (int p = 0; p < P; ++p) {
+            if constexpr (TOK == 4) {
+                const uint4 v0 = *reinterpret_cast<const uint4 *>(cp), v1 = *reinterpret_cast<const uint4 *>(cp + 16);
+                x.c[0] = v0.x; x.c[1] = v0.y; x.c[2] = v0.z; x.c[3] = v0.w;
+                x.c[4] = v1.x; x.c[5] = v1.y; x.c[6] = v1.z; x.c[7] = v1.w;
             } else {
-                const float4 lo = *reinterpret_cast<const float4 *>(rs), hi = *reinterpret_cast<const float4 *>(rs + 4);
-                // [j][sc, m]: lo = sc0 m0 sc1 m1, hi = sc2 m2 sc3 m3
-                c = (lo.x * (xd[0] * (float)R[0][i]) - lo.y * sxv.x) + (lo.z * (xd[1] * (float)R[1][i]) - lo.w * sxv.y) +
-                    (hi.x * (xd[2] * (float)R[2][i]) - hi.y * sxv.z) + (hi.z * (xd[3] * (float)R[3][i]) - hi.w * sxv.w);
+                const uint4 v = *reinterpret_cast<const uint4 *>(cp + p * G * 32);
+                x.c[4 * p] = v.x; x.c[4 * p + 1] = v.y; x.c[4 * p + 2] = v.z; x.c[4 * p + 3] = v.w;
             }
-            acc[i] = __builtin_fmaf(live, c, acc[i]);
+            x.s[p] = *reinterpret_cast<const float2 *>(sp + p * G * 8);
         }
     };
-    // straight-line: NSTEP steps (the last part's steps past k1 are clamped repeats with
-    // live = 0), no loop, so no register set crosses a back-edge (the copies the register
-    // allocator puts on a back-edge move sets whose loads are still in flight, and each copy
-    // waits for its load: one memory latency per step)
+    mma_f2 acc[2] = {{0.f, 0.f}, {0.f, 0.f}};   // rows 4g + {0, 1}, {2, 3}
+    auto compute = [&](W &w, Xf &x) __attribute__((always_inline)) {
+        long A[4];
+        w.frags(A, g, lo);
+        pin(x.c);
+        pin(x.s);
+        // publish this lane's block-g scales, [block g][k][row c]
+        float o[NSC];
+        w.sc(o, g);
+        float *ws = wsc[wave];
+#pragma unroll
+        for (int k = 0; k < NSC; ++k) ws[(g * NSC + k) * 16 + c] = o[k];
+        const i32x4_t zero = {0, 0, 0, 0};
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            i32x4_t R = zero;
+#pragma unroll
+            for (int q = 0; q < Qn; ++q) {
+                const int ci = TOK == 4 ? 2 * q : 4 * p + 2 * q;
+                R = __builtin_amdgcn_mfma_i32_16x16x32_i8(A[p * Qn + q], pack2(x.c[ci], x.c[ci + 1]), R, 0, 0, 0);
+            }
+            // outputs: rows 4g + i, token bt, block p G + bg (packed fp32, two rows at a time)
+            const float *rs = ws + (p * G + bg) * NSC * 16 + 4 * g;
+            const mma_f2 xd = {x.s[p].x, x.s[p].x};
+            const mma_f2 r[2] = {{(float)R[0], (float)R[1]}, {(float)R[2], (float)R[3]}};
+            if constexpr (T == T_Q4_0 || T == T_Q8_0) {
+                const float4 dw = *reinterpret_cast<const float4 *>(rs);
+                const mma_f2 dv[2] = {{dw.x, dw.y}, {dw.z, dw.w}};
+                const float o8 = T == T_Q4_0 ? -8.f * x.s[p].y : 0.f;
+                const mma_f2 off = {o8, o8};
+#pragma unroll
+                for (int h = 0; h < 2; ++h) acc[h] = __builtin_elementwise_fma(dv[h], __builtin_elementwise_fma(xd, r[h], off), acc[h]);
+            } else {
+                const float4 s4 = *reinterpret_cast<const float4 *>(rs), m4 = *reinterpret_cast<const float4 *>(rs + 16);
+                const mma_f2 sv[2] = {{s4.x, s4.y}, {s4.z, s4.w}}, nm[2] = {{-m4.x, -m4.y}, {-m4.z, -m4.w}};
+                const mma_f2 sx = {x.s[p].y, x.s[p].y};
+#pragma unroll
+                for (int h = 0; h < 2; ++h) acc[h] = __builtin_elementwise_fma(sv[h], xd * r[h], __builtin_elementwise_fma(nm[h], sx, acc[h]));
+            }
+        }
+        // (without the pins the scale sums of every step sink below the last step, each step's
+        // MFMA results stay live to the end, and the registers spill)
+        pin(acc);
+    };
+
+    W F[D];
+    Xf X[D];
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) {
+        if constexpr (!(MMA_EXP & 2)) F[d].load(wrs(step_of(d)), lo);
+        F[d].h = wave & 1;
+    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        const uint32_t o = threadIdx.x * 16 + k * 16384;
+        if (o < nbx) {
+            if constexpr (MMA_EXP & 1) *reinterpret_cast<uint4 *>(xl + o) = make_uint4(o, 1, 2, 3);
+            else *reinterpret_cast<uint4 *>(xl + o) = make_uint4(stg[k][0], stg[k][1], stg[k][2], stg[k][3]);
+        }
+    }
+    if (threadIdx.x < 8) *reinterpret_cast<uint4 *>(xl + nbx + threadIdx.x * 16) = make_uint4(0, 0, 0, 0);
+    lds_barrier();
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d) load_x(X[d], step_of(d));
     auto step = [&](auto k_c, int i) __attribute__((always_inline)) {
         constexpr int k = decltype(k_c)::value;
-        const int s = k0 + i;
-        if constexpr (!(MMA_EXP & 2))
-            if (i + D - 1 < NSTEP) F[(k + D - 1) % D].load(wrow, min(s + D - 1, k1 - 1), g, nblk);
+        if (i + D - 1 < NSTEP) {
+            const int s = step_of(i + D - 1);
+            if constexpr (!(MMA_EXP & 2)) F[(k + D - 1) % D].load(wrs(s), lo);
+            F[(k + D - 1) % D].h = wave & 1;
+            load_x(X[(k + D - 1) % D], s);
+        }
         __builtin_amdgcn_sched_barrier(0);
-        compute(F[k], min(s, k1 - 1), s < k1 ? 1.f : 0.f);
+        compute(F[k], X[k]);
     };
     mma_run_steps<D>(step, std::make_integer_sequence<int, NSTEP>{});
 
-    // 3. store (live lanes: column t < TOK, rows 4G + i)
-    const bool live_lane = r < TOK;
-    float *dcol = reinterpret_cast<float *>(a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3 + (int64_t)r * a.nb1);
-    if (n_kp == 1 || (MMA_EXP & 4)) {
-        if (live_lane && r < a.M)
+    // sum the block groups (columns c, c + TOK, ... of the 16-lane row), then the waves in order
+    float v[4] = {acc[0].x, acc[0].y, acc[1].x, acc[1].y};
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (row0 + 4 * g + i < a.N) dcol[row0 + 4 * g + i] = acc[i];
-        return;
+    for (int i = 0; i < 4; ++i) {
+        if constexpr (TOK == 4) v[i] += dpp_f<DPP_ROR4>(v[i]);
+        v[i] += dpp_f<DPP_ROR8>(v[i]);
     }
-    // partial of (slice, K part, tile): [lane (g, t < TOK)][4] floats
-    const int n_tiles8 = gridDim.x * 8;
-    auto slot = [&](int k) { return part + (((int64_t)z * n_kp + k) * n_tiles8 + tile) * (TOK * 4 * 4) + (g * TOK + tl) * 4; };
-    if (live_lane) {
-        float *p = slot(kp);
+    if (c < TOK) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) __hip_atomic_store(p + i, acc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = 0; i < 4; ++i) red[wave][(g * TOK + c) * 4 + i] = v[i];
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
     lds_barrier();
-    int *c = cnt + (int64_t)z * gridDim.x + rg;
-    if (threadIdx.x == 0) order = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    lds_barrier();
-    if (order != n_kp - 1) return;   // (uniform) a later workgroup finishes the row group
-    if (live_lane) {
-        // the parts in K order, loads of 8 parts issued before their sums (one latency per 8)
-        float v[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int k0p = 0; k0p < n_kp; k0p += 8) {
-            float pv[8][4];
+    if (wave != 0 || c >= TOK || c >= a.M) return;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const float *p = slot(min(k0p + k, n_kp - 1));
+    for (int i = 0; i < 4; ++i) v[i] = red[0][(g * TOK + c) * 4 + i];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) pv[k][i] = __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+    for (int w = 1; w < MMA_KS; ++w)
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
+        for (int i = 0; i < 4; ++i) v[i] += red[w][(g * TOK + c) * 4 + i];
+    float *dcol = reinterpret_cast<float *>(a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3 + (int64_t)c * a.nb1);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) v[i] += k0p + k < n_kp ? pv[k][i] : 0.f;
-        }
-        if (r < a.M)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (row0 + 4 * g + i < a.N) dcol[row0 + 4 * g + i] = v[i];
-    }
-    if (threadIdx.x == 0) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = 0; i < 4; ++i)
+        if (row0 + 4 * g + i < a.N) dcol[row0 + 4 * g + i] = v[i];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -537,82 +587,91 @@ __global__ __launch_bounds__(8 * WAVE) void mmvq_mma_kernel(const MmArgs a, int 
 // ------------------------------------------------------------------------------------------
 static int mma_steps(const MmArgs &a) { return (a.K + MMA_STEP_K - 1) / MMA_STEP_K; }
 
-// K parts of NSTEP steps: 8 (1024 K) when that still gives ~2 workgroups per CU over the grid
-// (row groups x slices x parts), else 4
+// steps per wave: the smallest run that covers K over the 16 waves (0: K too long)
+static constexpr int MMA_RUNS[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14};
 static int mma_nstep(const MmArgs &a) {
     const int S = mma_steps(a);
-    const int64_t groups = (a.N + 127) / 128, slices = (int64_t)a.ne12 * a.ne13;
-    const char *e = getenv("GGML_MI355X_MMA_NSTEP");   // per call: tests switch it
-    if (e) return atoi(e) <= 4 ? 4 : 8;
-    return groups * slices * ((S + 7) / 8) >= 384 ? 8 : 4;
+    for (int ns : MMA_RUNS)
+        if (MMA_KS * ns >= S) return ns;
+    return 0;
+}
+static int mma_tok_of(const MmArgs &a) { return a.M <= 4 ? 4 : 8; }
+// the column image of a slice lives in LDS next to the kernel's 16 KB of static arrays
+constexpr int MMA_LDS_IMG = 160 * 1024 - 16 * 1024 - 128;
+
+bool mmvq_mma_supported(int type, const MmArgs &a) {
+    const int tok = mma_tok_of(a);
+    return (type == T_Q4_0 || type == T_Q8_0 || type == T_Q4_K || type == T_Q5_K) && a.M >= 1 && a.M <= 8 &&
+           mma_nstep(a) > 0 && mma_steps(a) * tok * 160 <= MMA_LDS_IMG;
 }
 
-template <int T, int TOK> static void mma_geometry(const MmArgs &a, int &groups, int &n_kp, size_t &lds) {
-    const int S = mma_steps(a);
-    const int ns = mma_nstep(a);
-    groups = (a.N + 127) / 128;
-    n_kp = (S + ns - 1) / ns;
-    lds = (size_t)ns * mma_step_bytes<T, TOK>();
+size_t mmvq_mma_img_bytes(int, const MmArgs &a) {
+    return (size_t)mma_steps(a) * mma_tok_of(a) * 160 * a.ne12 * a.ne13;
 }
 
-size_t mmvq_mma_part_bytes(int type, const MmArgs &a) {
-    int groups = 0, n_kp = 1;
-    size_t lds = 0;
-    const bool t8 = a.M <= 8;
-    switch (type) {
-        case T_Q4_0: t8 ? mma_geometry<T_Q4_0, 8>(a, groups, n_kp, lds) : mma_geometry<T_Q4_0, 16>(a, groups, n_kp, lds); break;
-        case T_Q8_0: t8 ? mma_geometry<T_Q8_0, 8>(a, groups, n_kp, lds) : mma_geometry<T_Q8_0, 16>(a, groups, n_kp, lds); break;
-        case T_Q4_K: t8 ? mma_geometry<T_Q4_K, 8>(a, groups, n_kp, lds) : mma_geometry<T_Q4_K, 16>(a, groups, n_kp, lds); break;
-        case T_Q5_K: t8 ? mma_geometry<T_Q5_K, 8>(a, groups, n_kp, lds) : mma_geometry<T_Q5_K, 16>(a, groups, n_kp, lds); break;
-        default: return 0;
+template <int T, int TOK, int NS>
+static hipError_t mma_main(const MmArgs &a, const uint8_t *img, int S, hipStream_t st) {
+    if constexpr (MMA_KS * NS * mma_step_bytes<TOK>() > MMA_LDS_IMG + 16 * mma_step_bytes<TOK>()) {
+        return hipErrorInvalidValue;   // (runs whose image cannot fit: never selected)
+    } else {
+        auto kern = mmvq_mma_kernel<T, TOK, NS>;
+        const size_t lds = (size_t)S * mma_step_bytes<TOK>() + 128;
+        static bool attr_set = false;   // per instantiation; > 64 KB of dynamic LDS needs the attribute
+        if (lds > 64 * 1024 && !attr_set) {
+            hipFuncAttributes fa{};
+            hipError_t e = hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kern));
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)(160 * 1024 - fa.sharedSizeBytes));
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                return e;
+            }
+            attr_set = true;
+        }
+        hipLaunchKernelGGL(kern, dim3((a.N + 15) / 16, a.ne12 * a.ne13), dim3(MMA_KS * WAVE), lds, st, a, img, S);
+        return hipSuccess;
     }
-    if (n_kp == 1) return 0;
-    // [slice][part][tile][g 4][t TOK][4] floats
-    return (size_t)a.ne12 * a.ne13 * n_kp * groups * 8 * (t8 ? 8 : 16) * 16 * sizeof(float);
 }
 
 template <int T, int TOK>
-static hipError_t mma_tok(const MmArgs &a, float *part, int *cnt, hipStream_t st) {
-    int groups = 0, n_kp = 1;
-    size_t lds = 0;
-    mma_geometry<T, TOK>(a, groups, n_kp, lds);
-    const int slices = a.ne12 * a.ne13;
-    if (n_kp > 1 && (part == nullptr || cnt == nullptr || (int64_t)groups * slices > 16384)) return hipErrorInvalidValue;
-    const char *de = getenv("GGML_MI355X_MMA_D");   // measurements: 2 = one step ahead
-    const bool d2 = de && atoi(de) == 2;
-    const bool n8 = mma_nstep(a) == 8;
-    const dim3 grid(groups, n_kp, slices);
+static hipError_t mma_tok(const MmArgs &a, uint8_t *img, hipStream_t st) {
     const int S = mma_steps(a);
-    // (16-B activation loads when the rows are 16-B aligned; K is a multiple of 32 for every type)
-#define MMA_GO(DV, NS)                                                                                                \
-    if (a.x_aligned16) hipLaunchKernelGGL((mmvq_mma_kernel<T, TOK, DV, NS, true>), grid, dim3(8 * WAVE), lds, st, a, S, n_kp, part, cnt); \
-    else hipLaunchKernelGGL((mmvq_mma_kernel<T, TOK, DV, NS, false>), grid, dim3(8 * WAVE), lds, st, a, S, n_kp, part, cnt)
-    if (d2) {
-        if (n8) MMA_GO(2, 8);
-        else MMA_GO(2, 4);
-    } else {
-        if (n8) MMA_GO(mma_depth<T>(), 8);
-        else MMA_GO(mma_depth<T>(), 4);
+    const dim3 pg(S, a.ne12 * a.ne13);
+    if (a.x_aligned16) hipLaunchKernelGGL((mma_prequant<TOK, true>), pg, dim3(TOK * 16), 0, st, a, img);
+    else hipLaunchKernelGGL((mma_prequant<TOK, false>), pg, dim3(TOK * 16), 0, st, a, img);
+    hipError_t e;
+    switch (mma_nstep(a)) {
+        case 1: e = mma_main<T, TOK, 1>(a, img, S, st); break;
+        case 2: e = mma_main<T, TOK, 2>(a, img, S, st); break;
+        case 3: e = mma_main<T, TOK, 3>(a, img, S, st); break;
+        case 4: e = mma_main<T, TOK, 4>(a, img, S, st); break;
+        case 5: e = mma_main<T, TOK, 5>(a, img, S, st); break;
+        case 6: e = mma_main<T, TOK, 6>(a, img, S, st); break;
+        case 7: e = mma_main<T, TOK, 7>(a, img, S, st); break;
+        case 8: e = mma_main<T, TOK, 8>(a, img, S, st); break;
+        case 10: e = mma_main<T, TOK, 10>(a, img, S, st); break;
+        case 12: e = mma_main<T, TOK, 12>(a, img, S, st); break;
+        case 14: e = mma_main<T, TOK, 14>(a, img, S, st); break;
+        default: return hipErrorInvalidValue;
     }
-#undef MMA_GO
-    return hipGetLastError();
+    return e != hipSuccess ? e : hipGetLastError();
 }
 
 template <int T>
-static hipError_t mma_type(const MmArgs &a, float *part, int *cnt, hipStream_t st) {
-    return a.M <= 8 ? mma_tok<T, 8>(a, part, cnt, st) : mma_tok<T, 16>(a, part, cnt, st);
+static hipError_t mma_type(const MmArgs &a, uint8_t *img, hipStream_t st) {
+    return mma_tok_of(a) == 4 ? mma_tok<T, 4>(a, img, st) : mma_tok<T, 8>(a, img, st);
 }
 
-// plain MUL_MAT with 1 <= M <= 16 columns. part: mmvq_mma_part_bytes(type, a) bytes of scratch
-// (nullptr when that is 0), cnt: zeroed counters (Scratch::counters) when part is set
-hipError_t mmvq_mma_launch(int type, const MmArgs &a, float *part, int *cnt, hipStream_t st) {
-    if (a.M < 1 || a.M > 16) return hipErrorInvalidValue;
+// plain MUL_MAT with 1 <= M <= 8 columns (mmvq_mma_supported), img = mmvq_mma_img_bytes of scratch
+hipError_t mmvq_mma_launch(int type, const MmArgs &a, uint8_t *img, hipStream_t st) {
+    if (!mmvq_mma_supported(type, a) || img == nullptr) return hipErrorInvalidValue;
     switch (type) {
-        case T_Q4_0: return mma_type<T_Q4_0>(a, part, cnt, st);
-        case T_Q8_0: return mma_type<T_Q8_0>(a, part, cnt, st);
-        case T_Q4_K: return mma_type<T_Q4_K>(a, part, cnt, st);
-        case T_Q5_K: return mma_type<T_Q5_K>(a, part, cnt, st);
-        default: return hipErrorInvalidValue;   // (Q6_K: its eight MFMAs per step spill; the VALU kernels take it)
+        case T_Q4_0: return mma_type<T_Q4_0>(a, img, st);
+        case T_Q8_0: return mma_type<T_Q8_0>(a, img, st);
+        case T_Q4_K: return mma_type<T_Q4_K>(a, img, st);
+        case T_Q5_K: return mma_type<T_Q5_K>(a, img, st);
+        default: return hipErrorInvalidValue;   // (Q6_K stays on the VALU kernels)
     }
 }
 

@@ -95,6 +95,7 @@ __device__ __forceinline__ float dpp_f(float v) {
     return __builtin_bit_cast(float, dpp_u<CTRL>(__builtin_bit_cast(uint32_t, v)));
 }
 constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_MIR7 = 0x141, DPP_MIR15 = 0x140;
+constexpr int DPP_ROR4 = 0x124, DPP_ROR8 = 0x128;   // row_ror: rotate within 16-lane rows
 
 __device__ __forceinline__ float swap16_f(float v) {
     const uint32_t u = __builtin_bit_cast(uint32_t, v);

@@ -9,8 +9,8 @@ the CPU oracle (ggml-cpu's vec_dot on its own src1 quantization) the reference's
 
 Covered: all five types; 2, 3, 5 and 8 columns; ragged rows (N % 16 != 0); Q4_0 / Q8_0 K that
 ends inside a 128-step (K % 128 = 32, 64, 96), K-quants at odd super-block counts; the reference's
-perf shapes (K = 14336, bs 2..8); broadcast batch slices (ne12 = 2 * ne02); K parts of 4 and 8
-steps over workgroups. Q6_K stays on the VALU kernels.
+perf shapes (K = 14336, bs 2..8); broadcast batch slices (ne12 = 2 * ne02); every per-wave step
+run (K = 4096 .. 28672); one column. Q6_K stays on the VALU kernels.
 """
 import os
 
@@ -104,25 +104,24 @@ def test_mma_broadcast_slices(mm, t):
     check(mm, t, 64, 3, 256 if qref.BLCK[t] == 256 else 128, ne2=(2, 4))
 
 
-@pytest.mark.parametrize("nstep", [4, 8])
+@pytest.mark.parametrize("K", [4096, 8192, 14336, 28672])
 @pytest.mark.parametrize("t", [qref.Q4_0, qref.Q4_K], ids=lambda t: qref.NAMES[t])
-def test_mma_k_parts(mm, t, nstep):
-    """the K split into parts of 4 or 8 steps over workgroups (partials through write-through
-    stores and a counter; the last workgroup sums them in K order); run twice for the counters'
-    re-arming"""
-    a, b, out_ne = operands(t, 300, 5, 4096, 5)
-    env = {"GGML_MI355X_MMA": 2, "GGML_MI355X_MMA_NSTEP": nstep}
-    g1 = run_with(mm, a, b, out_ne, env)
-    g2 = run_with(mm, a, b, out_ne, env)
-    assert np.array_equal(g1.view(np.uint32), g2.view(np.uint32)), "K-split result not repeatable"
+def test_mma_wave_steps(mm, t, K):
+    """each K picks another straight-line run per wave (2, 4, 8, 16 steps of 128 over the 16
+    waves of a tile's workgroup; the last waves' steps past K are zero-weighted repeats); run
+    twice: the sums meet in LDS in wave order, so the result repeats bit for bit"""
+    a, b, out_ne = operands(t, 100, 5, K, 5)
+    g1 = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 2})
+    g2 = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 2})
+    assert np.array_equal(g1.view(np.uint32), g2.view(np.uint32)), "result not repeatable"
     valu = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 0})
     assert qref.nmse(g1, valu) <= 1e-10
 
 
 @pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])
-def test_mma_depth2(mm, t):
-    """one weight step ahead (GGML_MI355X_MMA_D=2) instead of the default depth"""
-    a, b, out_ne = operands(t, 100, 7, 2048, 9)
-    got = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 2, "GGML_MI355X_MMA_D": 2})
+def test_mma_one_column(mm, t):
+    """GGML_MI355X_MMA=1 takes single columns too (lanes past the live column repeat it)"""
+    a, b, out_ne = operands(t, 100, 1, 2048, 9)
+    got = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 1})
     valu = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 0})
     assert qref.nmse(got, valu) <= 1e-10
