@@ -191,7 +191,9 @@ template <int TOK> struct MmaW<T_Q4_0, TOK> {
     }
     __device__ inline void load(__amdgpu_buffer_rsrc_t rs, const MmaLanes &lo) {
         bl16(rs, lo.b, V);
-        V[4] = __builtin_amdgcn_raw_buffer_load_b32(rs, lo.b + 16, 0, 0);
+        // (the window's last dword is only used for its low 2 bytes, the block's last two: a 2-byte
+        // load keeps the tensor's last block inside the descriptor's range)
+        V[4] = __builtin_amdgcn_raw_buffer_load_b16(rs, lo.a + 16, 0, 0);
         d = __builtin_amdgcn_raw_buffer_load_b16(rs, lo.a, 0, 0);
     }
     __device__ inline void frags(long (&A)[4], int, const MmaLanes &lo) {
@@ -234,7 +236,7 @@ template <int TOK> struct MmaW<T_Q8_0, TOK> {
     __device__ inline void load(__amdgpu_buffer_rsrc_t rs, const MmaLanes &lo) {
         bl16(rs, lo.b, V);
         bl16(rs, lo.b + 16, V + 4);
-        V[8] = __builtin_amdgcn_raw_buffer_load_b32(rs, lo.b + 32, 0, 0);
+        V[8] = __builtin_amdgcn_raw_buffer_load_b16(rs, lo.a + 32, 0, 0);   // (as Q4_0)
         d = __builtin_amdgcn_raw_buffer_load_b16(rs, lo.a, 0, 0);
     }
     __device__ inline void frags(long (&A)[4], int, const MmaLanes &lo) {
@@ -376,9 +378,11 @@ template <int TOK> struct MmaW<T_Q5_K, TOK> {
 // ------------------------------------------------------------------------------------------
 // step sets in flight per wave (D - 1 steps ahead), within the 128 VGPRs of 16 waves per CU
 #ifdef MMA_D
-template <int T, int TOK> __host__ __device__ constexpr int mma_depth() { return MMA_D; }   // (measurement builds)
+template <int T, int TOK, int RT> __host__ __device__ constexpr int mma_depth() { return MMA_D; }   // (measurement builds)
 #else
-template <int T, int TOK> __host__ __device__ constexpr int mma_depth() { return T == T_Q5_K && TOK == 4 ? 2 : 3; }
+template <int T, int TOK, int RT> __host__ __device__ constexpr int mma_depth() {
+    return (T == T_Q5_K && TOK == 4) || (RT == 2 && T != T_Q4_0) ? 2 : 3;
+}
 #endif
 
 template <int D, typename F, int... Is>
@@ -387,9 +391,10 @@ __device__ __forceinline__ void mma_run_steps(F &&f, std::integer_sequence<int, 
 }
 
 // the columns' images once per call: grid (steps, slices), TOK * 16 threads, thread (t, j, m)
-// quantizes chunk m of block j of column t (zeros past K and M)
+// quantizes chunk m of block j of column t (zeros past K and M); zero_dst: also clear dst (the
+// two K halves of the main kernel add into it)
 template <int TOK, bool XA>
-__global__ __launch_bounds__(TOK * 16) void mma_prequant(const MmArgs a, uint8_t *__restrict__ img) {
+__global__ __launch_bounds__(TOK * 16) void mma_prequant(const MmArgs a, uint8_t *__restrict__ img, int zero_dst) {
     const int s = blockIdx.x, z = blockIdx.y;
     const int i12 = z % a.ne12, i13 = z / a.ne12;
     const int m = threadIdx.x & 3, j = (threadIdx.x >> 2) & 3, t = threadIdx.x >> 4;
@@ -401,18 +406,27 @@ __global__ __launch_bounds__(TOK * 16) void mma_prequant(const MmArgs a, uint8_t
     } else {
         mma_xload<XA>(a, col, s, j, m, v);
     }
+    if (zero_dst) {
+        uint8_t *dz = a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3;
+        for (int r = s * blockDim.x + threadIdx.x; r < a.N; r += gridDim.x * blockDim.x)
+            for (int c = 0; c < a.M; ++c) reinterpret_cast<float *>(dz + (int64_t)c * a.nb1)[r] = 0.f;
+    }
     mma_quant<TOK>(a, v, s, j, t, m, img + ((int64_t)z * gridDim.x + s) * mma_step_bytes<TOK>());
 }
 
-// Workgroup = one 16-row tile, 16 waves, wave w the steps w, w + 16, w + 32, ... of K, so that
-// the workgroup's loads in flight are 16 consecutive steps of each row (steps past K load through
-// empty descriptors: zero weights, zero columns): straight-line code, no loop, so no register
-// set crosses a back-edge (the copies the allocator puts on a back-edge move sets whose loads
-// are still in flight, and each copy waits for its load). Each step loads its weights and its
-// column codes and scales D - 1 steps ahead; all addresses are per-lane constants plus the
-// step's descriptor base (scalar arithmetic).
-template <int T, int TOK, int NSTEP>
-__global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a, const uint8_t *__restrict__ img, int n_steps) {
+// Workgroup = RT 16-row tiles x one K part (grid.z of them, 1 or 2: two halves add into the
+// zeroed dst, and 0 + a + b == 0 + b + a, so the result stays deterministic), 16 waves, wave w the
+// part's steps w, w + 16, w + 32, ..., so that the workgroup's loads in flight are 16 consecutive
+// steps of each row. The RT tiles of a wave share its column fragments: the column image a CU
+// stages and the LDS reads per weight byte both fall with RT x K parts (the column image is
+// most of the memory-pipeline work otherwise: 8 columns of K are more bytes than 16 weight rows).
+// Steps past the part load through empty descriptors (zero weights) against the part's last
+// column step. Straight-line code, no loop, so no register set crosses a back-edge (the copies
+// the allocator puts on a back-edge move sets whose loads are still in flight, and each copy
+// waits for its load). Each step loads its weights D - 1 steps ahead; all weight addresses are
+// per-lane constants plus the step's descriptor base (scalar arithmetic).
+template <int T, int TOK, int RT, int NSTEP>
+__global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a, const uint8_t *__restrict__ img, int n_steps, int part_steps) {
     using W = MmaW<T, TOK>;
     constexpr int G = 16 / TOK;   // block groups per MFMA
     constexpr int L = 4 / G;      // k-groups per block group
@@ -420,29 +434,39 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
     constexpr int Qn = G;         // MFMAs per output
     constexpr int NSC = W::NSC;
     constexpr int SB = mma_step_bytes<TOK>();
-    constexpr int D = mma_depth<T, TOK>();
-    __shared__ __align__(16) float wsc[MMA_KS][4 * NSC * 16];   // [wave][block][k][row]
-    __shared__ __align__(16) float red[MMA_KS][4 * TOK * 4];
-    extern __shared__ __align__(16) uint8_t xl[];   // [steps][SB] column image, then 128 zero bytes
+    constexpr int D = mma_depth<T, TOK, RT>();
+    __shared__ __align__(16) float wsc[MMA_KS][RT][4 * NSC * 16];   // [wave][tile][block][k][row]
+    __shared__ __align__(16) float red[MMA_KS][RT][4 * TOK * 4];
+    extern __shared__ __align__(16) uint8_t xl[];   // [part steps][SB] column image, then 128 zero bytes
 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int c = lane & 15, g = lane >> 4;
     const int z = blockIdx.y;
     const int i12 = z % a.ne12, i13 = z / a.ne12;
-    const int row0 = blockIdx.x * 16;
+    const int row0 = blockIdx.x * 16 * RT;
+    const int s0 = blockIdx.z * part_steps;                     // the part's first step (even)
+    const int n_loc = min(part_steps, n_steps - s0);            // its steps
+    if (n_loc <= 0) return;                                     // (uniform: nothing to add)
     const uint8_t *wtile = a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03 + (int64_t)row0 * a.nb01;
     const uint32_t nb01 = (uint32_t)a.nb01;
-    const uint32_t tile_bytes = (uint32_t)(min(16, a.N - row0) - 1) * nb01 + (uint32_t)(a.K / QT<T>::blck) * QT<T>::bytes;
-    const MmaLanes lo = W::lanes(c, g, wave & 1, nb01, (uint32_t)(reinterpret_cast<uintptr_t>(wtile) & 3));
-    auto wrs = [&](int s) __attribute__((always_inline)) {
-        const uint32_t so = W::step_off(s);
-        return __builtin_amdgcn_make_buffer_rsrc((void *)(wtile + so), 0, s < n_steps ? tile_bytes - so : 0u, MMA_RSRC_W3);
+    const uint32_t tile_bytes = (uint32_t)(min(16 * RT, a.N - row0) - 1) * nb01 + (uint32_t)(a.K / QT<T>::blck) * QT<T>::bytes;
+    const MmaLanes lo0 = W::lanes(c, g, wave & 1, nb01, (uint32_t)(reinterpret_cast<uintptr_t>(wtile) & 3));
+    MmaLanes lo[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) lo[t] = {lo0.a + 16 * t * nb01, lo0.b + 16 * t * nb01, lo0.c + (t && (T == T_Q5_K) ? 16 * t * nb01 : 0)};
+    if constexpr (T == T_Q4_0 || T == T_Q8_0) {
+#pragma unroll
+        for (int t = 0; t < RT; ++t) lo[t].c = lo0.c;   // (the funnel shift: 16 rows apart keep the alignment)
+    }
+    auto wrs = [&](int sl) __attribute__((always_inline)) {   // local step sl
+        const uint32_t so = W::step_off(s0 + sl);
+        return __builtin_amdgcn_make_buffer_rsrc((void *)(wtile + so), 0, sl < n_loc ? tile_bytes - so : 0u, MMA_RSRC_W3);
     };
-    // the slice's column image, staged in LDS once: 16-B pieces, thread t the pieces t + 1024 k
+    // the part's column image, staged in LDS once: 16-B pieces, thread t the pieces t + 1024 k
     // (issued before the weight prefetch, so the LDS writes wait for these loads only)
-    const uint32_t nbx = (uint32_t)(n_steps * SB);
+    const uint32_t nbx = (uint32_t)(n_loc * SB);
     const __amdgpu_buffer_rsrc_t xr =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(img + (int64_t)z * nbx), 0, nbx, MMA_RSRC_W3);
+        __builtin_amdgcn_make_buffer_rsrc((void *)(img + ((int64_t)z * n_steps + s0) * SB), 0, nbx, MMA_RSRC_W3);
     constexpr int NP = (MMA_KS * NSTEP * SB + 16383) / 16384;
     uint32_t stg[NP][4];
     if constexpr (!(MMA_EXP & 1)) {
@@ -462,11 +486,10 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
         uint32_t c[8];   // codes: TOK 4: 4 chunks of 8 B; TOK 8: pair p's 2 chunks at 4p
         float2 s[P];     // {d, d * sum(q)} of the output lane's (token, block) per pair
     };
-    // (steps past K read the last real step: finite values against zero weights)
-    auto load_x = [&](Xf &x, int s) __attribute__((always_inline)) {
-        const uint32_t sl = (uint32_t)min(s, n_steps - 1);
-        const uint8_t *cp = xl + xc + sl * xstep;
-        const uint8_t *sp = xl + xsc + sl * SB;
+    auto load_x = [&](Xf &x, int sl) __attribute__((always_inline)) {
+        const uint32_t sc = (uint32_t)min(sl, n_loc - 1);
+        const uint8_t *cp = xl + xc + sc * xstep;
+        const uint8_t *sp = xl + xsc + sc * SB;
 #pragma unroll
         for (int p = 0; p < P; ++p) {
             if constexpr (TOK == 4) {
@@ -480,44 +503,47 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
             x.s[p] = *reinterpret_cast<const float2 *>(sp + p * G * 8);
         }
     };
-    mma_f2 acc[2] = {{0.f, 0.f}, {0.f, 0.f}};   // rows 4g + {0, 1}, {2, 3}
-    auto compute = [&](W &w, Xf &x) __attribute__((always_inline)) {
-        long A[4];
-        w.frags(A, g, lo);
+    mma_f2 acc[RT][2] = {};   // tile t, rows 4g + {0, 1}, {2, 3}
+    auto compute = [&](W (&w)[RT], Xf &x) __attribute__((always_inline)) {
         pin(x.c);
         pin(x.s);
-        // publish this lane's block-g scales, [block g][k][row c]
-        float o[NSC];
-        w.sc(o, g);
-        float *ws = wsc[wave];
 #pragma unroll
-        for (int k = 0; k < NSC; ++k) ws[(g * NSC + k) * 16 + c] = o[k];
-        const i32x4_t zero = {0, 0, 0, 0};
+        for (int t = 0; t < RT; ++t) {
+            long A[4];
+            w[t].frags(A, g, lo[t]);
+            // publish this lane's block-g scales, [block g][k][row c]
+            float o[NSC];
+            w[t].sc(o, g);
+            float *ws = wsc[wave][t];
 #pragma unroll
-        for (int p = 0; p < P; ++p) {
-            i32x4_t R = zero;
+            for (int k = 0; k < NSC; ++k) ws[(g * NSC + k) * 16 + c] = o[k];
+            const i32x4_t zero = {0, 0, 0, 0};
 #pragma unroll
-            for (int q = 0; q < Qn; ++q) {
-                const int ci = TOK == 4 ? 2 * q : 4 * p + 2 * q;
-                R = __builtin_amdgcn_mfma_i32_16x16x32_i8(A[p * Qn + q], pack2(x.c[ci], x.c[ci + 1]), R, 0, 0, 0);
-            }
-            // outputs: rows 4g + i, token bt, block p G + bg (packed fp32, two rows at a time)
-            const float *rs = ws + (p * G + bg) * NSC * 16 + 4 * g;
-            const mma_f2 xd = {x.s[p].x, x.s[p].x};
-            const mma_f2 r[2] = {{(float)R[0], (float)R[1]}, {(float)R[2], (float)R[3]}};
-            if constexpr (T == T_Q4_0 || T == T_Q8_0) {
-                const float4 dw = *reinterpret_cast<const float4 *>(rs);
-                const mma_f2 dv[2] = {{dw.x, dw.y}, {dw.z, dw.w}};
-                const float o8 = T == T_Q4_0 ? -8.f * x.s[p].y : 0.f;
-                const mma_f2 off = {o8, o8};
+            for (int p = 0; p < P; ++p) {
+                i32x4_t R = zero;
 #pragma unroll
-                for (int h = 0; h < 2; ++h) acc[h] = __builtin_elementwise_fma(dv[h], __builtin_elementwise_fma(xd, r[h], off), acc[h]);
-            } else {
-                const float4 s4 = *reinterpret_cast<const float4 *>(rs), m4 = *reinterpret_cast<const float4 *>(rs + 16);
-                const mma_f2 sv[2] = {{s4.x, s4.y}, {s4.z, s4.w}}, nm[2] = {{-m4.x, -m4.y}, {-m4.z, -m4.w}};
-                const mma_f2 sx = {x.s[p].y, x.s[p].y};
+                for (int q = 0; q < Qn; ++q) {
+                    const int ci = TOK == 4 ? 2 * q : 4 * p + 2 * q;
+                    R = __builtin_amdgcn_mfma_i32_16x16x32_i8(A[p * Qn + q], pack2(x.c[ci], x.c[ci + 1]), R, 0, 0, 0);
+                }
+                // outputs: rows 4g + i, token bt, block p G + bg (packed fp32, two rows at a time)
+                const float *rs = ws + (p * G + bg) * NSC * 16 + 4 * g;
+                const mma_f2 xd = {x.s[p].x, x.s[p].x};
+                const mma_f2 r[2] = {{(float)R[0], (float)R[1]}, {(float)R[2], (float)R[3]}};
+                if constexpr (T == T_Q4_0 || T == T_Q8_0) {
+                    const float4 dw = *reinterpret_cast<const float4 *>(rs);
+                    const mma_f2 dv[2] = {{dw.x, dw.y}, {dw.z, dw.w}};
+                    const float o8 = T == T_Q4_0 ? -8.f * x.s[p].y : 0.f;
+                    const mma_f2 off = {o8, o8};
 #pragma unroll
-                for (int h = 0; h < 2; ++h) acc[h] = __builtin_elementwise_fma(sv[h], xd * r[h], __builtin_elementwise_fma(nm[h], sx, acc[h]));
+                    for (int h = 0; h < 2; ++h) acc[t][h] = __builtin_elementwise_fma(dv[h], __builtin_elementwise_fma(xd, r[h], off), acc[t][h]);
+                } else {
+                    const float4 s4 = *reinterpret_cast<const float4 *>(rs), m4 = *reinterpret_cast<const float4 *>(rs + 16);
+                    const mma_f2 sv[2] = {{s4.x, s4.y}, {s4.z, s4.w}}, nm[2] = {{-m4.x, -m4.y}, {-m4.z, -m4.w}};
+                    const mma_f2 sx = {x.s[p].y, x.s[p].y};
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) acc[t][h] = __builtin_elementwise_fma(sv[h], xd * r[h], __builtin_elementwise_fma(nm[h], sx, acc[t][h]));
+                }
             }
         }
         // (without the pins the scale sums of every step sink below the last step, each step's
@@ -525,13 +551,15 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
         pin(acc);
     };
 
-    W F[D];
+    W F[D][RT];
     Xf X[D];
 #pragma unroll
-    for (int d = 0; d < D - 1; ++d) {
-        if constexpr (!(MMA_EXP & 2)) F[d].load(wrs(step_of(d)), lo);
-        F[d].h = wave & 1;
-    }
+    for (int d = 0; d < D - 1; ++d)
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+            if constexpr (!(MMA_EXP & 2)) F[d][t].load(wrs(step_of(d)), lo[t]);
+            F[d][t].h = wave & 1;
+        }
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
         const uint32_t o = threadIdx.x * 16 + k * 16384;
@@ -547,10 +575,13 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
     auto step = [&](auto k_c, int i) __attribute__((always_inline)) {
         constexpr int k = decltype(k_c)::value;
         if (i + D - 1 < NSTEP) {
-            const int s = step_of(i + D - 1);
-            if constexpr (!(MMA_EXP & 2)) F[(k + D - 1) % D].load(wrs(s), lo);
-            F[(k + D - 1) % D].h = wave & 1;
-            load_x(X[(k + D - 1) % D], s);
+            const int sl = step_of(i + D - 1);
+#pragma unroll
+            for (int t = 0; t < RT; ++t) {
+                if constexpr (!(MMA_EXP & 2)) F[(k + D - 1) % D][t].load(wrs(sl), lo[t]);
+                F[(k + D - 1) % D][t].h = wave & 1;
+            }
+            load_x(X[(k + D - 1) % D], sl);
         }
         __builtin_amdgcn_sched_barrier(0);
         compute(F[k], X[k]);
@@ -558,64 +589,88 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
     mma_run_steps<D>(step, std::make_integer_sequence<int, NSTEP>{});
 
     // sum the block groups (columns c, c + TOK, ... of the 16-lane row), then the waves in order
-    float v[4] = {acc[0].x, acc[0].y, acc[1].x, acc[1].y};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        if constexpr (TOK == 4) v[i] += dpp_f<DPP_ROR4>(v[i]);
-        v[i] += dpp_f<DPP_ROR8>(v[i]);
-    }
-    if (c < TOK) {
+    for (int t = 0; t < RT; ++t) {
+        float v[4] = {acc[t][0].x, acc[t][0].y, acc[t][1].x, acc[t][1].y};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) red[wave][(g * TOK + c) * 4 + i] = v[i];
+        for (int i = 0; i < 4; ++i) {
+            if constexpr (TOK == 4) v[i] += dpp_f<DPP_ROR4>(v[i]);
+            v[i] += dpp_f<DPP_ROR8>(v[i]);
+        }
+        if (c < TOK) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) red[wave][t][(g * TOK + c) * 4 + i] = v[i];
+        }
     }
     lds_barrier();
-    if (wave != 0 || c >= TOK || c >= a.M) return;
+    if (wave >= RT || c >= TOK || c >= a.M) return;   // wave t sums tile t
+    const int t = wave;
+    float v[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = red[0][(g * TOK + c) * 4 + i];
+    for (int i = 0; i < 4; ++i) v[i] = red[0][t][(g * TOK + c) * 4 + i];
 #pragma unroll
     for (int w = 1; w < MMA_KS; ++w)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] += red[w][(g * TOK + c) * 4 + i];
+        for (int i = 0; i < 4; ++i) v[i] += red[w][t][(g * TOK + c) * 4 + i];
     float *dcol = reinterpret_cast<float *>(a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3 + (int64_t)c * a.nb1);
+    const int r0 = row0 + 16 * t + 4 * g;
+    if (gridDim.z == 2) {   // 0 + a + b == 0 + b + a: deterministic for exactly two parts
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-        if (row0 + 4 * g + i < a.N) dcol[row0 + 4 * g + i] = v[i];
+        for (int i = 0; i < 4; ++i)
+            if (r0 + i < a.N) unsafeAtomicAdd(dcol + r0 + i, v[i]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (r0 + i < a.N) dcol[r0 + i] = v[i];
+    }
 }
 
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
 static int mma_steps(const MmArgs &a) { return (a.K + MMA_STEP_K - 1) / MMA_STEP_K; }
-
-// steps per wave: the smallest run that covers K over the 16 waves (0: K too long)
-static constexpr int MMA_RUNS[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14};
-static int mma_nstep(const MmArgs &a) {
+static int mma_tok_of(const MmArgs &a) { return a.M <= 4 ? 4 : 8; }
+static int mma_env(const char *k, int dflt) {
+    const char *e = getenv(k);
+    return e ? atoi(e) : dflt;
+}
+// K parts (1 or 2: two from 32 steps) and 16-row tiles per workgroup (1 or 2; Q5_K 1: its two
+// weight sets per step do not fit twice); GGML_MI355X_MMA_KH / _RT override
+static int mma_kh(const MmArgs &a) { return a.K >= 32 * MMA_STEP_K && mma_env("GGML_MI355X_MMA_KH", 2) != 1 ? 2 : 1; }
+static int mma_rt() { return mma_env("GGML_MI355X_MMA_RT", 2) == 1 ? 1 : 2; }
+// steps of a K part (even: a K-quant super-block's two halves stay in one part)
+static int mma_part_steps(const MmArgs &a, int kh) {
     const int S = mma_steps(a);
+    return kh == 1 ? S : ((S + 1) / 2 + 1) & ~1;
+}
+
+// steps per wave: the smallest run that covers the part over the 16 waves (0: too long)
+static constexpr int MMA_RUNS[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14};
+static int mma_nstep(int part) {
     for (int ns : MMA_RUNS)
-        if (MMA_KS * ns >= S) return ns;
+        if (MMA_KS * ns >= part) return ns;
     return 0;
 }
-static int mma_tok_of(const MmArgs &a) { return a.M <= 4 ? 4 : 8; }
-// the column image of a slice lives in LDS next to the kernel's 16 KB of static arrays
-constexpr int MMA_LDS_IMG = 160 * 1024 - 16 * 1024 - 128;
+// the column image of a part lives in LDS next to the kernel's static arrays (<= 32 KB)
+constexpr int MMA_LDS_IMG = 160 * 1024 - 32 * 1024 - 128;
 
 bool mmvq_mma_supported(int type, const MmArgs &a) {
-    const int tok = mma_tok_of(a);
+    const int part = mma_part_steps(a, mma_kh(a));
     return (type == T_Q4_0 || type == T_Q8_0 || type == T_Q4_K || type == T_Q5_K) && a.M >= 1 && a.M <= 8 &&
-           mma_nstep(a) > 0 && mma_steps(a) * tok * 160 <= MMA_LDS_IMG;
+           mma_nstep(part) > 0 && part * mma_tok_of(a) * 160 <= MMA_LDS_IMG;
 }
 
 size_t mmvq_mma_img_bytes(int, const MmArgs &a) {
     return (size_t)mma_steps(a) * mma_tok_of(a) * 160 * a.ne12 * a.ne13;
 }
 
-template <int T, int TOK, int NS>
-static hipError_t mma_main(const MmArgs &a, const uint8_t *img, int S, hipStream_t st) {
+template <int T, int TOK, int RT, int NS>
+static hipError_t mma_main(const MmArgs &a, const uint8_t *img, int S, int part, int kh, hipStream_t st) {
     if constexpr (MMA_KS * NS * mma_step_bytes<TOK>() > MMA_LDS_IMG + 16 * mma_step_bytes<TOK>()) {
         return hipErrorInvalidValue;   // (runs whose image cannot fit: never selected)
     } else {
-        auto kern = mmvq_mma_kernel<T, TOK, NS>;
-        const size_t lds = (size_t)S * mma_step_bytes<TOK>() + 128;
+        auto kern = mmvq_mma_kernel<T, TOK, RT, NS>;
+        const size_t lds = (size_t)part * mma_step_bytes<TOK>() + 128;
         static bool attr_set = false;   // per instantiation; > 64 KB of dynamic LDS needs the attribute
         if (lds > 64 * 1024 && !attr_set) {
             hipFuncAttributes fa{};
@@ -629,32 +684,38 @@ static hipError_t mma_main(const MmArgs &a, const uint8_t *img, int S, hipStream
             }
             attr_set = true;
         }
-        hipLaunchKernelGGL(kern, dim3((a.N + 15) / 16, a.ne12 * a.ne13), dim3(MMA_KS * WAVE), lds, st, a, img, S);
+        hipLaunchKernelGGL(kern, dim3((a.N + 16 * RT - 1) / (16 * RT), a.ne12 * a.ne13, kh), dim3(MMA_KS * WAVE), lds, st, a, img, S, part);
         return hipSuccess;
+    }
+}
+
+template <int T, int TOK, int RT>
+static hipError_t mma_run(const MmArgs &a, const uint8_t *img, int S, int part, int kh, hipStream_t st) {
+    switch (mma_nstep(part)) {
+        case 1: return mma_main<T, TOK, RT, 1>(a, img, S, part, kh, st);
+        case 2: return mma_main<T, TOK, RT, 2>(a, img, S, part, kh, st);
+        case 3: return mma_main<T, TOK, RT, 3>(a, img, S, part, kh, st);
+        case 4: return mma_main<T, TOK, RT, 4>(a, img, S, part, kh, st);
+        case 5: return mma_main<T, TOK, RT, 5>(a, img, S, part, kh, st);
+        case 6: return mma_main<T, TOK, RT, 6>(a, img, S, part, kh, st);
+        case 7: return mma_main<T, TOK, RT, 7>(a, img, S, part, kh, st);
+        case 8: return mma_main<T, TOK, RT, 8>(a, img, S, part, kh, st);
+        case 10: return mma_main<T, TOK, RT, 10>(a, img, S, part, kh, st);
+        case 12: return mma_main<T, TOK, RT, 12>(a, img, S, part, kh, st);
+        case 14: return mma_main<T, TOK, RT, 14>(a, img, S, part, kh, st);
+        default: return hipErrorInvalidValue;
     }
 }
 
 template <int T, int TOK>
 static hipError_t mma_tok(const MmArgs &a, uint8_t *img, hipStream_t st) {
-    const int S = mma_steps(a);
+    const int S = mma_steps(a), kh = mma_kh(a), part = mma_part_steps(a, kh);
     const dim3 pg(S, a.ne12 * a.ne13);
-    if (a.x_aligned16) hipLaunchKernelGGL((mma_prequant<TOK, true>), pg, dim3(TOK * 16), 0, st, a, img);
-    else hipLaunchKernelGGL((mma_prequant<TOK, false>), pg, dim3(TOK * 16), 0, st, a, img);
+    if (a.x_aligned16) hipLaunchKernelGGL((mma_prequant<TOK, true>), pg, dim3(TOK * 16), 0, st, a, img, kh == 2);
+    else hipLaunchKernelGGL((mma_prequant<TOK, false>), pg, dim3(TOK * 16), 0, st, a, img, kh == 2);
     hipError_t e;
-    switch (mma_nstep(a)) {
-        case 1: e = mma_main<T, TOK, 1>(a, img, S, st); break;
-        case 2: e = mma_main<T, TOK, 2>(a, img, S, st); break;
-        case 3: e = mma_main<T, TOK, 3>(a, img, S, st); break;
-        case 4: e = mma_main<T, TOK, 4>(a, img, S, st); break;
-        case 5: e = mma_main<T, TOK, 5>(a, img, S, st); break;
-        case 6: e = mma_main<T, TOK, 6>(a, img, S, st); break;
-        case 7: e = mma_main<T, TOK, 7>(a, img, S, st); break;
-        case 8: e = mma_main<T, TOK, 8>(a, img, S, st); break;
-        case 10: e = mma_main<T, TOK, 10>(a, img, S, st); break;
-        case 12: e = mma_main<T, TOK, 12>(a, img, S, st); break;
-        case 14: e = mma_main<T, TOK, 14>(a, img, S, st); break;
-        default: return hipErrorInvalidValue;
-    }
+    if constexpr (T == T_Q5_K) e = mma_run<T, TOK, 1>(a, img, S, part, kh, st);
+    else e = mma_rt() == 2 ? mma_run<T, TOK, 2>(a, img, S, part, kh, st) : mma_run<T, TOK, 1>(a, img, S, part, kh, st);
     return e != hipSuccess ? e : hipGetLastError();
 }
 

@@ -43,6 +43,7 @@ for step in "$@"; do
         rehearse) run rehearse 900 bash -c 'for n in 2 4; do BENCH_ONE_GPU_REHEARSAL=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $n --steps 3 --warmup 1 --cpu-seconds 1 || exit 1; done' ;;
         mmaexp) run mmaexp 600 bash scripts/mma_exp.sh run base d4 d5 d6 ;;
         mmaprof) run mmaprof 600 bash scripts/mma_prof.sh $OUT/mmaprof base x1 x2 x3 ;;
+        pmcmma) run pmcmma 600 bash -c "bash scripts/pmc_mma.sh mma q4_0:14336:4096:8:1 && MMA=0 bash scripts/pmc_mma.sh valu q4_0:14336:4096:8:1" ;;
         ringpar2) run ringpar2 600 env GGML_MI355X_RING_PRE=2 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "k11008 or k14336 or k14368 or k12288 or k9216 or k8192 or k131072" ;;
         skb) run skb 600 bash -c 'S="q8_0:4096:11008:512 q4_K:4096:11008:512 q6_K:4096:11008:512 q4_0:4096:14336:512 q8_0:4096:4096:768 q8_0:4096:4096:512"; GGML_MI355X_MMQ8_SK=1 python scripts/mmq_bench.py $S && GGML_MI355X_MMQ8_SK=0 python scripts/mmq_bench.py $S' ;;
         gpt2ab) run gpt2ab 600 bash scripts/gpt2_ab.sh r4blk head ;;

@@ -104,18 +104,31 @@ def test_mma_broadcast_slices(mm, t):
     check(mm, t, 64, 3, 256 if qref.BLCK[t] == 256 else 128, ne2=(2, 4))
 
 
-@pytest.mark.parametrize("K", [4096, 8192, 14336, 28672])
+@pytest.mark.parametrize("K", [4096, 4224, 8192, 14336, 28672])
 @pytest.mark.parametrize("t", [qref.Q4_0, qref.Q4_K], ids=lambda t: qref.NAMES[t])
 def test_mma_wave_steps(mm, t, K):
-    """each K picks another straight-line run per wave (2, 4, 8, 16 steps of 128 over the 16
-    waves of a tile's workgroup; the last waves' steps past K are zero-weighted repeats); run
-    twice: the sums meet in LDS in wave order, so the result repeats bit for bit"""
+    """each K picks another straight-line run per wave over the 16 waves of a workgroup, and from
+    32 steps the K halves add into the zeroed dst (K = 4224: 33 steps, parts of 18 and 15); run
+    twice: the waves meet in LDS in wave order and two halves add the same either way round, so
+    the result repeats bit for bit"""
     a, b, out_ne = operands(t, 100, 5, K, 5)
     g1 = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 2})
     g2 = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 2})
     assert np.array_equal(g1.view(np.uint32), g2.view(np.uint32)), "result not repeatable"
     valu = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 0})
     assert qref.nmse(g1, valu) <= 1e-10
+
+
+@pytest.mark.parametrize("layout", [(1, 1), (1, 2), (2, 1)], ids=lambda l: f"kh{l[0]}rt{l[1]}")
+@pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])
+def test_mma_layouts(mm, t, layout):
+    """one K part and/or one 16-row tile per workgroup (GGML_MI355X_MMA_KH / _RT) against the
+    VALU path; ragged rows (N % 32 = 20)"""
+    kh, rt = layout
+    a, b, out_ne = operands(t, 180, 6, 8192, 11)
+    got = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 2, "GGML_MI355X_MMA_KH": kh, "GGML_MI355X_MMA_RT": rt})
+    valu = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 0})
+    assert qref.nmse(got, valu) <= 1e-10
 
 
 @pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])
