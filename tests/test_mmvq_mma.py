@@ -104,11 +104,11 @@ def test_mma_broadcast_slices(mm, t):
     check(mm, t, 64, 3, 256 if qref.BLCK[t] == 256 else 128, ne2=(2, 4))
 
 
-@pytest.mark.parametrize("K", [4096, 4224, 8192, 14336, 28672])
+@pytest.mark.parametrize("K", [4096, 4352, 8192, 14336, 28672])
 @pytest.mark.parametrize("t", [qref.Q4_0, qref.Q4_K], ids=lambda t: qref.NAMES[t])
 def test_mma_wave_steps(mm, t, K):
     """each K picks another straight-line run per wave over the 16 waves of a workgroup, and from
-    32 steps the K halves add into the zeroed dst (K = 4224: 33 steps, parts of 18 and 15); run
+    32 steps the K halves add into the zeroed dst (K = 4352: 34 steps, parts of 18 and 16); run
     twice: the waves meet in LDS in wave order and two halves add the same either way round, so
     the result repeats bit for bit"""
     a, b, out_ne = operands(t, 100, 5, K, 5)
