@@ -526,7 +526,8 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
                     const int ci = TOK == 4 ? 2 * q : 4 * p + 2 * q;
                     R = __builtin_amdgcn_mfma_i32_16x16x32_i8(A[p * Qn + q], pack2(x.c[ci], x.c[ci + 1]), R, 0, 0, 0);
                 }
-                // outputs: rows 4g + i, token bt, block p G + bg (packed fp32, two rows at a time)
+                // outputs: rows 4g + i, token bt, block p G + bg, two rows at a time (the object is
+                // built without packed-f32 ops, as mmq8.o: scalar fmas beside the MFMAs, Makefile)
                 const float *rs = ws + (p * G + bg) * NSC * 16 + 4 * g;
                 const mma_f2 xd = {x.s[p].x, x.s[p].x};
                 const mma_f2 r[2] = {{(float)R[0], (float)R[1]}, {(float)R[2], (float)R[3]}};
