@@ -182,21 +182,33 @@ static int ring_pre_min() {
     return v == 0 ? 1 << 30 : v == 2 ? 2 : 4;
 }
 
-// the int8 MFMA mat-vec (mmvq_mma.hip: the columns are the N side of a 16 x 16 tile, so the
-// weights are read once and the per-column cost is one MFMA column), for 2..8 columns.
-// GGML_MI355X_MMA=N: from N columns on; unset or 0: the per-column VALU kernels (the MFMA form
-// does not beat them yet: profiles/r05_mma_matvec_ab.txt)
-static int mma_min_cols() {
+// the int8 MFMA mat-vec (mmvq_mma.hip: the weights read once, the columns packed
+// block-diagonally into the MFMA's 16 columns, flat in the column count). Measured against the
+// per-column VALU kernels (profiles/r05_mma_sweep.txt, 5 shapes x 4 types x 4..8 columns) it is
+// never slower for Q4_0 / Q8_0 from 5 columns (0.67-1.00x) and faster for Q4_K from 5 / Q5_K from
+// 6 columns at K <= 4096; slower below 5 columns and for the K-quants at long K.
+// GGML_MI355X_MMA=N: from N columns on for every type it takes; 0: never.
+static int mma_min_cols(int type, int K, int slices) {
     const char *e = getenv("GGML_MI355X_MMA");   // per call: tests switch it
-    const int v = e ? atoi(e) : 0;
-    return v <= 0 ? 1 << 30 : std::max(v, 1);
+    if (e != nullptr) {
+        const int v = atoi(e);
+        return v <= 0 ? 1 << 30 : v;
+    }
+    if (slices > 1) return 1 << 30;   // (8 batch slices: 2-4 % slower than the VALU kernels)
+    switch (type) {
+        case T_Q4_0:
+        case T_Q8_0: return 5;
+        case T_Q4_K: return K <= 4096 ? 5 : 1 << 30;
+        case T_Q5_K: return K <= 4096 ? 6 : 1 << 30;
+        default: return 1 << 30;
+    }
 }
 
 // mat-vec over columns [c0, c0 + ncols) in groups of at most 8 (scratch: the caller holds its
 // mutex; nullptr = no pre-quantized images)
 static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st, Scratch *scratch = nullptr) {
     const int rpw = pick_rpw(type, (int64_t)m.N * m.ne12 * m.ne13);
-    if (scratch != nullptr && ncols >= mma_min_cols() && ncols <= 8) {
+    if (scratch != nullptr && ncols >= mma_min_cols(type, m.K, m.ne12 * m.ne13) && ncols <= 8) {
         MmArgs g = m;
         g.x = m.x + (int64_t)c0 * m.nb11;
         g.dst = m.dst + (int64_t)c0 * m.nb1;

@@ -35,7 +35,7 @@ for step in "$@"; do
         ringpar) run ringpar 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "k11008 or k14336 or k14368 or k12288 or k9216 or k8192 or k131072 or k4096 or k1024" ;;
         ringb) run ringb 600 bash -c 'S="q4_0:14336:4096:1:1 q4_0:14336:4096:2:1 q4_0:14336:4096:3:1 q4_0:14336:4096:4:1 q4_0:14336:4096:5:1 q4_0:14336:4096:8:1 q4_K:14336:4096:1:1 q4_K:14336:4096:2:1 q4_K:14336:4096:4:1 q4_K:14336:4096:8:1 q5_K:14336:4096:8:1 q6_K:14336:4096:1:1 q6_K:14336:4096:8:1 q8_0:14336:4096:1:1 q8_0:14336:4096:8:1 q4_0:11008:4096:4:1 q4_0:11008:4096:8:1 q4_0:14336:4096:1:8 q4_0:14336:4096:8:8"; python scripts/mmvq_bench.py $S && GGML_MI355X_RING_DEPTH=2 python scripts/mmvq_bench.py $S && GGML_MI355X_RING_PRE=2 python scripts/mmvq_bench.py q4_0:14336:4096:2:1 q4_K:14336:4096:2:1 q6_K:14336:4096:2:1 q8_0:14336:4096:2:1' ;;
         mmatest) run mmatest 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_mmvq_mma.py ;;
-        mmab) run mmab 600 bash -c 'S="q4_0:14336:4096:1:1 q4_0:14336:4096:2:1 q4_0:14336:4096:3:1 q4_0:14336:4096:4:1 q4_0:14336:4096:5:1 q4_0:14336:4096:8:1 q8_0:14336:4096:2:1 q8_0:14336:4096:8:1 q4_K:14336:4096:2:1 q4_K:14336:4096:8:1 q5_K:14336:4096:8:1 q6_K:14336:4096:2:1 q6_K:14336:4096:8:1 q4_0:4096:4096:1:1 q4_0:4096:4096:2:1 q4_0:4096:4096:8:1 q4_K:4096:11008:8:1 q4_0:14336:4096:1:8 q4_0:14336:4096:2:8 q4_0:14336:4096:8:8 q4_K:14336:4096:8:8"; GGML_MI355X_MMA=1 python scripts/mmvq_bench.py $S && python scripts/mmvq_bench.py $S' ;;
+        mmab) run mmab 600 bash -c 'S="q4_0:14336:4096:1:1 q4_0:14336:4096:2:1 q4_0:14336:4096:3:1 q4_0:14336:4096:4:1 q4_0:14336:4096:5:1 q4_0:14336:4096:8:1 q8_0:14336:4096:2:1 q8_0:14336:4096:8:1 q4_K:14336:4096:2:1 q4_K:14336:4096:8:1 q5_K:14336:4096:8:1 q6_K:14336:4096:2:1 q6_K:14336:4096:8:1 q4_0:4096:4096:1:1 q4_0:4096:4096:2:1 q4_0:4096:4096:8:1 q4_K:4096:11008:8:1 q4_0:14336:4096:1:8 q4_0:14336:4096:2:8 q4_0:14336:4096:8:8 q4_K:14336:4096:8:8"; GGML_MI355X_MMA=1 python scripts/mmvq_bench.py $S && GGML_MI355X_MMA=0 python scripts/mmvq_bench.py $S && python scripts/mmvq_bench.py $S' ;;
         profmma) run profmma 300 env GGML_MI355X_MMA=1 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profmma -o run -- python scripts/mmvq_bench.py q4_0:14336:4096:1:1 q4_0:14336:4096:8:1 q4_K:4096:11008:8:1 q4_0:4096:4096:8:1 \
                  && for t in $(find $OUT/profmma -name '*kernel_trace.csv'); do rm -f $t; done ;;
         q8x) run q8x 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_mmq8.py tests/test_gpu_parity.py -k "mmq8 or mm_1 or mmid or grouped or m512 or m2048" ;;
@@ -44,7 +44,8 @@ for step in "$@"; do
         mmaexp) run mmaexp 600 bash scripts/mma_exp.sh run base d4 d5 d6 ;;
         mmaprof) run mmaprof 600 bash scripts/mma_prof.sh $OUT/mmaprof base x1 x2 x3 ;;
         pmcmma) run pmcmma 600 bash -c "bash scripts/pmc_mma.sh mma q4_0:14336:4096:8:1 && MMA=0 bash scripts/pmc_mma.sh valu q4_0:14336:4096:8:1" ;;
-        ringpar2) run ringpar2 600 env GGML_MI355X_RING_PRE=2 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "k11008 or k14336 or k14368 or k12288 or k9216 or k8192 or k131072" ;;
+        mmasweep) run mmasweep 900 bash -c 'S=" q4_0:4096:4096:4:1 q4_0:4096:4096:5:1 q4_0:4096:4096:6:1 q4_0:4096:4096:8:1 q4_0:4096:11008:4:1 q4_0:4096:11008:5:1 q4_0:4096:11008:6:1 q4_0:4096:11008:8:1 q4_0:11008:4096:4:1 q4_0:11008:4096:5:1 q4_0:11008:4096:6:1 q4_0:11008:4096:8:1 q4_0:14336:4096:4:1 q4_0:14336:4096:5:1 q4_0:14336:4096:6:1 q4_0:14336:4096:8:1 q4_0:4096:14336:4:1 q4_0:4096:14336:5:1 q4_0:4096:14336:6:1 q4_0:4096:14336:8:1 q8_0:4096:4096:4:1 q8_0:4096:4096:5:1 q8_0:4096:4096:6:1 q8_0:4096:4096:8:1 q8_0:4096:11008:4:1 q8_0:4096:11008:5:1 q8_0:4096:11008:6:1 q8_0:4096:11008:8:1 q8_0:11008:4096:4:1 q8_0:11008:4096:5:1 q8_0:11008:4096:6:1 q8_0:11008:4096:8:1 q8_0:14336:4096:4:1 q8_0:14336:4096:5:1 q8_0:14336:4096:6:1 q8_0:14336:4096:8:1 q8_0:4096:14336:4:1 q8_0:4096:14336:5:1 q8_0:4096:14336:6:1 q8_0:4096:14336:8:1 q4_K:4096:4096:4:1 q4_K:4096:4096:5:1 q4_K:4096:4096:6:1 q4_K:4096:4096:8:1 q4_K:4096:11008:4:1 q4_K:4096:11008:5:1 q4_K:4096:11008:6:1 q4_K:4096:11008:8:1 q4_K:11008:4096:4:1 q4_K:11008:4096:5:1 q4_K:11008:4096:6:1 q4_K:11008:4096:8:1 q4_K:14336:4096:4:1 q4_K:14336:4096:5:1 q4_K:14336:4096:6:1 q4_K:14336:4096:8:1 q4_K:4096:14336:4:1 q4_K:4096:14336:5:1 q4_K:4096:14336:6:1 q4_K:4096:14336:8:1 q5_K:4096:4096:4:1 q5_K:4096:4096:5:1 q5_K:4096:4096:6:1 q5_K:4096:4096:8:1 q5_K:4096:11008:4:1 q5_K:4096:11008:5:1 q5_K:4096:11008:6:1 q5_K:4096:11008:8:1 q5_K:11008:4096:4:1 q5_K:11008:4096:5:1 q5_K:11008:4096:6:1 q5_K:11008:4096:8:1 q5_K:14336:4096:4:1 q5_K:14336:4096:5:1 q5_K:14336:4096:6:1 q5_K:14336:4096:8:1 q5_K:4096:14336:4:1 q5_K:4096:14336:5:1 q5_K:4096:14336:6:1 q5_K:4096:14336:8:1"; GGML_MI355X_MMA=1 python scripts/mmvq_bench.py $S && GGML_MI355X_MMA=0 python scripts/mmvq_bench.py $S' ;;
+        ringpar2) run ringpar2 600 env GGML_MI355X_RING_PRE=2 GGML_MI355X_MMA=0 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "k11008 or k14336 or k14368 or k12288 or k9216 or k8192 or k131072" ;;
         skb) run skb 600 bash -c 'S="q8_0:4096:11008:512 q4_K:4096:11008:512 q6_K:4096:11008:512 q4_0:4096:14336:512 q8_0:4096:4096:768 q8_0:4096:4096:512"; GGML_MI355X_MMQ8_SK=1 python scripts/mmq_bench.py $S && GGML_MI355X_MMQ8_SK=0 python scripts/mmq_bench.py $S' ;;
         gpt2ab) run gpt2ab 600 bash scripts/gpt2_ab.sh r4blk head ;;
         stamps) run stamps 300 bash -c 'python scripts/stamps_probe.py q4_K 4096 4096 1 && python scripts/stamps_probe.py q4_0 4096 4096 1' ;;
