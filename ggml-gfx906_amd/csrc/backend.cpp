@@ -1927,12 +1927,15 @@ enum ggml_status be_graph_compute(ggml_backend_t b, struct ggml_cgraph *g) {
         hg.exec = nullptr;
         return run_nodes(c, g, false);
     }
+    c->scratch.short_in_capture = false;
     HIP_OK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed));
     const enum ggml_status st = run_nodes(c, g, true, true);
     hipGraph_t graph = nullptr;
     const hipError_t ec = hipStreamEndCapture(c->stream, &graph);
-    if (st != GGML_STATUS_SUCCESS || ec != hipSuccess || graph == nullptr) {
-        // a launch that cannot be captured yet (first use of a scratch size): run eagerly once
+    if (st != GGML_STATUS_SUCCESS || ec != hipSuccess || graph == nullptr || c->scratch.short_in_capture) {
+        // a launch that cannot be captured yet (first use of a scratch size, whether it failed or
+        // took a scratch-free slower path): run eagerly once, which grows the scratch, and capture
+        // on the next call
         (void)hipGetLastError();
         if (graph) (void)hipGraphDestroy(graph);
         hg.props.clear();

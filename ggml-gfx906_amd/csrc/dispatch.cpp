@@ -554,8 +554,10 @@ void *Scratch::get(size_t bytes, hipStream_t st) {
         cs = hipStreamCaptureStatusNone;
     }
     if (cs != hipStreamCaptureStatusNone) {
-        fprintf(stderr, "[ggml-mi355x] scratch of %zu bytes needed inside a hipGraph capture: run the launch once "
-                        "eagerly on this stream before capturing it\n", bytes);
+        if (!short_in_capture)
+            fprintf(stderr, "[ggml-mi355x] scratch of %zu bytes needed inside a hipGraph capture: run the launch once "
+                            "eagerly on this stream before capturing it\n", bytes);
+        short_in_capture = true;
         return nullptr;
     }
     if (ptr) {

@@ -38,6 +38,11 @@ struct Scratch {
     size_t cap = 0;
     int device = -1;
     uint64_t gen = 0;
+    // set when get() had to refuse a larger buffer inside a stream capture. Some users then take
+    // a slower path that needs no scratch (the mat-vec's pre-quantized forms), so the capture
+    // itself succeeds; the backend checks this flag and runs eagerly instead (which grows the
+    // buffer), so the graph it captures next holds the fast path
+    bool short_in_capture = false;
     void *get(size_t bytes, hipStream_t st);
     // stream-K tile counters (mmq8.hip): a separate zeroed allocation of COUNTERS ints, made once
     // (outside any capture) and never moved; every launch leaves them zero
