@@ -128,3 +128,25 @@ def test_cpy_seeded_sweep():
     assert r.returncode == 0 and "CPY_CHECK_OK" in r.stdout, "\n".join(bad) + r.stdout[-2000:] + r.stderr[-2000:]
     m = re.search(r"(\d+) cases run on the plugin", r.stdout)
     assert m and int(m.group(1)) >= 85, r.stdout[-2000:]   # (85 of the sweep's cases are claimed on MI355X0)
+
+
+def test_backend_ops_perf_times_every_matvec_case():
+    """test-backend-ops perf (tests/test-backend-ops.cpp:1299-1365) through the backend's hipGraph
+    capture and replay, the K = 14336 mat-vec cases of every hot type at 1..8 columns: each must
+    report a time. (A mat-vec that could not grow its scratch inside the capture used to fail there
+    for the K-quants at 3..8 columns, no timing at all, or to bake a slower scratch-free form into
+    the replayed graph; a shortfall now fails the capture and the eager run grows the scratch.)"""
+    if not os.path.exists(TBO):
+        pytest.skip("oracle/_ref/test-backend-ops not built")
+    env = dict(os.environ, GGML_BACKEND_PATH=LIB)
+    r = subprocess.run([TBO, "perf", "-o", "MUL_MAT", "-b", "MI355X0", "-p", r"m=4096,n=[1-8],k=14336"],
+                       capture_output=True, text=True, env=env, timeout=600)
+    out = ANSI.sub("", r.stdout)
+    assert r.returncode == 0, out[-2000:] + r.stderr[-1000:]
+    timed = set()
+    for line in out.splitlines():
+        m = re.search(r"MUL_MAT\(type_a=(\w+),type_b=f32,m=4096,n=(\d),k=14336.*us/run", line)
+        if m and m.group(1) in HOT:
+            timed.add((m.group(1), int(m.group(2))))
+    want = {(t, n) for t in HOT for n in (1, 2, 3, 4, 5, 8)}
+    assert want <= timed, sorted(want - timed)
