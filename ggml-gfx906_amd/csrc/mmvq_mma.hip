@@ -162,6 +162,18 @@ __device__ __forceinline__ void bl8(__amdgpu_buffer_rsrc_t r, uint32_t off, uint
     o[0] = v[0]; o[1] = v[1];
 }
 
+// K-quants with 8 tokens: lane g loaded half g & 1 of qs run 2h + (g >> 1); pair p needs half
+// g & 1 of run 2h + p. Lanes g and g ^ 2 (32 apart) trade their own halves: afterwards X holds
+// run 2h's half and Y run 2h + 1's on every lane.
+__device__ __forceinline__ void runs_to_pairs(const uint32_t (&own)[4], uint32_t (&X)[4], uint32_t (&Y)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        X[k] = own[k];
+        Y[k] = own[k];
+        swap32(Y[k], X[k]);   // upper lanes' X <- lower lanes' own, lower lanes' Y <- upper lanes' own
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // per-type weights of one step for lane (row r, k-group g), loaded through a per-step buffer
 // descriptor (base = the tile at the step's first byte; no records at all for a step past K,
@@ -273,12 +285,14 @@ template <int TOK> struct MmaW<T_Q8_0, TOK> {
 //   TOK 8: lane g loads bytes 8 (g & 1) + 16 q .. + 8 (q = 0, 1) of run 2h + p for both pairs
 template <int TOK> struct MmaW<T_Q4_K, TOK> {
     static constexpr int NSC = 2;
-    uint32_t H[4], Q[8];
+    uint32_t H[4], Q[TOK == 4 ? 8 : 4];
     int h;
     __device__ static uint32_t step_off(int s) { return 144u * (uint32_t)(s >> 1); }
+    // b: TOK 4 the 32-B run of sub-block g; TOK 8 half g & 1 of run 2h + (g >> 1) (bytes 8 (g & 1)
+    // and 16 + 8 (g & 1), 8 each): the other run's half comes from lane g ^ 2 (runs_to_pairs)
     __device__ static MmaLanes lanes(int r, int g, int h, uint32_t nb01, uint32_t) {
         const uint32_t row = r * nb01;
-        return {row, row + 16 + 32 * (2 * h + (TOK == 4 ? (g >> 1) : 0)) + (TOK == 4 ? 0 : 8 * (g & 1)), 0};
+        return {row, row + 16 + 32 * (2 * h + (g >> 1)) + (TOK == 4 ? 0 : 8 * (g & 1)), 0};
     }
     __device__ inline void load(__amdgpu_buffer_rsrc_t rs, const MmaLanes &lo) {
         bl16(rs, lo.a, H);
@@ -286,8 +300,8 @@ template <int TOK> struct MmaW<T_Q4_K, TOK> {
             bl16(rs, lo.b, Q);
             bl16(rs, lo.b + 16, Q + 4);
         } else {
-#pragma unroll
-            for (int pq = 0; pq < 4; ++pq) bl8(rs, lo.b + 32 * (pq >> 1) + 16 * (pq & 1), Q + 2 * pq);
+            bl8(rs, lo.b, Q);
+            bl8(rs, lo.b + 16, Q + 2);
         }
     }
     __device__ inline void frags(long (&A)[4], int g, const MmaLanes &) {
@@ -301,9 +315,13 @@ template <int TOK> struct MmaW<T_Q4_K, TOK> {
                 A[m] = pack2((Q[o] >> sft) & NIB, (Q[o + 1] >> sft) & NIB);
             }
         } else {
+            uint32_t X[4], Y[4];
+            runs_to_pairs(Q, X, Y);
             const int sft = 4 * (g >> 1);
-#pragma unroll
-            for (int pq = 0; pq < 4; ++pq) A[pq] = pack2((Q[2 * pq] >> sft) & NIB, (Q[2 * pq + 1] >> sft) & NIB);
+            A[0] = pack2((X[0] >> sft) & NIB, (X[1] >> sft) & NIB);
+            A[1] = pack2((X[2] >> sft) & NIB, (X[3] >> sft) & NIB);
+            A[2] = pack2((Y[0] >> sft) & NIB, (Y[1] >> sft) & NIB);
+            A[3] = pack2((Y[2] >> sft) & NIB, (Y[3] >> sft) & NIB);
         }
     }
     // d * sc and dmin * m of sub-block 4h + g
@@ -321,13 +339,12 @@ template <int TOK> struct MmaW<T_Q4_K, TOK> {
 // sub-block 4h + b
 template <int TOK> struct MmaW<T_Q5_K, TOK> {
     static constexpr int NSC = 2;
-    uint32_t H[4], Q[8], QH[TOK == 4 ? 8 : 4];
+    uint32_t H[4], Q[TOK == 4 ? 8 : 4], QH[TOK == 4 ? 8 : 4];
     int h;
     __device__ static uint32_t step_off(int s) { return 176u * (uint32_t)(s >> 1); }
     __device__ static MmaLanes lanes(int r, int g, int h, uint32_t nb01, uint32_t) {
         const uint32_t row = r * nb01;
-        return {row, row + 48 + 32 * (2 * h + (TOK == 4 ? (g >> 1) : 0)) + (TOK == 4 ? 0 : 8 * (g & 1)),
-                row + 16 + (TOK == 4 ? 0 : 8 * (g & 1))};
+        return {row, row + 48 + 32 * (2 * h + (g >> 1)) + (TOK == 4 ? 0 : 8 * (g & 1)), row + 16 + (TOK == 4 ? 0 : 8 * (g & 1))};
     }
     __device__ inline void load(__amdgpu_buffer_rsrc_t rs, const MmaLanes &lo) {
         bl16(rs, lo.a, H);
@@ -337,8 +354,8 @@ template <int TOK> struct MmaW<T_Q5_K, TOK> {
             bl16(rs, lo.c, QH);
             bl16(rs, lo.c + 16, QH + 4);
         } else {
-#pragma unroll
-            for (int pq = 0; pq < 4; ++pq) bl8(rs, lo.b + 32 * (pq >> 1) + 16 * (pq & 1), Q + 2 * pq);
+            bl8(rs, lo.b, Q);
+            bl8(rs, lo.b + 16, Q + 2);
             bl8(rs, lo.c, QH);
             bl8(rs, lo.c + 16, QH + 2);
         }
@@ -356,12 +373,15 @@ template <int TOK> struct MmaW<T_Q5_K, TOK> {
                              ((Q[o + 1] >> sft) & NIB) | (((QH[o + 1] >> hb) & 0x01010101u) << 4));
             }
         } else {
+            uint32_t X[4], Y[4];
+            runs_to_pairs(Q, X, Y);
             const int sft = 4 * (g >> 1);
 #pragma unroll
             for (int pq = 0; pq < 4; ++pq) {
+                const uint32_t *R = pq < 2 ? X : Y;
                 const int hb = 4 * h + 2 * (pq >> 1) + (g >> 1), o = 2 * (pq & 1);
-                A[pq] = pack2(((Q[2 * pq] >> sft) & NIB) | (((QH[o] >> hb) & 0x01010101u) << 4),
-                              ((Q[2 * pq + 1] >> sft) & NIB) | (((QH[o + 1] >> hb) & 0x01010101u) << 4));
+                A[pq] = pack2(((R[o] >> sft) & NIB) | (((QH[o] >> hb) & 0x01010101u) << 4),
+                              ((R[o + 1] >> sft) & NIB) | (((QH[o + 1] >> hb) & 0x01010101u) << 4));
             }
         }
     }
