@@ -213,6 +213,10 @@ template <int TOK> struct MmaW<T_Q4_0, TOK> {
         uint32_t q[4];   // qs dwords
 #pragma unroll
         for (int k = 0; k < 4; ++k) q[k] = __builtin_amdgcn_alignbyte(V[k + 1], V[k], lo.c);
+        frags_q(q, A);
+    }
+    // A fragments from the block's 16 qs bytes (lane g owns block g of the step)
+    __device__ static inline void frags_q(const uint32_t (&q)[4], long (&A)[4]) {
         if constexpr (TOK == 4) {
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
@@ -256,6 +260,9 @@ template <int TOK> struct MmaW<T_Q8_0, TOK> {
         uint32_t q[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) q[k] = __builtin_amdgcn_alignbyte(V[k + 1], V[k], lo.c);
+        frags_q(q, A);
+    }
+    __device__ static inline void frags_q(const uint32_t (&q)[8], long (&A)[4]) {
         if constexpr (TOK == 4) {
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
@@ -395,6 +402,55 @@ template <int TOK> struct MmaW<T_Q5_K, TOK> {
     }
 };
 
+
+// ------------------------------------------------------------------------------------------
+// Paired steps (Q4_0 / Q8_0, 4-byte-aligned contiguous rows): lane g loads blocks 2g and 2g + 1
+// of a double step (8 blocks of its row, 256 k) as one aligned window — half the load
+// instructions of one block per step — and two permlane swaps per dword hand every lane its
+// block of each of the two steps:
+//   F = block 2g, S = block 2g + 1:  g0 F0 S0 | g1 F1 S1 | g2 F2 S2 | g3 F3 S3
+//   --swap16-->  X: F0 S0 F2 S2 / Y: F1 S1 F3 S3  --swap32-->  X: F0 S0 F1 S1 (step 2j: blocks 0..3)
+//                                                            Y: F2 S2 F3 S3 (step 2j + 1: 4..7)
+// ------------------------------------------------------------------------------------------
+template <int T, int TOK> struct MmaHalf {   // one step's block of a lane, in registers
+    static constexpr int NQ = T == T_Q4_0 ? 4 : 8;
+    static constexpr int NSC = 1;
+    uint32_t q[NQ], d;
+    int h;   // (unused)
+    __device__ inline void frags(long (&A)[4], int, const MmaLanes &) { MmaW<T, TOK>::frags_q(q, A); }
+    __device__ inline void sc(float *o, int) { o[0] = h2f((uint16_t)d); }
+};
+template <int T, int TOK> struct MmaPair {
+    static constexpr int NQ = T == T_Q4_0 ? 4 : 8;
+    static constexpr int NV = T == T_Q4_0 ? 9 : 17;   // 36 / 68 bytes
+    uint32_t V[NV];
+    __device__ static MmaLanes lanes(int r, int g, uint32_t nb01) { return {r * nb01 + (2u * QT<T>::bytes) * g, 0, 0}; }
+    __device__ inline void load(__amdgpu_buffer_rsrc_t rs, const MmaLanes &lo) {
+#pragma unroll
+        for (int k = 0; k + 4 <= NV; k += 4) bl16(rs, lo.a + 4 * k, V + k);
+        V[NV - 1] = __builtin_amdgcn_raw_buffer_load_b32(rs, lo.a + 4 * (NV - 1), 0, 0);
+    }
+    // the two steps' blocks of this lane (X: step 2j, Y: step 2j + 1)
+    __device__ inline void split(MmaHalf<T, TOK> &X, MmaHalf<T, TOK> &Y) {
+        pin(V);
+        // F = bytes 0..QT-1 (d at 0, qs from 2: funnel by 2), S = the next block (d in the high half
+        // of dword NQ, qs dword-aligned after it)
+        X.d = V[0] & 0xffff;
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) X.q[k] = __builtin_amdgcn_alignbyte(V[k + 1], V[k], 2);
+        Y.d = V[NQ] >> 16;
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) Y.q[k] = V[NQ + 1 + k];
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) {
+            swap16(Y.q[k], X.q[k]);
+            swap32(Y.q[k], X.q[k]);
+        }
+        swap16(Y.d, X.d);
+        swap32(Y.d, X.d);
+    }
+};
+
 // ------------------------------------------------------------------------------------------
 // step sets in flight per wave (D - 1 steps ahead), within the 128 VGPRs of 16 waves per CU
 #ifdef MMA_D
@@ -445,9 +501,10 @@ __global__ __launch_bounds__(TOK * 16) void mma_prequant(const MmArgs a, uint8_t
 // the allocator puts on a back-edge move sets whose loads are still in flight, and each copy
 // waits for its load). Each step loads its weights D - 1 steps ahead; all weight addresses are
 // per-lane constants plus the step's descriptor base (scalar arithmetic).
-template <int T, int TOK, int RT, int NSTEP>
+template <int T, int TOK, int RT, int NSTEP, bool PR>
 __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a, const uint8_t *__restrict__ img, int n_steps, int part_steps) {
     using W = MmaW<T, TOK>;
+    static_assert(!PR || ((T == T_Q4_0 || T == T_Q8_0) && NSTEP % 2 == 0), "paired steps: Q4_0 / Q8_0, even runs");
     constexpr int G = 16 / TOK;   // block groups per MFMA
     constexpr int L = 4 / G;      // k-groups per block group
     constexpr int P = 4 / G;      // MFMA outputs per step
@@ -500,16 +557,18 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
     const uint32_t xc = xlive ? (uint32_t)((bt * 4 + bg) * 32 + (g % L) * Qn * 8) : nbx;
     const uint32_t xstep = xlive ? (uint32_t)SB : 0u;
     const uint32_t xsc = (uint32_t)(TOK * 128 + (bt * 4 + bg) * 8);
-    auto step_of = [&](int i) { return wave + MMA_KS * i; };
+    // (paired: wave w the double steps w, w + 16, ..., i.e. steps 2w, 2w + 1, 2w + 32, ...)
+    auto step_of = [&](int i) { return PR ? 2 * (wave + MMA_KS * (i >> 1)) + (i & 1) : wave + MMA_KS * i; };
 
     struct Xf {
         uint32_t c[8];   // codes: TOK 4: 4 chunks of 8 B; TOK 8: pair p's 2 chunks at 4p
         float2 s[P];     // {d, d * sum(q)} of the output lane's (token, block) per pair
     };
+    // (steps past the part read the zero bytes after the image: zero codes and zero scales)
     auto load_x = [&](Xf &x, int sl) __attribute__((always_inline)) {
-        const uint32_t sc = (uint32_t)min(sl, n_loc - 1);
-        const uint8_t *cp = xl + xc + sc * xstep;
-        const uint8_t *sp = xl + xsc + sc * SB;
+        const bool live = sl < n_loc;
+        const uint8_t *cp = live ? xl + xc + (uint32_t)sl * xstep : xl + nbx;
+        const uint8_t *sp = live ? xl + xsc + (uint32_t)sl * SB : xl + nbx;
 #pragma unroll
         for (int p = 0; p < P; ++p) {
             if constexpr (TOK == 4) {
@@ -524,7 +583,7 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
         }
     };
     mma_f2 acc[RT][2] = {};   // tile t, rows 4g + {0, 1}, {2, 3}
-    auto compute = [&](W (&w)[RT], Xf &x) __attribute__((always_inline)) {
+    auto compute = [&](auto &w, Xf &x) __attribute__((always_inline)) {
         pin(x.c);
         pin(x.s);
 #pragma unroll
@@ -572,42 +631,80 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
         pin(acc);
     };
 
-    W F[D][RT];
-    Xf X[D];
+    auto stage_x = [&]() __attribute__((always_inline)) {
 #pragma unroll
-    for (int d = 0; d < D - 1; ++d)
-#pragma unroll
-        for (int t = 0; t < RT; ++t) {
-            if constexpr (!(MMA_EXP & 2)) F[d][t].load(wrs(step_of(d)), lo[t]);
-            F[d][t].h = wave & 1;
+        for (int k = 0; k < NP; ++k) {
+            const uint32_t o = threadIdx.x * 16 + k * 16384;
+            if (o < nbx) {
+                if constexpr (MMA_EXP & 1) *reinterpret_cast<uint4 *>(xl + o) = make_uint4(o, 1, 2, 3);
+                else *reinterpret_cast<uint4 *>(xl + o) = make_uint4(stg[k][0], stg[k][1], stg[k][2], stg[k][3]);
+            }
         }
+        if (threadIdx.x < 8) *reinterpret_cast<uint4 *>(xl + nbx + threadIdx.x * 16) = make_uint4(0, 0, 0, 0);
+        lds_barrier();
+    };
+    if constexpr (!PR) {
+        W F[D][RT];
+        Xf X[D];
 #pragma unroll
-    for (int k = 0; k < NP; ++k) {
-        const uint32_t o = threadIdx.x * 16 + k * 16384;
-        if (o < nbx) {
-            if constexpr (MMA_EXP & 1) *reinterpret_cast<uint4 *>(xl + o) = make_uint4(o, 1, 2, 3);
-            else *reinterpret_cast<uint4 *>(xl + o) = make_uint4(stg[k][0], stg[k][1], stg[k][2], stg[k][3]);
-        }
-    }
-    if (threadIdx.x < 8) *reinterpret_cast<uint4 *>(xl + nbx + threadIdx.x * 16) = make_uint4(0, 0, 0, 0);
-    lds_barrier();
-#pragma unroll
-    for (int d = 0; d < D - 1; ++d) load_x(X[d], step_of(d));
-    auto step = [&](auto k_c, int i) __attribute__((always_inline)) {
-        constexpr int k = decltype(k_c)::value;
-        if (i + D - 1 < NSTEP) {
-            const int sl = step_of(i + D - 1);
+        for (int d = 0; d < D - 1; ++d)
 #pragma unroll
             for (int t = 0; t < RT; ++t) {
-                if constexpr (!(MMA_EXP & 2)) F[(k + D - 1) % D][t].load(wrs(sl), lo[t]);
-                F[(k + D - 1) % D][t].h = wave & 1;
+                if constexpr (!(MMA_EXP & 2)) F[d][t].load(wrs(step_of(d)), lo[t]);
+                F[d][t].h = wave & 1;
             }
-            load_x(X[(k + D - 1) % D], sl);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        compute(F[k], X[k]);
-    };
-    mma_run_steps<D>(step, std::make_integer_sequence<int, NSTEP>{});
+        stage_x();
+#pragma unroll
+        for (int d = 0; d < D - 1; ++d) load_x(X[d], step_of(d));
+        auto step = [&](auto k_c, int i) __attribute__((always_inline)) {
+            constexpr int k = decltype(k_c)::value;
+            if (i + D - 1 < NSTEP) {
+                const int sl = step_of(i + D - 1);
+#pragma unroll
+                for (int t = 0; t < RT; ++t) {
+                    if constexpr (!(MMA_EXP & 2)) F[(k + D - 1) % D][t].load(wrs(sl), lo[t]);
+                    F[(k + D - 1) % D][t].h = wave & 1;
+                }
+                load_x(X[(k + D - 1) % D], sl);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            compute(F[k], X[k]);
+        };
+        mma_run_steps<D>(step, std::make_integer_sequence<int, NSTEP>{});
+    } else {
+        // one pair (two steps) ahead; a pair's descriptor is its first step's (the second step's
+        // blocks follow in the row; past the part its columns are zero)
+        constexpr int DP = 2;
+        using WP = MmaPair<T, TOK>;
+        MmaLanes lp[RT];
+#pragma unroll
+        for (int t = 0; t < RT; ++t) lp[t] = WP::lanes(c + 16 * t, g, nb01);
+        WP F[DP][RT];
+        Xf X[DP][2];
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+            if constexpr (!(MMA_EXP & 2)) F[0][t].load(wrs(step_of(0)), lp[t]);
+        stage_x();
+        load_x(X[0][0], step_of(0));
+        load_x(X[0][1], step_of(1));
+        auto pstep = [&](auto k_c, int j) __attribute__((always_inline)) {
+            constexpr int k = decltype(k_c)::value;
+            if (j + 1 < NSTEP / 2) {
+#pragma unroll
+                for (int t = 0; t < RT; ++t)
+                    if constexpr (!(MMA_EXP & 2)) F[(k + 1) % DP][t].load(wrs(step_of(2 * j + 2)), lp[t]);
+                load_x(X[(k + 1) % DP][0], step_of(2 * j + 2));
+                load_x(X[(k + 1) % DP][1], step_of(2 * j + 3));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            MmaHalf<T, TOK> H0[RT], H1[RT];
+#pragma unroll
+            for (int t = 0; t < RT; ++t) F[k][t].split(H0[t], H1[t]);
+            compute(H0, X[k][0]);
+            compute(H1, X[k][1]);
+        };
+        mma_run_steps<DP>(pstep, std::make_integer_sequence<int, NSTEP / 2>{});
+    }
 
     // sum the block groups (columns c, c + TOK, ... of the 16-lane row), then the waves in order
 #pragma unroll
@@ -685,12 +782,12 @@ size_t mmvq_mma_img_bytes(int, const MmArgs &a) {
     return (size_t)mma_steps(a) * mma_tok_of(a) * 160 * a.ne12 * a.ne13;
 }
 
-template <int T, int TOK, int RT, int NS>
+template <int T, int TOK, int RT, int NS, bool PR>
 static hipError_t mma_main(const MmArgs &a, const uint8_t *img, int S, int part, int kh, hipStream_t st) {
     if constexpr (MMA_KS * NS * mma_step_bytes<TOK>() > MMA_LDS_IMG + 16 * mma_step_bytes<TOK>()) {
         return hipErrorInvalidValue;   // (runs whose image cannot fit: never selected)
     } else {
-        auto kern = mmvq_mma_kernel<T, TOK, RT, NS>;
+        auto kern = mmvq_mma_kernel<T, TOK, RT, NS, PR>;
         const size_t lds = (size_t)part * mma_step_bytes<TOK>() + 128;
         static bool attr_set = false;   // per instantiation; > 64 KB of dynamic LDS needs the attribute
         if (lds > 64 * 1024 && !attr_set) {
@@ -710,22 +807,33 @@ static hipError_t mma_main(const MmArgs &a, const uint8_t *img, int S, int part,
     }
 }
 
-template <int T, int TOK, int RT>
+template <int T, int TOK, int RT, bool PR>
 static hipError_t mma_run(const MmArgs &a, const uint8_t *img, int S, int part, int kh, hipStream_t st) {
-    switch (mma_nstep(part)) {
-        case 1: return mma_main<T, TOK, RT, 1>(a, img, S, part, kh, st);
-        case 2: return mma_main<T, TOK, RT, 2>(a, img, S, part, kh, st);
-        case 3: return mma_main<T, TOK, RT, 3>(a, img, S, part, kh, st);
-        case 4: return mma_main<T, TOK, RT, 4>(a, img, S, part, kh, st);
-        case 5: return mma_main<T, TOK, RT, 5>(a, img, S, part, kh, st);
-        case 6: return mma_main<T, TOK, RT, 6>(a, img, S, part, kh, st);
-        case 7: return mma_main<T, TOK, RT, 7>(a, img, S, part, kh, st);
-        case 8: return mma_main<T, TOK, RT, 8>(a, img, S, part, kh, st);
-        case 10: return mma_main<T, TOK, RT, 10>(a, img, S, part, kh, st);
-        case 12: return mma_main<T, TOK, RT, 12>(a, img, S, part, kh, st);
-        case 14: return mma_main<T, TOK, RT, 14>(a, img, S, part, kh, st);
-        default: return hipErrorInvalidValue;
+    int ns = mma_nstep(part);
+    if constexpr (PR) ns = (ns + 1) & ~1;   // (pairs: even runs)
+    switch (ns) {
+        case 1: if constexpr (!PR) return mma_main<T, TOK, RT, 1, PR>(a, img, S, part, kh, st); else break;
+        case 2: return mma_main<T, TOK, RT, 2, PR>(a, img, S, part, kh, st);
+        case 3: if constexpr (!PR) return mma_main<T, TOK, RT, 3, PR>(a, img, S, part, kh, st); else break;
+        case 4: return mma_main<T, TOK, RT, 4, PR>(a, img, S, part, kh, st);
+        case 5: if constexpr (!PR) return mma_main<T, TOK, RT, 5, PR>(a, img, S, part, kh, st); else break;
+        case 6: return mma_main<T, TOK, RT, 6, PR>(a, img, S, part, kh, st);
+        case 7: if constexpr (!PR) return mma_main<T, TOK, RT, 7, PR>(a, img, S, part, kh, st); else break;
+        case 8: return mma_main<T, TOK, RT, 8, PR>(a, img, S, part, kh, st);
+        case 10: return mma_main<T, TOK, RT, 10, PR>(a, img, S, part, kh, st);
+        case 12: return mma_main<T, TOK, RT, 12, PR>(a, img, S, part, kh, st);
+        case 14: return mma_main<T, TOK, RT, 14, PR>(a, img, S, part, kh, st);
+        default: break;
     }
+    return hipErrorInvalidValue;
+}
+
+// paired steps (GGML_MI355X_MMA_PAIR=1): Q4_0 / Q8_0 rows contiguous and 4-byte aligned
+static bool mma_pair_ok(int type, const MmArgs &a) {
+    if (type != T_Q4_0 && type != T_Q8_0) return false;
+    if (mma_env("GGML_MI355X_MMA_PAIR", 0) != 1) return false;
+    const int64_t row = (int64_t)(a.K / 32) * (type == T_Q4_0 ? 18 : 34);
+    return a.nb01 == row && row % 4 == 0 && a.nb02 % 4 == 0 && a.nb03 % 4 == 0 && (reinterpret_cast<uintptr_t>(a.w) & 3) == 0;
 }
 
 template <int T, int TOK>
@@ -735,8 +843,14 @@ static hipError_t mma_tok(const MmArgs &a, uint8_t *img, hipStream_t st) {
     if (a.x_aligned16) hipLaunchKernelGGL((mma_prequant<TOK, true>), pg, dim3(TOK * 16), 0, st, a, img, kh == 2);
     else hipLaunchKernelGGL((mma_prequant<TOK, false>), pg, dim3(TOK * 16), 0, st, a, img, kh == 2);
     hipError_t e;
-    if constexpr (T == T_Q5_K) e = mma_run<T, TOK, 1>(a, img, S, part, kh, st);
-    else e = mma_rt() == 2 ? mma_run<T, TOK, 2>(a, img, S, part, kh, st) : mma_run<T, TOK, 1>(a, img, S, part, kh, st);
+    if constexpr (T == T_Q5_K) e = mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
+    else if constexpr (T == T_Q4_0 || T == T_Q8_0) {
+        if (mma_pair_ok(T, a)) {   // (Q8_0 pairs: one tile per workgroup, two would spill)
+            if constexpr (T == T_Q8_0) e = mma_run<T, TOK, 1, true>(a, img, S, part, kh, st);
+            else e = mma_rt() == 2 ? mma_run<T, TOK, 2, true>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, true>(a, img, S, part, kh, st);
+        }
+        else e = mma_rt() == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
+    } else e = mma_rt() == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
     return e != hipSuccess ? e : hipGetLastError();
 }
 

@@ -138,3 +138,19 @@ def test_mma_one_column(mm, t):
     got = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 1})
     valu = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 0})
     assert qref.nmse(got, valu) <= 1e-10
+
+
+@pytest.mark.parametrize("K", [4096, 4160, 14336])
+@pytest.mark.parametrize("M_", [3, 8])
+@pytest.mark.parametrize("t", [qref.Q4_0, qref.Q8_0], ids=lambda t: qref.NAMES[t])
+def test_mma_paired_steps(mm, t, M_, K):
+    """paired steps (GGML_MI355X_MMA_PAIR=1): a lane loads two adjacent blocks and permlane swaps
+    hand each lane its block of both steps; K = 4160 ends inside a double step (the pair's second
+    step past K meets zero columns); ragged rows; run twice for bitwise repeatability"""
+    a, b, out_ne = operands(t, 200, M_, K, 13)
+    env = {"GGML_MI355X_MMA": 1, "GGML_MI355X_MMA_PAIR": 1}
+    g1 = run_with(mm, a, b, out_ne, env)
+    g2 = run_with(mm, a, b, out_ne, env)
+    assert np.array_equal(g1.view(np.uint32), g2.view(np.uint32)), "result not repeatable"
+    valu = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 0})
+    assert qref.nmse(g1, valu) <= 1e-10
