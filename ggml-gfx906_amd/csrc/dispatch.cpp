@@ -183,24 +183,29 @@ static int ring_pre_min() {
 }
 
 // the int8 MFMA mat-vec (mmvq_mma.hip: the weights read once, the columns packed
-// block-diagonally into the MFMA's 16 columns, flat in the column count). Measured against the
-// per-column VALU kernels (profiles/r05_mma_sweep.txt, 5 shapes x 4 types x 4..8 columns) it is
-// never slower for Q4_0 / Q8_0 from 5 columns (0.67-1.00x) and faster for Q4_K from 5 / Q5_K from
-// 6 columns at K <= 4096; slower below 5 columns and for the K-quants at long K.
+// block-diagonally into the MFMA's 16 columns, flat in the column count). From a sweep against
+// the per-column VALU kernels (profiles/r05_mma_sweep2.txt: 5 shapes x 4 types x 3..8 columns,
+// single matrices), the first column count from which it is used:
+//   Q4_0  K >= 8192: 4 (paired steps, mmvq_mma.hip); else N >= 8192: 5
+//   Q8_0  K >= 8192: 3 (paired steps from K >= 12288); else N >= 8192: 5
+//   Q4_K  K >= 8192 or N >= 8192: 5
+//   Q5_K  K < 8192: 5
+// everywhere else the VALU kernels are as fast or faster (0.65-0.99x where it is used).
 // GGML_MI355X_MMA=N: from N columns on for every type it takes; 0: never.
-static int mma_min_cols(int type, int K, int slices) {
+static int mma_min_cols(int type, int K, int N, int slices) {
     const char *e = getenv("GGML_MI355X_MMA");   // per call: tests switch it
     if (e != nullptr) {
         const int v = atoi(e);
         return v <= 0 ? 1 << 30 : v;
     }
-    if (slices > 1) return 1 << 30;   // (8 batch slices: 2-4 % slower than the VALU kernels)
+    constexpr int NEVER = 1 << 30;
+    if (slices > 1) return NEVER;   // (8 batch slices: 2-4 % slower than the VALU kernels)
     switch (type) {
-        case T_Q4_0:
-        case T_Q8_0: return 5;
-        case T_Q4_K: return K <= 4096 ? 5 : 1 << 30;
-        case T_Q5_K: return K <= 4096 ? 6 : 1 << 30;
-        default: return 1 << 30;
+        case T_Q4_0: return K >= 8192 ? 4 : N >= 8192 ? 5 : NEVER;
+        case T_Q8_0: return K >= 8192 ? 3 : N >= 8192 ? 5 : NEVER;
+        case T_Q4_K: return K >= 8192 || N >= 8192 ? 5 : NEVER;
+        case T_Q5_K: return K < 8192 ? 5 : NEVER;
+        default: return NEVER;
     }
 }
 
@@ -208,7 +213,7 @@ static int mma_min_cols(int type, int K, int slices) {
 // mutex; nullptr = no pre-quantized images)
 static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st, Scratch *scratch = nullptr) {
     const int rpw = pick_rpw(type, (int64_t)m.N * m.ne12 * m.ne13);
-    if (scratch != nullptr && ncols >= mma_min_cols(type, m.K, m.ne12 * m.ne13) && ncols <= 8) {
+    if (scratch != nullptr && ncols >= mma_min_cols(type, m.K, m.N, m.ne12 * m.ne13) && ncols <= 8) {
         MmArgs g = m;
         g.x = m.x + (int64_t)c0 * m.nb11;
         g.dst = m.dst + (int64_t)c0 * m.nb1;

@@ -828,10 +828,12 @@ static hipError_t mma_run(const MmArgs &a, const uint8_t *img, int S, int part, 
     return hipErrorInvalidValue;
 }
 
-// paired steps (GGML_MI355X_MMA_PAIR=1): Q4_0 / Q8_0 rows contiguous and 4-byte aligned
+// paired steps: Q4_0 rows from K = 8192, Q8_0 from 12288 (profiles/r05_mma_sweep2.txt), rows
+// contiguous and 4-byte aligned; GGML_MI355X_MMA_PAIR=1 / 0 forces them on / off
 static bool mma_pair_ok(int type, const MmArgs &a) {
     if (type != T_Q4_0 && type != T_Q8_0) return false;
-    if (mma_env("GGML_MI355X_MMA_PAIR", 0) != 1) return false;
+    const int pe = mma_env("GGML_MI355X_MMA_PAIR", -1);
+    if (pe == 0 || (pe < 0 && a.K < (type == T_Q4_0 ? 8192 : 12288))) return false;
     const int64_t row = (int64_t)(a.K / 32) * (type == T_Q4_0 ? 18 : 34);
     return a.nb01 == row && row % 4 == 0 && a.nb02 % 4 == 0 && a.nb03 % 4 == 0 && (reinterpret_cast<uintptr_t>(a.w) & 3) == 0;
 }

@@ -123,10 +123,12 @@ def test_mma_wave_steps(mm, t, K):
 @pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])
 def test_mma_layouts(mm, t, layout):
     """one K part and/or one 16-row tile per workgroup (GGML_MI355X_MMA_KH / _RT) against the
-    VALU path; ragged rows (N % 32 = 20)"""
+    VALU path, unpaired steps (Q4_0 / Q8_0 at this K would pair by default); ragged rows
+    (N % 32 = 20)"""
     kh, rt = layout
     a, b, out_ne = operands(t, 180, 6, 8192, 11)
-    got = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 2, "GGML_MI355X_MMA_KH": kh, "GGML_MI355X_MMA_RT": rt})
+    got = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 2, "GGML_MI355X_MMA_KH": kh, "GGML_MI355X_MMA_RT": rt,
+                                      "GGML_MI355X_MMA_PAIR": 0})
     valu = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 0})
     assert qref.nmse(got, valu) <= 1e-10
 
@@ -140,7 +142,7 @@ def test_mma_one_column(mm, t):
     assert qref.nmse(got, valu) <= 1e-10
 
 
-@pytest.mark.parametrize("K", [4096, 4160, 14336])
+@pytest.mark.parametrize("K", [4096, 4160, 14336, 28672])
 @pytest.mark.parametrize("M_", [3, 8])
 @pytest.mark.parametrize("t", [qref.Q4_0, qref.Q8_0], ids=lambda t: qref.NAMES[t])
 def test_mma_paired_steps(mm, t, M_, K):
