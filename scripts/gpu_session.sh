@@ -61,6 +61,7 @@ for step in "$@"; do
         profsingles) run profsingles 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profsingles -o run -- python scripts/prof_singles.py ;;
         profgpt2) run profgpt2 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profgpt2 -o run -- python scripts/gpt2_bench.py 1 256 1 ;;
         gpt2b) run gpt2b 300 python scripts/gpt2_bench.py 1 256 1 ;;
+        pmcfetch) run pmcfetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/pmcfetch -o pmc -- python scripts/mmvq_bench.py q4_0:14336:4096:1:1 q4_0:14336:4096:8:1 q8_0:14336:4096:1:1 q8_0:14336:4096:8:1 q4_K:14336:4096:1:1 q4_K:14336:4096:8:1 && python scripts/pmc_summary.py $OUT/pmcfetch > $OUT/pmcfetch_summary.txt && find $OUT/pmcfetch -name "*.csv" -size +2M -delete ;;
         gpt2tests) run gpt2tests 900 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpt2.py tests/test_gpt2_example.py tests/test_graph_fusion.py tests/test_gpt2_pipeline.py -m gpu ;;
         plugab) run plugab 600 bash scripts/plugin_gpt2_ab.sh ;;
         pmcring) run pmcring 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/pmcring -o pmc -- python scripts/mmvq_bench.py q4_0:14336:4096:1:8 q4_0:14336:4096:8:8 q4_K:14336:4096:8:8
