@@ -18,16 +18,23 @@
 //    (128 K) and lane (row r, k-group g) owns block g of row r for the whole step;
 //  * TOK = 8 (5..8 columns): 2 blocks per MFMA, 16 K of each; two pairs of MFMAs per step,
 //    lane g holds half g & 1 of block g >> 1 of the pair (Q4_0 / Q8_0: a permlane exchange of
-//    the halves of the blocks the lanes loaded whole);
-//  * the B fragments come from the columns' records, quantized once per call by mma_prequant
-//    (int8 per 32-block, d = amax / 127, round-to-nearest-even, exactly as the other mat-vec
-//    kernels); a lane outside its group's range loads from an offset past the buffer's end,
-//    which returns zeros without a memory access;
+//    the halves of the blocks the lanes loaded whole; K-quants: each lane loads its own qs run's
+//    half and trades the other run's half with lane g ^ 2);
+//  * the B fragments come from the columns' images (int8 per 32-block, d = amax / 127,
+//    round-to-nearest-even, exactly as the other mat-vec kernels), quantized once per call by
+//    mma_prequant and staged per workgroup in LDS — or, for K <= 4096 on request, quantized by
+//    the workgroup itself (no pre-pass launch); lanes outside their group's range read a zero
+//    region after the image;
 //  * the row scales reach the output lanes through a per-wave LDS slot; Q4_0 codes stay
 //    unsigned (0..15) and the - 8 comes back through d * sum(q) of the column block;
-//  * a workgroup = 16 waves on one 16-row tile, wave w a straight-line run of K steps; the
-//    block groups are summed across lanes (DPP) and the waves through LDS in a fixed order,
-//    so no workgroup depends on another and results repeat bit for bit.
+//  * a workgroup = RT 16-row tiles sharing the column fragments x one of KH K parts, 16 waves
+//    striding its steps in straight-line code; the block groups are summed across lanes (DPP),
+//    the waves through LDS in a fixed order, and two K parts add into the zeroed dst (two terms:
+//    order-free), so results repeat bit for bit;
+//  * weight loads go through a per-step buffer descriptor (scalar base, per-lane constant
+//    offsets; steps past K have no records, so they read zeros); the number of load
+//    instructions per step is what bounds the kernel, so Q4_0 / Q8_0 at long K
+//    load two adjacent blocks per lane for two steps at once (paired steps).
 #include <type_traits>
 
 // measurement builds only (scripts/mma_exp.sh; results wrong by design): bit 1 = no activation
@@ -45,7 +52,6 @@ typedef int i32x4_t __attribute__((ext_vector_type(4)));
 constexpr int MMA_STEP_K = 128;   // K per step: 4 blocks of 32
 constexpr int MMA_KS = 16;        // waves per workgroup
 constexpr uint32_t MMA_RSRC_W3 = 0x00020000u;   // raw buffer descriptor dword 3 (as mmq8.hip)
-constexpr uint32_t MMA_OOB = 0x80000000u;       // an offset past any image: loads return zeros
 
 // activation image of one (slice, step): codes [t TOK][block 4][32 B] in chunk order, then
 // [t][block] {d, d * sum(q)} f32
