@@ -507,7 +507,7 @@ __global__ __launch_bounds__(TOK * 16) void mma_prequant(const MmArgs a, uint8_t
 // the allocator puts on a back-edge move sets whose loads are still in flight, and each copy
 // waits for its load). Each step loads its weights D - 1 steps ahead; all weight addresses are
 // per-lane constants plus the step's descriptor base (scalar arithmetic).
-template <int T, int TOK, int RT, int NSTEP, bool PR, bool FQ = false, bool XA = false>
+template <int T, int TOK, int RT, int NSTEP, bool PR>
 __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a, const uint8_t *__restrict__ img, int n_steps, int part_steps) {
     using W = MmaW<T, TOK>;
     static_assert(!PR || ((T == T_Q4_0 || T == T_Q8_0) && NSTEP % 2 == 0), "paired steps: Q4_0 / Q8_0, even runs");
@@ -550,33 +550,11 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
     const uint32_t nbx = (uint32_t)(n_loc * SB);
     const __amdgpu_buffer_rsrc_t xr =
         __builtin_amdgcn_make_buffer_rsrc((void *)(img + ((int64_t)z * n_steps + s0) * SB), 0, nbx, MMA_RSRC_W3);
-    constexpr int NP = FQ ? 1 : (MMA_KS * NSTEP * SB + 16383) / 16384;
-    [[maybe_unused]] uint32_t stg[NP][4];
-    if constexpr (!FQ && !(MMA_EXP & 1)) {
+    constexpr int NP = (MMA_KS * NSTEP * SB + 16383) / 16384;
+    uint32_t stg[NP][4];
+    if constexpr (!(MMA_EXP & 1)) {
 #pragma unroll
         for (int k = 0; k < NP; ++k) bl16(xr, threadIdx.x * 16 + k * 16384, stg[k]);
-    }
-    // fused quantization (FQ, short K): the workgroup quantizes its columns itself, chunk ci =
-    // thread + 1024 it = (step, column t, block j, chunk m) in the image's order (the 4 chunks of
-    // a block in consecutive lanes, as mma_prequant); loads first, unconditional (clamped step)
-    constexpr int NQC = FQ ? (NSTEP * MMA_KS * TOK * 16 + 1023) / 1024 : 1;
-    [[maybe_unused]] float xv[NQC][8];
-    auto chunk = [&](int it, int &sl, int &t, int &j, int &m) __attribute__((always_inline)) {
-        const int ci = threadIdx.x + 1024 * it;
-        m = ci & 3;
-        j = (ci >> 2) & 3;
-        t = (ci >> 4) % TOK;
-        sl = (ci >> 4) / TOK;
-    };
-    if constexpr (FQ) {
-#pragma unroll
-        for (int it = 0; it < NQC; ++it) {
-            int sl, t, j, m;
-            chunk(it, sl, t, j, m);
-            const float *col = reinterpret_cast<const float *>(a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13 +
-                                                               (int64_t)min(t, a.M - 1) * a.nb11);
-            mma_xload<XA>(a, col, s0 + min(sl, n_loc - 1), j, m, xv[it]);
-        }
     }
     // B role: column c = token bt of block group bg; codes only where k-group g is in bg's range
     // (the other lanes read the zero bytes after the image, at a fixed address)
@@ -660,21 +638,12 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
     };
 
     auto stage_x = [&]() __attribute__((always_inline)) {
-        if constexpr (FQ) {
 #pragma unroll
-            for (int it = 0; it < NQC; ++it) {
-                int sl, t, j, m;
-                chunk(it, sl, t, j, m);
-                if (sl < n_loc) mma_quant<TOK>(a, xv[it], s0 + sl, j, t, m, xl + sl * SB);   // (uniform per wave)
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < NP; ++k) {
-                const uint32_t o = threadIdx.x * 16 + k * 16384;
-                if (o < nbx) {
-                    if constexpr (MMA_EXP & 1) *reinterpret_cast<uint4 *>(xl + o) = make_uint4(o, 1, 2, 3);
-                    else *reinterpret_cast<uint4 *>(xl + o) = make_uint4(stg[k][0], stg[k][1], stg[k][2], stg[k][3]);
-                }
+        for (int k = 0; k < NP; ++k) {
+            const uint32_t o = threadIdx.x * 16 + k * 16384;
+            if (o < nbx) {
+                if constexpr (MMA_EXP & 1) *reinterpret_cast<uint4 *>(xl + o) = make_uint4(o, 1, 2, 3);
+                else *reinterpret_cast<uint4 *>(xl + o) = make_uint4(stg[k][0], stg[k][1], stg[k][2], stg[k][3]);
             }
         }
         if (threadIdx.x < 8) *reinterpret_cast<uint4 *>(xl + nbx + threadIdx.x * 16) = make_uint4(0, 0, 0, 0);
@@ -819,12 +788,12 @@ size_t mmvq_mma_img_bytes(int, const MmArgs &a) {
     return (size_t)mma_steps(a) * mma_tok_of(a) * 160 * a.ne12 * a.ne13;
 }
 
-template <int T, int TOK, int RT, int NS, bool PR, bool FQ = false, bool XA = false>
+template <int T, int TOK, int RT, int NS, bool PR>
 static hipError_t mma_main(const MmArgs &a, const uint8_t *img, int S, int part, int kh, hipStream_t st) {
     if constexpr (MMA_KS * NS * mma_step_bytes<TOK>() > MMA_LDS_IMG + 16 * mma_step_bytes<TOK>()) {
         return hipErrorInvalidValue;   // (runs whose image cannot fit: never selected)
     } else {
-        auto kern = mmvq_mma_kernel<T, TOK, RT, NS, PR, FQ, XA>;
+        auto kern = mmvq_mma_kernel<T, TOK, RT, NS, PR>;
         const size_t lds = (size_t)part * mma_step_bytes<TOK>() + 128;
         static bool attr_set = false;   // per instantiation; > 64 KB of dynamic LDS needs the attribute
         if (lds > 64 * 1024 && !attr_set) {
@@ -875,24 +844,8 @@ static bool mma_pair_ok(int type, const MmArgs &a) {
     return a.nb01 == row && row % 4 == 0 && a.nb02 % 4 == 0 && a.nb03 % 4 == 0 && (reinterpret_cast<uintptr_t>(a.w) & 3) == 0;
 }
 
-// fused quantization (GGML_MI355X_MMA_FUSE=1): up to 32 steps (K <= 4096), one K part and one
-// tile per workgroup, no pre-pass launch
-static bool mma_fuse_ok(const MmArgs &a) { return mma_env("GGML_MI355X_MMA_FUSE", 0) == 1 && mma_steps(a) <= 32; }
-
-template <int T, int TOK>
-static hipError_t mma_fused(const MmArgs &a, hipStream_t st) {
-    const int S = mma_steps(a);
-    hipError_t e;
-    if (a.x_aligned16) e = mma_nstep(S) == 1 ? mma_main<T, TOK, 1, 1, false, true, true>(a, nullptr, S, S, 1, st)
-                                              : mma_main<T, TOK, 1, 2, false, true, true>(a, nullptr, S, S, 1, st);
-    else e = mma_nstep(S) == 1 ? mma_main<T, TOK, 1, 1, false, true, false>(a, nullptr, S, S, 1, st)
-                               : mma_main<T, TOK, 1, 2, false, true, false>(a, nullptr, S, S, 1, st);
-    return e != hipSuccess ? e : hipGetLastError();
-}
-
 template <int T, int TOK>
 static hipError_t mma_tok(const MmArgs &a, uint8_t *img, hipStream_t st) {
-    if (mma_fuse_ok(a)) return mma_fused<T, TOK>(a, st);
     const int S = mma_steps(a), kh = mma_kh(a), part = mma_part_steps(a, kh);
     const dim3 pg(S, a.ne12 * a.ne13);
     if (a.x_aligned16) hipLaunchKernelGGL((mma_prequant<TOK, true>), pg, dim3(TOK * 16), 0, st, a, img, kh == 2);

@@ -156,19 +156,3 @@ def test_mma_paired_steps(mm, t, M_, K):
     assert np.array_equal(g1.view(np.uint32), g2.view(np.uint32)), "result not repeatable"
     valu = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 0})
     assert qref.nmse(g1, valu) <= 1e-10
-
-
-@pytest.mark.parametrize("K", [448, 1024, 4096])
-@pytest.mark.parametrize("M_", [1, 3, 5, 8])
-@pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])
-def test_mma_fused_quantization(mm, t, M_, K):
-    """the workgroup quantizes its own columns into LDS (GGML_MI355X_MMA_FUSE=1, K <= 4096: no
-    pre-pass launch, one K part); K = 448: a partial last step (Q4_0 / Q8_0), the K-quants at
-    512 instead; ragged rows"""
-    if qref.BLCK[t] == 256 and K % 256:
-        K = 512
-    a, b, out_ne = operands(t, 150, M_, K, 17)
-    got = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 1, "GGML_MI355X_MMA_FUSE": 1})
-    valu = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 0})
-    assert np.all(np.isfinite(got))
-    assert qref.nmse(got, valu) <= 1e-10
