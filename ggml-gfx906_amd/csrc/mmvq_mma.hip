@@ -22,9 +22,8 @@
 //    half and trades the other run's half with lane g ^ 2);
 //  * the B fragments come from the columns' images (int8 per 32-block, d = amax / 127,
 //    round-to-nearest-even, exactly as the other mat-vec kernels), quantized once per call by
-//    mma_prequant and staged per workgroup in LDS — or, for K <= 4096 on request, quantized by
-//    the workgroup itself (no pre-pass launch); lanes outside their group's range read a zero
-//    region after the image;
+//    mma_prequant and staged per workgroup in LDS; lanes outside their group's range read a
+//    zero region after the image;
 //  * the row scales reach the output lanes through a per-wave LDS slot; Q4_0 codes stay
 //    unsigned (0..15) and the - 8 comes back through d * sum(q) of the column block;
 //  * a workgroup = RT 16-row tiles sharing the column fragments x one of KH K parts, 16 waves
