@@ -398,6 +398,17 @@ int main(int argc, char **argv) {
     gen_mul_mat(GGML_TYPE_Q4_0, 16, 1, 131072, 1, 1, 1, 1, id4, false);
     gen_mul_mat(GGML_TYPE_Q6_K, 16, 2, 131072, 1, 1, 1, 1, id4, false);
 
+    // round 5, later: the int8-MFMA mat-vec's default forms (dispatch.cpp mma_min_cols) — paired
+    // steps at 4 tokens (Q4_0 from 4 columns, Q8_0 from 3 at K = 14336), the K-quants' 8-token
+    // form (Q4_K at K = 11008, Q5_K at K = 4096) and the wide-N rule (N = 8192 at K = 4096)
+    gen_mul_mat(GGML_TYPE_Q4_0, 256, 4, 14336, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q8_0, 256, 3, 14336, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q8_0, 256, 4, 14336, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q4_K, 256, 6, 11008, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q5_K, 256, 6, 4096, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q4_0, 8192, 5, 4096, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q4_K, 8192, 8, 4096, 1, 1, 1, 1, id4, false);
+
     std::string path = g_dir + "/manifest.json";
     FILE *f = fopen(path.c_str(), "w");
     fprintf(f, "{\n\"generator\": \"oracle/gen_golden.cpp linked to oracle/_ref/libggml-ref.so (reference sources, oracle/ref.mk)\",\n"
