@@ -295,31 +295,58 @@ template <int TOK> struct MmaW<T_Q8_0, TOK> {
 // loads the 16-B header.
 //   TOK 4: lane g loads the 32-B run of its sub-block g;
 //   TOK 8: lane g loads bytes 8 (g & 1) + 16 q .. + 8 (q = 0, 1) of run 2h + p for both pairs
+// K-quant runs: lanes g and g ^ 1 (adjacent 16-lane rows) each load one 16-byte half of a 32-byte
+// run and trade the other half by one permlane16 swap per dword.
+// whole run (4 tokens): both lanes want all 32 bytes. With A = B = the lane's own half, the swap
+// leaves B = bytes 0..15 and A = bytes 16..31 on both lanes (the even lane's B and the odd lane's
+// A are their own halves, the others the partner's).
+__device__ __forceinline__ void run_whole(const uint32_t (&own)[4], uint32_t (&q)[8]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t A = own[k], B = own[k];
+        swap16(A, B);
+        q[k] = B;
+        q[4 + k] = A;
+    }
+}
+// half g & 1 of a run (8 tokens): lane a = g & 1 wants bytes 8a..8a+7 and 16+8a..16+8a+7; it
+// loaded 16a..16a+15. With X = own dwords 2, 3 and Y = own dwords 0, 1, the swap leaves
+// {Y, X} = the wanted 16 bytes on both lanes.
+__device__ __forceinline__ void run_half(const uint32_t (&own)[4], uint32_t (&q)[4]) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        uint32_t X = own[2 + k], Y = own[k];
+        swap16(X, Y);
+        q[k] = Y;
+        q[2 + k] = X;
+    }
+}
+
+// Q4_K: step s = half h = s & 1 of super-block s >> 1 (h is the wave's: s = wave + 16 i); sub-block
+// 4h + b is nibble b & 1 of qs run 2h + (b >> 1) (32 B at 16 + 32 (2h + (b >> 1))); every lane
+// loads the 16-B header and half g & 1 of the run of its sub-block g (run_whole / run_half).
+//   TOK 4: lane g uses the whole run of sub-block g;
+//   TOK 8: lane g uses half g & 1 of run 2h + (g >> 1), and trades it for run 2h + 1 - (g >> 1)'s
+//          with lane g ^ 2 (runs_to_pairs)
 template <int TOK> struct MmaW<T_Q4_K, TOK> {
     static constexpr int NSC = 2;
-    uint32_t H[4], Q[TOK == 4 ? 8 : 4];
+    uint32_t H[4], QV[4];
     int h;
     __device__ static uint32_t step_off(int s) { return 144u * (uint32_t)(s >> 1); }
-    // b: TOK 4 the 32-B run of sub-block g; TOK 8 half g & 1 of run 2h + (g >> 1) (bytes 8 (g & 1)
-    // and 16 + 8 (g & 1), 8 each): the other run's half comes from lane g ^ 2 (runs_to_pairs)
     __device__ static MmaLanes lanes(int r, int g, int h, uint32_t nb01, uint32_t) {
         const uint32_t row = r * nb01;
-        return {row, row + 16 + 32 * (2 * h + (g >> 1)) + (TOK == 4 ? 0 : 8 * (g & 1)), 0};
+        return {row, row + 16 + 32 * (2 * h + (g >> 1)) + 16 * (g & 1), 0};
     }
     __device__ inline void load(__amdgpu_buffer_rsrc_t rs, const MmaLanes &lo) {
         bl16(rs, lo.a, H);
-        if constexpr (TOK == 4) {
-            bl16(rs, lo.b, Q);
-            bl16(rs, lo.b + 16, Q + 4);
-        } else {
-            bl8(rs, lo.b, Q);
-            bl8(rs, lo.b + 16, Q + 2);
-        }
+        bl16(rs, lo.b, QV);
     }
     __device__ inline void frags(long (&A)[4], int g, const MmaLanes &) {
         pin(H);
-        pin(Q);
+        pin(QV);
         if constexpr (TOK == 4) {
+            uint32_t Q[8];
+            run_whole(QV, Q);
             const int sft = 4 * (g & 1);
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
@@ -327,7 +354,8 @@ template <int TOK> struct MmaW<T_Q4_K, TOK> {
                 A[m] = pack2((Q[o] >> sft) & NIB, (Q[o + 1] >> sft) & NIB);
             }
         } else {
-            uint32_t X[4], Y[4];
+            uint32_t Q[4], X[4], Y[4];
+            run_half(QV, Q);
             runs_to_pairs(Q, X, Y);
             const int sft = 4 * (g >> 1);
             A[0] = pack2((X[0] >> sft) & NIB, (X[1] >> sft) & NIB);
@@ -348,35 +376,29 @@ template <int TOK> struct MmaW<T_Q4_K, TOK> {
 };
 
 // Q5_K: as Q4_K (runs at 48 + 32 c) plus the 5th bits: qh byte e (32 B at 16), bit 4h + b for
-// sub-block 4h + b
+// sub-block 4h + b; the qh run is split and traded the same way
 template <int TOK> struct MmaW<T_Q5_K, TOK> {
     static constexpr int NSC = 2;
-    uint32_t H[4], Q[TOK == 4 ? 8 : 4], QH[TOK == 4 ? 8 : 4];
+    uint32_t H[4], QV[4], QHV[4];
     int h;
     __device__ static uint32_t step_off(int s) { return 176u * (uint32_t)(s >> 1); }
     __device__ static MmaLanes lanes(int r, int g, int h, uint32_t nb01, uint32_t) {
         const uint32_t row = r * nb01;
-        return {row, row + 48 + 32 * (2 * h + (g >> 1)) + (TOK == 4 ? 0 : 8 * (g & 1)), row + 16 + (TOK == 4 ? 0 : 8 * (g & 1))};
+        return {row, row + 48 + 32 * (2 * h + (g >> 1)) + 16 * (g & 1), row + 16 + 16 * (g & 1)};
     }
     __device__ inline void load(__amdgpu_buffer_rsrc_t rs, const MmaLanes &lo) {
         bl16(rs, lo.a, H);
-        if constexpr (TOK == 4) {
-            bl16(rs, lo.b, Q);
-            bl16(rs, lo.b + 16, Q + 4);
-            bl16(rs, lo.c, QH);
-            bl16(rs, lo.c + 16, QH + 4);
-        } else {
-            bl8(rs, lo.b, Q);
-            bl8(rs, lo.b + 16, Q + 2);
-            bl8(rs, lo.c, QH);
-            bl8(rs, lo.c + 16, QH + 2);
-        }
+        bl16(rs, lo.b, QV);
+        bl16(rs, lo.c, QHV);
     }
     __device__ inline void frags(long (&A)[4], int g, const MmaLanes &) {
         pin(H);
-        pin(Q);
-        pin(QH);
+        pin(QV);
+        pin(QHV);
         if constexpr (TOK == 4) {
+            uint32_t Q[8], QH[8];
+            run_whole(QV, Q);
+            run_whole(QHV, QH);
             const int sft = 4 * (g & 1), hb = 4 * h + g;
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
@@ -385,7 +407,9 @@ template <int TOK> struct MmaW<T_Q5_K, TOK> {
                              ((Q[o + 1] >> sft) & NIB) | (((QH[o + 1] >> hb) & 0x01010101u) << 4));
             }
         } else {
-            uint32_t X[4], Y[4];
+            uint32_t Q[4], QH[4], X[4], Y[4];
+            run_half(QV, Q);
+            run_half(QHV, QH);
             runs_to_pairs(Q, X, Y);
             const int sft = 4 * (g >> 1);
 #pragma unroll
@@ -406,7 +430,6 @@ template <int TOK> struct MmaW<T_Q5_K, TOK> {
         o[1] = dmin * (float)(g & 1 ? m1 : m0);
     }
 };
-
 
 // ------------------------------------------------------------------------------------------
 // Paired steps (Q4_0 / Q8_0, 4-byte-aligned contiguous rows): lane g loads blocks 2g and 2g + 1
