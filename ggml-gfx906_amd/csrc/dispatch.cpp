@@ -188,9 +188,10 @@ static int ring_pre_min() {
 // single matrices), the first column count from which it is used:
 //   Q4_0  K >= 8192: 4 (paired steps, mmvq_mma.hip); else N >= 8192: 5
 //   Q8_0  K >= 8192: 3 (paired steps from K >= 12288); else N >= 8192: 5
-//   Q4_K  K >= 8192 or N >= 8192: 5
-//   Q5_K  K < 8192: 5
-// everywhere else the VALU kernels are as fast or faster (0.65-0.99x where it is used).
+//   Q4_K  K >= 8192: 3; else N >= 8192: 4; else 5
+//   Q5_K  K < 8192: 5; K < 12288: 3; else 8
+// (the K-quant rows from profiles/r05_mma_sweep3.txt, after their loads per step were halved);
+// everywhere else the VALU kernels are as fast or faster (0.56-0.99x where it is used).
 // GGML_MI355X_MMA=N: from N columns on for every type it takes; 0: never.
 static int mma_min_cols(int type, int K, int N, int slices) {
     const char *e = getenv("GGML_MI355X_MMA");   // per call: tests switch it
@@ -203,8 +204,8 @@ static int mma_min_cols(int type, int K, int N, int slices) {
     switch (type) {
         case T_Q4_0: return K >= 8192 ? 4 : N >= 8192 ? 5 : NEVER;
         case T_Q8_0: return K >= 8192 ? 3 : N >= 8192 ? 5 : NEVER;
-        case T_Q4_K: return K >= 8192 || N >= 8192 ? 5 : NEVER;
-        case T_Q5_K: return K < 8192 ? 5 : NEVER;
+        case T_Q4_K: return K >= 8192 ? 3 : N >= 8192 ? 4 : 5;
+        case T_Q5_K: return K < 8192 ? 5 : K < 12288 ? 3 : 8;
         default: return NEVER;
     }
 }
