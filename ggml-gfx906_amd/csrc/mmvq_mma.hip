@@ -780,14 +780,44 @@ static int mma_env(const char *k, int dflt) {
     const char *e = getenv(k);
     return e ? atoi(e) : dflt;
 }
-// K parts (1 or 2: two from 32 steps) and 16-row tiles per workgroup (1 or 2; Q5_K 1: its two
-// weight sets per step do not fit twice); GGML_MI355X_MMA_KH / _RT override
-static int mma_kh(const MmArgs &a) { return a.K >= 32 * MMA_STEP_K && mma_env("GGML_MI355X_MMA_KH", 2) != 1 ? 2 : 1; }
-static int mma_rt() { return mma_env("GGML_MI355X_MMA_RT", 2) == 1 ? 1 : 2; }
 // steps of a K part (even: a K-quant super-block's two halves stay in one part)
 static int mma_part_steps(const MmArgs &a, int kh) {
     const int S = mma_steps(a);
     return kh == 1 ? S : ((S + 1) / 2 + 1) & ~1;
+}
+
+// Q4_0 / Q8_0 rows contiguous and 4-byte aligned (paired steps load aligned 36 / 68-byte windows)
+static bool mma_pair_aligned(int type, const MmArgs &a) {
+    if (type != T_Q4_0 && type != T_Q8_0) return false;
+    const int64_t row = (int64_t)(a.K / 32) * (type == T_Q4_0 ? 18 : 34);
+    return a.nb01 == row && row % 4 == 0 && a.nb02 % 4 == 0 && a.nb03 % 4 == 0 && (reinterpret_cast<uintptr_t>(a.w) & 3) == 0;
+}
+
+// the launch plan (profiles/r05_mma_sweep2.txt, r05_mma_k4096.txt):
+//   pr  paired steps: Q4_0 always, Q8_0 below K = 8192 and from 12288 (at 11008 the unpaired
+//       form with two tiles wins), where the rows allow it;
+//   kh  K parts: 2 when each part keeps >= 32 steps for pairs (every wave a pair; at K = 4096 two
+//       parts would idle half the waves), >= 16 unpaired (from K = 4096);
+//   rt  16-row tiles per workgroup: Q5_K and Q8_0 pairs 1 (registers); unsplit Q4_0 pairs 2 from
+//       N = 12288 (enough workgroups), else 1; otherwise 2.
+// GGML_MI355X_MMA_PAIR / _KH / _RT force (measurements; _KH=1 and _RT=1/2 as before)
+struct MmaPlan {
+    int kh, rt;
+    bool pr;
+};
+static MmaPlan mma_plan(int type, const MmArgs &a) {
+    const int S = mma_steps(a);
+    MmaPlan p;
+    const int pe = mma_env("GGML_MI355X_MMA_PAIR", -1);
+    const bool want = pe >= 0 ? pe == 1 : (type == T_Q4_0 || (type == T_Q8_0 && (a.K < 8192 || a.K >= 12288)));
+    p.pr = want && mma_pair_aligned(type, a);
+    p.kh = (p.pr ? S >= 64 : S >= 32) && mma_env("GGML_MI355X_MMA_KH", 2) != 1 ? 2 : 1;
+    const int re = mma_env("GGML_MI355X_MMA_RT", 0);
+    if (type == T_Q5_K || (type == T_Q8_0 && p.pr)) p.rt = 1;
+    else if (re == 1 || re == 2) p.rt = re;
+    else if (p.pr && p.kh == 1) p.rt = a.N >= 12288 ? 2 : 1;
+    else p.rt = 2;
+    return p;
 }
 
 // steps per wave: the smallest run that covers the part over the 16 waves (0: too long)
@@ -801,7 +831,7 @@ static int mma_nstep(int part) {
 constexpr int MMA_LDS_IMG = 160 * 1024 - 32 * 1024 - 128;
 
 bool mmvq_mma_supported(int type, const MmArgs &a) {
-    const int part = mma_part_steps(a, mma_kh(a));
+    const int part = mma_part_steps(a, mma_plan(type, a).kh);
     return (type == T_Q4_0 || type == T_Q8_0 || type == T_Q4_K || type == T_Q5_K) && a.M >= 1 && a.M <= 8 &&
            mma_nstep(part) > 0 && part * mma_tok_of(a) * 160 <= MMA_LDS_IMG;
 }
@@ -856,31 +886,22 @@ static hipError_t mma_run(const MmArgs &a, const uint8_t *img, int S, int part, 
     return hipErrorInvalidValue;
 }
 
-// paired steps: Q4_0 rows from K = 8192, Q8_0 from 12288 (profiles/r05_mma_sweep2.txt), rows
-// contiguous and 4-byte aligned; GGML_MI355X_MMA_PAIR=1 / 0 forces them on / off
-static bool mma_pair_ok(int type, const MmArgs &a) {
-    if (type != T_Q4_0 && type != T_Q8_0) return false;
-    const int pe = mma_env("GGML_MI355X_MMA_PAIR", -1);
-    if (pe == 0 || (pe < 0 && a.K < (type == T_Q4_0 ? 8192 : 12288))) return false;
-    const int64_t row = (int64_t)(a.K / 32) * (type == T_Q4_0 ? 18 : 34);
-    return a.nb01 == row && row % 4 == 0 && a.nb02 % 4 == 0 && a.nb03 % 4 == 0 && (reinterpret_cast<uintptr_t>(a.w) & 3) == 0;
-}
-
 template <int T, int TOK>
 static hipError_t mma_tok(const MmArgs &a, uint8_t *img, hipStream_t st) {
-    const int S = mma_steps(a), kh = mma_kh(a), part = mma_part_steps(a, kh);
+    const MmaPlan pl = mma_plan(T, a);
+    const int S = mma_steps(a), kh = pl.kh, part = mma_part_steps(a, kh);
     const dim3 pg(S, a.ne12 * a.ne13);
     if (a.x_aligned16) hipLaunchKernelGGL((mma_prequant<TOK, true>), pg, dim3(TOK * 16), 0, st, a, img, kh == 2);
     else hipLaunchKernelGGL((mma_prequant<TOK, false>), pg, dim3(TOK * 16), 0, st, a, img, kh == 2);
     hipError_t e;
     if constexpr (T == T_Q5_K) e = mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
-    else if constexpr (T == T_Q4_0 || T == T_Q8_0) {
-        if (mma_pair_ok(T, a)) {   // (Q8_0 pairs: one tile per workgroup, two would spill)
-            if constexpr (T == T_Q8_0) e = mma_run<T, TOK, 1, true>(a, img, S, part, kh, st);
-            else e = mma_rt() == 2 ? mma_run<T, TOK, 2, true>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, true>(a, img, S, part, kh, st);
-        }
-        else e = mma_rt() == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
-    } else e = mma_rt() == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
+    else if constexpr (T == T_Q8_0) {
+        if (pl.pr) e = mma_run<T, TOK, 1, true>(a, img, S, part, kh, st);   // (two tiles of pairs would spill)
+        else e = pl.rt == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
+    } else if constexpr (T == T_Q4_0) {
+        if (pl.pr) e = pl.rt == 2 ? mma_run<T, TOK, 2, true>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, true>(a, img, S, part, kh, st);
+        else e = pl.rt == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
+    } else e = pl.rt == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
     return e != hipSuccess ? e : hipGetLastError();
 }
 

@@ -49,6 +49,7 @@ for step in "$@"; do
         mmasweep2) run mmasweep2 1000 bash -c 'S1=" q4_0:4096:4096:3:1 q4_0:4096:4096:4:1 q4_0:4096:4096:5:1 q4_0:4096:4096:6:1 q4_0:4096:4096:8:1 q4_0:4096:11008:3:1 q4_0:4096:11008:4:1 q4_0:4096:11008:5:1 q4_0:4096:11008:6:1 q4_0:4096:11008:8:1 q4_0:11008:4096:3:1 q4_0:11008:4096:4:1 q4_0:11008:4096:5:1 q4_0:11008:4096:6:1 q4_0:11008:4096:8:1 q4_0:14336:4096:3:1 q4_0:14336:4096:4:1 q4_0:14336:4096:5:1 q4_0:14336:4096:6:1 q4_0:14336:4096:8:1 q4_0:4096:14336:3:1 q4_0:4096:14336:4:1 q4_0:4096:14336:5:1 q4_0:4096:14336:6:1 q4_0:4096:14336:8:1 q8_0:4096:4096:3:1 q8_0:4096:4096:4:1 q8_0:4096:4096:5:1 q8_0:4096:4096:6:1 q8_0:4096:4096:8:1 q8_0:4096:11008:3:1 q8_0:4096:11008:4:1 q8_0:4096:11008:5:1 q8_0:4096:11008:6:1 q8_0:4096:11008:8:1 q8_0:11008:4096:3:1 q8_0:11008:4096:4:1 q8_0:11008:4096:5:1 q8_0:11008:4096:6:1 q8_0:11008:4096:8:1 q8_0:14336:4096:3:1 q8_0:14336:4096:4:1 q8_0:14336:4096:5:1 q8_0:14336:4096:6:1 q8_0:14336:4096:8:1 q8_0:4096:14336:3:1 q8_0:4096:14336:4:1 q8_0:4096:14336:5:1 q8_0:4096:14336:6:1 q8_0:4096:14336:8:1"; S2=" q4_K:4096:4096:4:1 q4_K:4096:4096:5:1 q4_K:4096:4096:6:1 q4_K:4096:4096:8:1 q4_K:4096:11008:4:1 q4_K:4096:11008:5:1 q4_K:4096:11008:6:1 q4_K:4096:11008:8:1 q4_K:11008:4096:4:1 q4_K:11008:4096:5:1 q4_K:11008:4096:6:1 q4_K:11008:4096:8:1 q4_K:14336:4096:4:1 q4_K:14336:4096:5:1 q4_K:14336:4096:6:1 q4_K:14336:4096:8:1 q4_K:4096:14336:4:1 q4_K:4096:14336:5:1 q4_K:4096:14336:6:1 q4_K:4096:14336:8:1 q5_K:4096:4096:4:1 q5_K:4096:4096:5:1 q5_K:4096:4096:6:1 q5_K:4096:4096:8:1 q5_K:4096:11008:4:1 q5_K:4096:11008:5:1 q5_K:4096:11008:6:1 q5_K:4096:11008:8:1 q5_K:11008:4096:4:1 q5_K:11008:4096:5:1 q5_K:11008:4096:6:1 q5_K:11008:4096:8:1 q5_K:14336:4096:4:1 q5_K:14336:4096:5:1 q5_K:14336:4096:6:1 q5_K:14336:4096:8:1 q5_K:4096:14336:4:1 q5_K:4096:14336:5:1 q5_K:4096:14336:6:1 q5_K:4096:14336:8:1"; GGML_MI355X_MMA=1 GGML_MI355X_MMA_PAIR=1 python scripts/mmvq_bench.py $S1 && GGML_MI355X_MMA=1 python scripts/mmvq_bench.py $S1 $S2 && GGML_MI355X_MMA=0 python scripts/mmvq_bench.py $S1 $S2' ;;
         ringpar2) run ringpar2 600 env GGML_MI355X_RING_PRE=2 GGML_MI355X_MMA=0 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "k11008 or k14336 or k14368 or k12288 or k9216 or k8192 or k131072" ;;
         mmasweep3) run mmasweep3 900 bash -c 'S2=" q4_K:4096:4096:2:1 q4_K:4096:4096:3:1 q4_K:4096:4096:4:1 q4_K:4096:4096:5:1 q4_K:4096:4096:6:1 q4_K:4096:4096:8:1 q4_K:4096:11008:2:1 q4_K:4096:11008:3:1 q4_K:4096:11008:4:1 q4_K:4096:11008:5:1 q4_K:4096:11008:6:1 q4_K:4096:11008:8:1 q4_K:11008:4096:2:1 q4_K:11008:4096:3:1 q4_K:11008:4096:4:1 q4_K:11008:4096:5:1 q4_K:11008:4096:6:1 q4_K:11008:4096:8:1 q4_K:14336:4096:2:1 q4_K:14336:4096:3:1 q4_K:14336:4096:4:1 q4_K:14336:4096:5:1 q4_K:14336:4096:6:1 q4_K:14336:4096:8:1 q4_K:4096:14336:2:1 q4_K:4096:14336:3:1 q4_K:4096:14336:4:1 q4_K:4096:14336:5:1 q4_K:4096:14336:6:1 q4_K:4096:14336:8:1 q5_K:4096:4096:2:1 q5_K:4096:4096:3:1 q5_K:4096:4096:4:1 q5_K:4096:4096:5:1 q5_K:4096:4096:6:1 q5_K:4096:4096:8:1 q5_K:4096:11008:2:1 q5_K:4096:11008:3:1 q5_K:4096:11008:4:1 q5_K:4096:11008:5:1 q5_K:4096:11008:6:1 q5_K:4096:11008:8:1 q5_K:11008:4096:2:1 q5_K:11008:4096:3:1 q5_K:11008:4096:4:1 q5_K:11008:4096:5:1 q5_K:11008:4096:6:1 q5_K:11008:4096:8:1 q5_K:14336:4096:2:1 q5_K:14336:4096:3:1 q5_K:14336:4096:4:1 q5_K:14336:4096:5:1 q5_K:14336:4096:6:1 q5_K:14336:4096:8:1 q5_K:4096:14336:2:1 q5_K:4096:14336:3:1 q5_K:4096:14336:4:1 q5_K:4096:14336:5:1 q5_K:4096:14336:6:1 q5_K:4096:14336:8:1"; GGML_MI355X_MMA=1 python scripts/mmvq_bench.py $S2 && GGML_MI355X_MMA=0 python scripts/mmvq_bench.py $S2' ;;
+        mmak4) run mmak4 900 bash -c 'S="q4_0:4096:4096:4:1 q4_0:4096:4096:5:1 q4_0:4096:4096:8:1 q4_0:4096:11008:4:1 q4_0:4096:11008:5:1 q4_0:4096:11008:8:1 q4_0:4096:14336:5:1 q4_0:4096:14336:8:1 q8_0:4096:4096:5:1 q8_0:4096:4096:8:1 q8_0:4096:11008:5:1 q8_0:4096:11008:8:1"; GGML_MI355X_MMA=1 GGML_MI355X_MMA_PAIR=1 GGML_MI355X_MMA_KH=1 GGML_MI355X_MMA_RT=1 python scripts/mmvq_bench.py $S && GGML_MI355X_MMA=1 GGML_MI355X_MMA_PAIR=1 GGML_MI355X_MMA_KH=1 python scripts/mmvq_bench.py $S && GGML_MI355X_MMA=1 python scripts/mmvq_bench.py $S && GGML_MI355X_MMA=0 python scripts/mmvq_bench.py $S' ;;
         skb) run skb 600 bash -c 'S="q8_0:4096:11008:512 q4_K:4096:11008:512 q6_K:4096:11008:512 q4_0:4096:14336:512 q8_0:4096:4096:768 q8_0:4096:4096:512"; GGML_MI355X_MMQ8_SK=1 python scripts/mmq_bench.py $S && GGML_MI355X_MMQ8_SK=0 python scripts/mmq_bench.py $S' ;;
         gpt2ab) run gpt2ab 600 bash scripts/gpt2_ab.sh r4blk head ;;
         stamps) run stamps 300 bash -c 'python scripts/stamps_probe.py q4_K 4096 4096 1 && python scripts/stamps_probe.py q4_0 4096 4096 1' ;;
