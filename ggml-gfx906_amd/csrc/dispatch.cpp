@@ -186,8 +186,10 @@ static int ring_pre_min() {
 // block-diagonally into the MFMA's 16 columns, flat in the column count). From a sweep against
 // the per-column VALU kernels (profiles/r05_mma_sweep2.txt, r05_mma_k4096.txt: 5 shapes x 4 types x 3..8 columns,
 // single matrices), the first column count from which it is used:
-//   Q4_0  K >= 8192 or N >= 8192: 4; else 5 (paired steps, mmvq_mma.hip mma_plan)
-//   Q8_0  K >= 8192: 3; else 5 (paired below 8192 and from 12288)
+//   Q4_0  K >= 8192 or N >= 8192: 4 (paired steps, mmvq_mma.hip mma_plan)
+//   Q8_0  K >= 8192: 3; else N >= 8192: 5 (paired below K = 8192 and from 12288)
+// (K and N both below 8192, e.g. 4096 x 4096: within run-to-run noise of the VALU kernels at 5..6
+// columns and ~10 % slower at 8: VALU)
 //   Q4_K  K >= 8192: 3; else N >= 8192: 4; else 5
 //   Q5_K  K < 8192: 5; K < 12288: 3; else 8
 // (the K-quant rows from profiles/r05_mma_sweep3.txt, after their loads per step were halved);
@@ -202,8 +204,8 @@ static int mma_min_cols(int type, int K, int N, int slices) {
     constexpr int NEVER = 1 << 30;
     if (slices > 1) return NEVER;   // (8 batch slices: 2-4 % slower than the VALU kernels)
     switch (type) {
-        case T_Q4_0: return K >= 8192 || N >= 8192 ? 4 : 5;
-        case T_Q8_0: return K >= 8192 ? 3 : 5;
+        case T_Q4_0: return K >= 8192 || N >= 8192 ? 4 : NEVER;
+        case T_Q8_0: return K >= 8192 ? 3 : N >= 8192 ? 5 : NEVER;
         case T_Q4_K: return K >= 8192 ? 3 : N >= 8192 ? 4 : 5;
         case T_Q5_K: return K < 8192 ? 5 : K < 12288 ? 3 : 8;
         default: return NEVER;
