@@ -38,6 +38,7 @@ for step in "$@"; do
         mmab) run mmab 600 bash -c 'S="q4_0:14336:4096:1:1 q4_0:14336:4096:2:1 q4_0:14336:4096:3:1 q4_0:14336:4096:4:1 q4_0:14336:4096:5:1 q4_0:14336:4096:8:1 q8_0:14336:4096:2:1 q8_0:14336:4096:8:1 q4_K:14336:4096:2:1 q4_K:14336:4096:8:1 q5_K:14336:4096:8:1 q6_K:14336:4096:2:1 q6_K:14336:4096:8:1 q4_0:4096:4096:1:1 q4_0:4096:4096:2:1 q4_0:4096:4096:8:1 q4_K:4096:11008:8:1 q4_0:14336:4096:1:8 q4_0:14336:4096:2:8 q4_0:14336:4096:8:8 q4_K:14336:4096:8:8"; GGML_MI355X_MMA=1 python scripts/mmvq_bench.py $S && GGML_MI355X_MMA=0 python scripts/mmvq_bench.py $S && python scripts/mmvq_bench.py $S' ;;
         profmma) run profmma 300 env GGML_MI355X_MMA=1 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profmma -o run -- python scripts/mmvq_bench.py q4_0:14336:4096:1:1 q4_0:14336:4096:8:1 q4_K:4096:11008:8:1 q4_0:4096:4096:8:1 \
                  && for t in $(find $OUT/profmma -name '*kernel_trace.csv'); do rm -f $t; done ;;
+        profmma2) run profmma2 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profmma2 -o run -- python scripts/mmvq_bench.py q4_0:14336:4096:8:1 q4_0:4096:11008:8:1 q8_0:4096:11008:8:1 q4_K:14336:4096:8:1 q4_K:4096:14336:8:1 q5_K:4096:11008:8:1 && find $OUT/profmma2 -name '*kernel_trace.csv' -delete ;;
         q8x) run q8x 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_mmq8.py tests/test_gpu_parity.py -k "mmq8 or mm_1 or mmid or grouped or m512 or m2048" ;;
         q8xb) run q8xb 600 bash -c 'S="q8_0:4096:4096:512 q4_0:4096:4096:512 q4_K:4096:4096:512 q6_K:4096:11008:512 q8_0:4096:4096:2048 q4_K:4096:11008:512"; python scripts/mmq_bench.py $S' ;;
         rehearse) run rehearse 900 bash -c 'for n in 2 4; do BENCH_ONE_GPU_REHEARSAL=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $n --steps 3 --warmup 1 --cpu-seconds 1 || exit 1; done' ;;
