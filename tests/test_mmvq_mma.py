@@ -1,16 +1,19 @@
-"""GPU parity of the int8-MFMA mat-vec for 2..8 src1 columns (csrc/mmvq_mma.hip).
+"""GPU parity of the int8-MFMA mat-vec for 1..8 src1 columns (csrc/mmvq_mma.hip).
 
 The path quantizes every src1 column per 32-block exactly as the VALU mat-vec kernels do
 (d = amax/127, round-to-nearest-even: mmvq_impl.h xblock_store) and sums the integer block dots
 in int32 on v_mfma_i32_16x16x32_i8, so against the VALU path (GGML_MI355X_MMA=0, the same
 activation bytes) only the fp32 order of the per-block scale sums differs: NMSE <= 1e-10. Against
 the CPU oracle (ggml-cpu's vec_dot on its own src1 quantization) the reference's MUL_MAT bar
-5e-4 (tests/test-backend-ops.cpp:3106-3108) applies, as for every mat-vec case.
+5e-4 (tests/test-backend-ops.cpp:3106-3108) applies, as for every mat-vec case. (Its default
+forms are also pinned by golden records from the reference itself, tests/golden mm_166..mm_172,
+replayed by test_gpu_parity.py.)
 
-Covered: all five types; 2, 3, 5 and 8 columns; ragged rows (N % 16 != 0); Q4_0 / Q8_0 K that
-ends inside a 128-step (K % 128 = 32, 64, 96), K-quants at odd super-block counts; the reference's
-perf shapes (K = 14336, bs 2..8); broadcast batch slices (ne12 = 2 * ne02); every per-wave step
-run (K = 4096 .. 28672); one column. Q6_K stays on the VALU kernels.
+Covered: Q4_0, Q8_0, Q4_K, Q5_K (Q6_K stays on the VALU kernels); 1..8 columns (4- and 8-token
+forms); ragged rows (N % 16 != 0); Q4_0 / Q8_0 K that ends inside a 128-step (K % 128 = 32, 64,
+96), K-quants at odd super-block counts; the reference's perf shapes (K = 14336, bs 2..8);
+broadcast batch slices (ne12 = 2 * ne02); every per-wave step run (K = 4096 .. 28672) with one and
+two K parts; one or two row tiles per workgroup; paired and unpaired steps; bitwise repeatability.
 """
 import os
 
