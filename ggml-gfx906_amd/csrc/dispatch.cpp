@@ -203,6 +203,8 @@ static int mma_min_cols(int type, int K, int N, int slices) {
     }
     constexpr int NEVER = 1 << 30;
     if (slices > 1) return NEVER;   // (8 batch slices: 2-4 % slower than the VALU kernels)
+    if (K < 4096) return NEVER;     // (outside the swept range; below 32 steps most of a workgroup's
+                                    // 16 waves would idle, e.g. GPT-2's lm_head at K = 768)
     switch (type) {
         case T_Q4_0: return K >= 8192 || N >= 8192 ? 4 : NEVER;
         case T_Q8_0: return K >= 8192 ? 3 : N >= 8192 ? 5 : NEVER;
