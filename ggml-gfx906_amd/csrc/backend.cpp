@@ -39,6 +39,7 @@
 #include "../../include/ggml-mi355x.h"
 #include "dispatch.h"
 #include "ggml_abi.h"
+#include "settings.h"
 
 using namespace mi355x;
 
@@ -73,8 +74,7 @@ const GgmlBase &ggml_base() {
 }
 
 bool debug_on() {
-    static const bool on = getenv("GGML_MI355X_DEBUG") != nullptr;
-    return on;
+    return settings().debug;
 }
 
 void logf(const char *fmt, ...) {
@@ -543,7 +543,7 @@ int device_of(int idx);
 ggml_backend_dev_t dev_handle(int idx);
 
 int n_shards() {
-    static const int forced = getenv("GGML_MI355X_SPLIT_SHARDS") ? atoi(getenv("GGML_MI355X_SPLIT_SHARDS")) : 0;
+    const int forced = settings().split_shards;
     const int n = forced > 0 ? forced : n_devices();
     return std::max(1, std::min(n, SPLIT_MAX));
 }
@@ -736,7 +736,7 @@ ggml_backend_buffer_t host_buft_alloc(ggml_backend_buffer_type_t bt, size_t size
     const GgmlBase &gb = ggml_base();
     if (!gb.cpu_buffer_from_ptr || !gb.cpu_buffer_type) return nullptr;
     void *p = nullptr;
-    if (getenv("GGML_MI355X_NO_PINNED") == nullptr && hipHostMalloc(&p, size ? size : 1, hipHostMallocPortable) != hipSuccess) {
+    if (!settings().no_pinned && hipHostMalloc(&p, size ? size : 1, hipHostMallocPortable) != hipSuccess) {
         (void)hipGetLastError();
         p = nullptr;
     }
@@ -768,7 +768,7 @@ ggml_backend_buffer_type_t host_buft() {
 // ggml_backend_register_host_buffer / unregister (reference ggml-cuda.cu:3733-3740): pin
 // caller-owned memory for fast transfers
 extern "C" bool mi355x_register_host_buffer(void *buffer, size_t size) {
-    if (getenv("GGML_MI355X_NO_PINNED") != nullptr) return false;
+    if (settings().no_pinned) return false;
     const hipError_t e = hipHostRegister(buffer, size, hipHostRegisterPortable | hipHostRegisterReadOnly);
     if (e != hipSuccess) (void)hipGetLastError();
     return e == hipSuccess;
@@ -949,8 +949,7 @@ int be_split_mul_mat(BackendCtx *c, struct ggml_tensor *node) {
 // turns fusion off.
 // ------------------------------------------------------------------------------------------
 bool fusion_on() {
-    static const bool on = !(getenv("GGML_MI355X_FUSION") && atoi(getenv("GGML_MI355X_FUSION")) == 0);
-    return on;
+    return settings().fusion;
 }
 
 // the graph's use count of t (ggml_node_has_n_uses, ggml-impl.h:550-557), -1 when t is unknown
@@ -1445,8 +1444,7 @@ void match_attention(const struct ggml_cgraph *g, int n, int ism, FusePlan &plan
 // differs. GGML_MI355X_LAYER_FUSION=0 turns it off.
 // ------------------------------------------------------------------------------------------
 bool layer_fusion_on() {
-    static const bool on = !(getenv("GGML_MI355X_LAYER_FUSION") && atoi(getenv("GGML_MI355X_LAYER_FUSION")) == 0);
-    return on;
+    return settings().layer_fusion;
 }
 
 // head-major c_proj and slice-major MLP-projection copies of a fused layer's weights (Q4_0 /
@@ -1810,12 +1808,10 @@ enum ggml_status run_nodes(BackendCtx *c, struct ggml_cgraph *g, bool quiet, boo
 // place, and after GGML_MI355X_GRAPH_MAX_UPDATES (default 4) such calls in a row the backend
 // stops capturing (the graph changes every call, so capturing only adds host work).
 bool graphs_on() {
-    static const bool on = !(getenv("GGML_MI355X_GRAPHS") && atoi(getenv("GGML_MI355X_GRAPHS")) == 0);
-    return on;
+    return settings().graphs;
 }
 int graph_max_updates() {
-    static const int v = getenv("GGML_MI355X_GRAPH_MAX_UPDATES") ? atoi(getenv("GGML_MI355X_GRAPH_MAX_UPDATES")) : 4;
-    return v;
+    return settings().graph_max_updates;
 }
 
 void node_props(const struct ggml_tensor *t, NodeProps &p) {
@@ -2076,9 +2072,12 @@ bool dv_supports_op(ggml_backend_dev_t d, const struct ggml_tensor *op) {
             if (!is_hot_quant(op->src[0]->type)) break;   // f32 / f16 weights: graph_ops (below)
             return op->type == GGMLABI_TYPE_F32 && supports_mm_operands(op->src[0], op->src[1]) &&
                    op->src[1]->ne[2] % op->src[0]->ne[2] == 0 && op->src[1]->ne[3] % op->src[0]->ne[3] == 0;
-        case GGMLABI_OP_MUL_MAT_ID:
-            return op->type == GGMLABI_TYPE_F32 && supports_mm_operands(op->src[0], op->src[1]) &&
-                   op->src[2]->type == GGMLABI_TYPE_I32 && op->src[2]->ne[0] * op->src[2]->ne[1] <= 65535;
+        case GGMLABI_OP_MUL_MAT_ID: {
+            // exactly what mul_mat_id accepts (whole-K activations in LDS, <= 65535 pairs)
+            if (op->type != GGMLABI_TYPE_F32 || !supports_mm_operands(op->src[0], op->src[1])) return false;
+            const TensorView as = tv(op->src[0]), b = tv(op->src[1]), ids = tv(op->src[2]);
+            return check_mul_mat_id(as, b, ids, tv(op)) == GGML_MI355X_OK;
+        }
         // GET_ROWS of the hot quant types / f32 (dequantized rows, bit-exact), like get_rows_cuda
         case GGMLABI_OP_GET_ROWS:
             return check_get_rows(tv(op->src[0]), tv(op->src[1]), tv(op)) == GGML_MI355X_OK;
@@ -2220,8 +2219,7 @@ Registry &registry() {
         // cross-device tensor copies, stream / event hand-offs) runs with every device on GPU 0
         // (same-GPU copies instead of peer copies)
         const int n_real = (int)R->ctxs.size();
-        const char *vd = getenv("GGML_MI355X_VIRTUAL_DEVICES");
-        for (int i = n_real; n_real > 0 && vd && i < atoi(vd); ++i) {
+        for (int i = n_real; n_real > 0 && i < settings().virtual_devices; ++i) {
             const DeviceCtx &src = *R->ctxs[i % n_real];
             add(src.device, (src.desc + " (virtual)").c_str());
         }

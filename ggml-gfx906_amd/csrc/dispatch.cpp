@@ -15,9 +15,11 @@
 #include <mutex>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 
 #include "../../include/ggml-mi355x.h"
 #include "qcommon.h"
+#include "settings.h"
 
 namespace mi355x {
 
@@ -62,6 +64,10 @@ int64_t mmq8_tiles128(const MmArgs &a);
 hipError_t mmq8r_launch(int type, const MmArgs &a, const void *rp, int ne02, int n_mat, hipStream_t st, Scratch &scratch);
 bool mmq8_id_supported(int type, const MmArgs &a);
 hipError_t mmq8_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
+std::string mmvq_plan_text(const MmArgs &a, int nc, int rpw);
+std::string mmvq_ring_plan_text(int type, const MmArgs &a, int nc, int rpw, bool pre);
+std::string mmvq_mma_plan_text(int type, const MmArgs &a);
+std::string mmq8_plan_text(const MmArgs &a);
 
 // mat-mat kernel family: the int8 MFMA tile (csrc/mmq8.hip). It takes every K and every
 // 2-byte-aligned Q4_0 / Q8_0 / Q6_K layout (16-B aligned Q4_K / Q5_K) and is exact in the block
@@ -101,8 +107,7 @@ bool is_hot_quant(int t) { return type_blck(t) != 0; }
 // Q6_K keeps one row per wave: its two-row kernel needs 133 VGPRs, which leaves one 8-wave
 // workgroup per CU instead of two (Q6_K 4096x11008 x24: 169 vs 178 us, profiles/r03_q6k_rpw.txt).
 static int pick_rpw(int type, int64_t rows_total) {
-    static const int force = getenv("GGML_MI355X_RPW") ? atoi(getenv("GGML_MI355X_RPW")) : 0;
-    if (force > 0) return force;
+    if (settings().rpw > 0) return settings().rpw;
     if (type == T_Q6_K) return 1;
     return rows_total >= 16384 ? 2 : 1;
 }
@@ -117,8 +122,7 @@ static const size_t STAMP_SLOTS = 8 * 65536;
 
 unsigned long long *stamps_buffer();
 unsigned long long *stamps_buffer() {
-    static const bool on = getenv("GGML_MI355X_STAMPS") != nullptr;
-    if (!on) return nullptr;
+    if (!settings().stamps) return nullptr;
     if (!g_stamps && hipMalloc(&g_stamps, STAMP_SLOTS * sizeof(unsigned long long)) != hipSuccess) g_stamps = nullptr;
     return g_stamps;
 }
@@ -154,8 +158,7 @@ static MmArgs base_args(const TensorView &a, const TensorView &b, const TensorVi
     m.r3 = (int)(b.ne[3] / a.ne[3]);
     m.x_aligned16 = aligned16(b.data, m.nb11, m.nb12, m.nb13);
     m.stamps = stamps_buffer();
-    static const int diag = getenv("GGML_MI355X_DIAG") ? atoi(getenv("GGML_MI355X_DIAG")) : 0;
-    m.diag = diag;
+    m.diag = settings().diag;
     return m;
 }
 
@@ -164,10 +167,7 @@ static MmArgs base_args(const TensorView &a, const TensorView &b, const TensorVi
 // whole-K kernel would split them into passes of 1..3 columns) or the group's whole-K image would
 // not fit LDS. GGML_MI355X_RING: 0 = never (the whole-K kernel's column splits, measurements),
 // 2 = also single columns at K > 4096.
-static int ring_policy() {
-    static const int v = getenv("GGML_MI355X_RING") ? atoi(getenv("GGML_MI355X_RING")) : 1;
-    return v;
-}
+static int ring_policy() { return settings().ring; }
 
 static bool use_ring(int K, int ncols) {
     if (K <= 4096 || ring_policy() == 0) return mmvq_lds_bytes(K, 1) > LDS_LIMIT;
@@ -178,7 +178,7 @@ static bool use_ring(int K, int ncols) {
 // scratch (mmvq_prequant) instead of by every workgroup; GGML_MI355X_RING_PRE=0: in the
 // workgroups (A/B), =2: from 2 columns on (default 4)
 static int ring_pre_min() {
-    static const int v = getenv("GGML_MI355X_RING_PRE") ? atoi(getenv("GGML_MI355X_RING_PRE")) : 1;
+    const int v = settings().ring_pre;
     return v == 0 ? 1 << 30 : v == 2 ? 2 : 4;
 }
 
@@ -196,11 +196,8 @@ static int ring_pre_min() {
 // everywhere else the VALU kernels are as fast or faster (0.56-0.99x where it is used).
 // GGML_MI355X_MMA=N: from N columns on for every type it takes; 0: never.
 static int mma_min_cols(int type, int K, int N, int slices) {
-    const char *e = getenv("GGML_MI355X_MMA");   // per call: tests switch it
-    if (e != nullptr) {
-        const int v = atoi(e);
-        return v <= 0 ? 1 << 30 : v;
-    }
+    const int v = settings().mma;
+    if (v >= 0) return v == 0 ? 1 << 30 : v;
     constexpr int NEVER = 1 << 30;
     if (slices > 1) return NEVER;   // (8 batch slices: 2-4 % slower than the VALU kernels)
     if (K < 4096) return NEVER;     // (outside the swept range; below 32 steps most of a workgroup's
@@ -215,17 +212,32 @@ static int mma_min_cols(int type, int K, int N, int slices) {
 }
 
 // mat-vec over columns [c0, c0 + ncols) in groups of at most 8 (scratch: the caller holds its
-// mutex; nullptr = no pre-quantized images)
-static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st, Scratch *scratch = nullptr) {
+// mutex; nullptr = no pre-quantized images). plan != nullptr: launch nothing, append the launches
+// that would run (ggml_mi355x_mul_mat_plan; scratch then counts as available)
+static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st, Scratch *scratch = nullptr,
+                           std::string *plan = nullptr) {
     const int rpw = pick_rpw(type, (int64_t)m.N * m.ne12 * m.ne13);
-    if (scratch != nullptr && ncols >= mma_min_cols(type, m.K, m.N, m.ne12 * m.ne13) && ncols <= 8) {
+    const bool have_scratch = scratch != nullptr || plan != nullptr;
+    auto note = [&](const std::string &s) {
+        if (!plan->empty()) *plan += "; ";
+        *plan += s;
+    };
+    if (have_scratch && ncols >= mma_min_cols(type, m.K, m.N, m.ne12 * m.ne13) && ncols <= 8) {
         MmArgs g = m;
         g.x = m.x + (int64_t)c0 * m.nb11;
         g.dst = m.dst + (int64_t)c0 * m.nb1;
         g.M = ncols;
         // (nullptr inside a capture that would grow the scratch: the kernels below take it)
-        if (mmvq_mma_supported(type, g))
-            if (uint8_t *img = static_cast<uint8_t *>(scratch->get(mmvq_mma_img_bytes(type, g), st))) return mmvq_mma_launch(type, g, img, st);
+        if (mmvq_mma_supported(type, g)) {
+            if (plan) {
+                note(mmvq_mma_plan_text(type, g));
+                return hipSuccess;
+            }
+            if (uint8_t *img = static_cast<uint8_t *>(scratch->get(mmvq_mma_img_bytes(type, g), st))) {
+                const hipError_t e = mmvq_mma_launch(type, g, img, st);
+                if (e != hipErrorInvalidValue) return e;   // (a shape the launcher refuses: the kernels below)
+            }
+        }
     }
     while (ncols > 0) {
         MmArgs g = m;
@@ -238,15 +250,25 @@ static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st
             nc = take <= 1 ? 1 : take <= 2 ? 2 : take <= 4 ? 4 : 8;
             g.M = take;
             uint8_t *img = nullptr;
-            if (nc >= ring_pre_min() && scratch != nullptr)   // (nullptr inside a capture that would grow it)
-                img = static_cast<uint8_t *>(scratch->get(mmvq_ring_img_bytes(g, nc), st));
-            e = mmvq_ring_launch(type, g, nc, rpw, img, st);
+            if (plan) {
+                note(mmvq_ring_plan_text(type, g, nc, rpw, nc >= ring_pre_min()));
+                e = hipSuccess;
+            } else {
+                if (nc >= ring_pre_min() && scratch != nullptr)   // (nullptr inside a capture that would grow it)
+                    img = static_cast<uint8_t *>(scratch->get(mmvq_ring_img_bytes(g, nc), st));
+                e = mmvq_ring_launch(type, g, nc, rpw, img, st);
+            }
             nc = take;
         } else {
             nc = mmvq_bigk(m.K) ? 1 : std::min(ncols, 8);
             while (nc > 1 && (!mmvq_has_nc(nc) || mmvq_lds_bytes(m.K, nc) > LDS_LIMIT || m.K > mmvq_max_k_for_nc(nc))) --nc;
             g.M = nc;
-            e = mmvq_launch(type, g, nc, rpw, st);
+            if (plan) {
+                note(mmvq_plan_text(g, nc, rpw));
+                e = hipSuccess;
+            } else {
+                e = mmvq_launch(type, g, nc, rpw, st);
+            }
         }
         if (e != hipSuccess) return e;
         c0 += nc;
@@ -278,22 +300,16 @@ int repack(const TensorView &w, void *dst, size_t bytes, hipStream_t st) {
 // copy of src0 (made in scratch by one extra launch when the caller has none); below it, and for
 // layouts the repack does not take, the in-place int8 tile. GGML_MI355X_MMQ_REPACK_MIN overrides
 // (measurements: 0 = never repack per call).
-static int repack_min_tokens() {
-    const char *e = getenv("GGML_MI355X_MMQ_REPACK_MIN");   // per call: tests switch it
-    return e ? atoi(e) : 1 << 30;
-}
+static int repack_min_tokens() { return settings().mmq_repack_min; }
 
 int mul_mat(const TensorView &a, const TensorView &b, const TensorView &d, hipStream_t st, Scratch &scratch) {
     return mul_mat_rp(a, nullptr, b, d, st, scratch);
 }
 
-int mul_mat_rp(const TensorView &a, const void *rp, const TensorView &b, const TensorView &d, hipStream_t st,
-               Scratch &scratch) {
-    const int rc = check_mul_mat(a, b, d);
-    if (rc != GGML_MI355X_OK) return rc;
-    if (a.ne[1] == 0 || b.ne[1] == 0 || b.ne[2] == 0 || b.ne[3] == 0) return GGML_MI355X_OK;
-    MmArgs m = base_args(a, b, d);
-    std::lock_guard<std::mutex> hold(scratch.mu);   // until the scratch users are queued
+// the kernel choice of mul_mat_rp, shared with ggml_mi355x_mul_mat_plan (plan != nullptr:
+// describe, launch nothing)
+static hipError_t mul_mat_route(const TensorView &a, const void *rp, const MmArgs &m, hipStream_t st, Scratch *scratch,
+                                std::string *plan) {
     hipError_t e;
     const int n_mat = (int)(a.ne[2] * a.ne[3]);
     const int rmin = repack_min_tokens();
@@ -305,14 +321,31 @@ int mul_mat_rp(const TensorView &a, const void *rp, const TensorView &b, const T
     // 164) (profiles/r04_mmq_m_sweep.txt, r04_rp_shape_sweep.txt, r04_mmq8_tt_sweep2.txt). Both
     // are exact: only the fp32 order of the scale sums differs.
     // GGML_MI355X_MMQ_RP_ALL=1: always read the copy (measurements)
-    static const bool rp_all = getenv("GGML_MI355X_MMQ_RP_ALL") && atoi(getenv("GGML_MI355X_MMQ_RP_ALL")) == 1;
+    const bool rp_all = settings().mmq_rp_all;
     const bool wide = !rp_all && mmq8_supported(a.type, m) && mmq8_tile_tokens(m) == 128 &&
                       (m.M >= 1024 || mmq8_tiles128(m) < 256);
     const bool use_rp = m.M > 8 && ((rp != nullptr && !wide) || (rmin > 0 && m.M >= rmin)) &&
                         repack_size(a) != 0 && mmq8_images_fit(a.type, m);
-    if (use_rp) e = mmq8r_launch(a.type, m, rp, (int)a.ne[2], n_mat, st, scratch);
-    else if (m.M > 8 && mmq8_supported(a.type, m)) e = mmq8_launch(a.type, m, st, scratch);
-    else e = run_mmvq(a.type, m, 0, m.M, st, &scratch);
+    if (plan) {
+        if (use_rp) *plan = std::string(rp ? "mmq8r" : "repack+mmq8r") + " tile=128x64";
+        else if (m.M > 8 && mmq8_supported(a.type, m)) *plan = mmq8_plan_text(m);
+        else (void)run_mmvq(a.type, m, 0, m.M, st, nullptr, plan);
+        return hipSuccess;
+    }
+    if (use_rp) e = mmq8r_launch(a.type, m, rp, (int)a.ne[2], n_mat, st, *scratch);
+    else if (m.M > 8 && mmq8_supported(a.type, m)) e = mmq8_launch(a.type, m, st, *scratch);
+    else e = run_mmvq(a.type, m, 0, m.M, st, scratch);
+    return e;
+}
+
+int mul_mat_rp(const TensorView &a, const void *rp, const TensorView &b, const TensorView &d, hipStream_t st,
+               Scratch &scratch) {
+    const int rc = check_mul_mat(a, b, d);
+    if (rc != GGML_MI355X_OK) return rc;
+    if (a.ne[1] == 0 || b.ne[1] == 0 || b.ne[2] == 0 || b.ne[3] == 0) return GGML_MI355X_OK;
+    const MmArgs m = base_args(a, b, d);
+    std::lock_guard<std::mutex> hold(scratch.mu);   // until the scratch users are queued
+    const hipError_t e = mul_mat_route(a, rp, m, st, &scratch, nullptr);
     if (e == hipErrorOutOfMemory) return GGML_MI355X_ENOMEM;
     return e == hipSuccess ? GGML_MI355X_OK : GGML_MI355X_EHIP;
 }
@@ -328,8 +361,8 @@ int check_mul_mat_id(const TensorView &as, const TensorView &b, const TensorView
     return GGML_MI355X_OK;
 }
 
-// (slot, token) pairs from which the grouped MFMA path beats one mat-vec per pair
-static const int MMQ_ID_MIN_PAIRS = 64;
+// (slot, token) pairs from which the grouped MFMA path beats one mat-vec per pair:
+// settings().mmq_id_min, 64 by default
 
 int mul_mat_id(const TensorView &as, const TensorView &b, const TensorView &ids, const TensorView &d, hipStream_t st,
                Scratch &scratch) {
@@ -355,8 +388,7 @@ int mul_mat_id(const TensorView &as, const TensorView &b, const TensorView &ids,
     m.ne11_b = (int)b.ne[1];
     m.n_expert = (int)as.ne[2];
     m.x_aligned16 = aligned16(b.data, m.nb11, m.nb12, m.nb13);
-    static const int min_pairs = getenv("GGML_MI355X_MMQ_ID_MIN") ? atoi(getenv("GGML_MI355X_MMQ_ID_MIN")) : MMQ_ID_MIN_PAIRS;
-    const bool grouped = m.n_used * m.n_tok >= min_pairs;
+    const bool grouped = m.n_used * m.n_tok >= settings().mmq_id_min;
     const bool i8 = grouped && mmq8_id_supported(as.type, m);
     std::lock_guard<std::mutex> hold(scratch.mu);
     const hipError_t e = i8 ? mmq8_id_launch(as.type, m, st, scratch) : mmvq_id_launch(as.type, m, 1, st);
@@ -713,6 +745,45 @@ int ggml_mi355x_supports_mul_mat(const ggml_mi355x_tensor *src0, const ggml_mi35
     if (!src0 || !src1) return 0;
     return is_hot_quant(src0->type) && src1->type == T_F32 && src0->ne[0] % type_blck(src0->type) == 0 &&
            src0->ne[0] <= (1 << 24);
+}
+
+// the MUL_MAT_ID geometry mul_mat_id accepts (check_mul_mat_id on the dst ggml_mul_mat_id makes:
+// [N, n_used, T] f32), so that supports_op never claims what compute would refuse (whole-K
+// activations in LDS: K up to ~108K)
+int ggml_mi355x_supports_mul_mat_id(const ggml_mi355x_tensor *as, const ggml_mi355x_tensor *b, const ggml_mi355x_tensor *ids) {
+    if (!as || !b || !ids) return 0;
+    TensorView d{};
+    d.type = T_F32;
+    d.ne[0] = as->ne[1]; d.ne[1] = ids->ne[0]; d.ne[2] = ids->ne[1]; d.ne[3] = 1;
+    d.nb[0] = 4; d.nb[1] = 4 * d.ne[0]; d.nb[2] = d.nb[1] * d.ne[1]; d.nb[3] = d.nb[2] * d.ne[2];
+    return check_mul_mat_id(view_of(as), view_of(b), view_of(ids), d) == GGML_MI355X_OK;
+}
+
+int ggml_mi355x_reload_settings(void) {
+    reload_settings();
+    return GGML_MI355X_OK;
+}
+
+int ggml_mi355x_mul_mat_plan(const ggml_mi355x_tensor *src0, const ggml_mi355x_tensor *src1, int repacked, char *buf,
+                             size_t len) {
+    if (!src0 || !src1 || !buf || len == 0) return GGML_MI355X_EINVAL;
+    const TensorView a = view_of(src0), b = view_of(src1);
+    TensorView d{};
+    d.type = T_F32;
+    d.ne[0] = a.ne[1]; d.ne[1] = b.ne[1]; d.ne[2] = b.ne[2]; d.ne[3] = b.ne[3];
+    d.nb[0] = 4; d.nb[1] = 4 * d.ne[0]; d.nb[2] = d.nb[1] * d.ne[1]; d.nb[3] = d.nb[2] * d.ne[2];
+    const int rc = check_mul_mat(a, b, d);
+    if (rc != GGML_MI355X_OK) return rc;
+    std::string plan;
+    if (a.ne[1] == 0 || b.ne[1] == 0 || b.ne[2] == 0 || b.ne[3] == 0) {
+        plan = "none";
+    } else {
+        MmArgs m = base_args(a, b, d);
+        static const uint8_t rp_token = 0;   // any non-null copy: only its presence routes
+        (void)mul_mat_route(a, repacked ? &rp_token : nullptr, m, nullptr, nullptr, &plan);
+    }
+    snprintf(buf, len, "%s", plan.c_str());
+    return GGML_MI355X_OK;
 }
 
 int ggml_mi355x_device_count(void) {

@@ -28,6 +28,7 @@
 #include "../../include/ggml-mi355x-gpt2.h"
 #include "dispatch.h"
 #include "qcommon.h"
+#include "settings.h"
 
 namespace mi355x {
 hipError_t mmvq_fused_launch(int type, const MmArgs &a, int nc, int rpw, hipStream_t st);
@@ -160,7 +161,7 @@ int fused_matvec(const ggml_mi355x_gpt2_ctx *c, const Tensor &w, const float *x,
     a.n_head = c->m->hp.n_head;
     // diagnostics: GGML_MI355X_STAMPS=1 + GGML_MI355X_STAMP_MV=i stamps the i-th fused mat-vec of
     // a decode step (0 = first layer's c_attn); scripts/gpt2_stamps.py reads them
-    static const int stamp_mv = getenv("GGML_MI355X_STAMP_MV") ? atoi(getenv("GGML_MI355X_STAMP_MV")) : -1;
+    const int stamp_mv = settings().stamp_mv;
     static thread_local int mv_counter = 0;
     if (mv_counter++ == stamp_mv) a.stamps = stamps_buffer();
     if (epi & EPI_ARGMAX) mv_counter = 0;      // the last mat-vec of a step
@@ -176,7 +177,7 @@ int run_step(ggml_mi355x_gpt2_ctx *c, hipStream_t st) {
     const int E = hp.n_embd;
     int rc;
     // the two-launch layer takes the embedding in layer 0's prologue (32-block types)
-    const bool emb_fused = c->block && m->first && gpt2_block_embeds(m->wtype) && !getenv("GGML_MI355X_GPT2_EMBED_KERNEL");
+    const bool emb_fused = c->block && m->first && gpt2_block_embeds(m->wtype) && !settings().gpt2_embed_kernel;
     if (m->first && !emb_fused) {
         rc = hip_status(gpt2_embed_launch(m->wte.type, m->wte.data, row_bytes(m->wte.type, E), reinterpret_cast<const float *>(m->wpe.data),
                                           c->tokens, c->pos, c->x, c->n_seq, E, hp.n_vocab, hp.n_ctx, st));
@@ -484,8 +485,7 @@ int ggml_mi355x_gpt2_ctx_init(ggml_mi355x_gpt2_model *m, int32_t n_seq, ggml_mi3
     const size_t b_amax = m->last ? al(4 * S * ARGMAX_SLOTS) : 0;
     const size_t b_part = al(4 * S * hp.n_head * ATTN_SPLITS * ATTN_PART_STRIDE);
     // GGML_MI355X_GPT2_BLOCK=0 selects the five-launch layer (A/B and fallback)
-    const char *benv = getenv("GGML_MI355X_GPT2_BLOCK");
-    const bool block = gpt2_block_supported(hp.n_embd, hp.n_head) && !(benv && atoi(benv) == 0);
+    const bool block = gpt2_block_supported(hp.n_embd, hp.n_head) && settings().gpt2_block != 0;
     const size_t b_pa = block ? al(4 * S * E * hp.n_head) : 0, b_pm = block ? al(4 * S * E * gpt2_block_mlp_slices(hp.n_embd)) : 0;
     const size_t b_xb = block ? b_x : 0;
     const size_t total = 2 * b_tok + 2 * b_x + b_qkv + b_h + b_logits + 2 * b_cache + 2 * b_amax + b_part + 2 * b_xb + b_pa + b_pm;

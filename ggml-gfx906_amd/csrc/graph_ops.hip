@@ -10,6 +10,7 @@
 #include "../../include/ggml-mi355x.h"
 #include "dispatch.h"
 #include "qcommon.h"
+#include "settings.h"
 
 #include <algorithm>
 #include <cmath>
@@ -648,7 +649,7 @@ int run_attention(const AttnView &a, hipStream_t st) {
     const dim3 grid((unsigned)a.n_q, (unsigned)a.H);
     const size_t lds = (size_t)a.n_kv * sizeof(float);
     auto al16 = [](const void *p, int64_t s1, int64_t s2) { return (uintptr_t)p % 16 == 0 && s1 % 16 == 0 && s2 % 16 == 0; };
-    static const bool generic = getenv("GGML_MI355X_ATTN_GENERIC") != nullptr;   // A/B switch
+    const bool generic = settings().attn_generic;   // A/B switch
     if (!generic && a.D == 64 && !a.k_f16 && !a.v_f16 && a.k_d == 4 && a.v_d == 4 && al16(a.k, a.k_j, a.k_h) &&
         al16(a.v, a.v_j, a.v_h)) {
         hipLaunchKernelGGL(attn_kernel_d64, grid, dim3(256), lds, st, a);

@@ -41,6 +41,8 @@
 
 #include "dispatch.h"
 #include "qcommon.h"
+#include "settings.h"
+#include <string>
 
 namespace mi355x {
 
@@ -786,7 +788,13 @@ __device__ __forceinline__ void mmq8_job(const MmArgs &a, const uint8_t *__restr
         // 256-B wave row per register), drains, and one lane adds to the tile's counter (agent
         // scope); the workgroup whose add returns 1 came second: it loads the other partial with
         // sc1 loads, adds it (two operands: the same sum in either order) and stores dst; it
-        // also re-arms the counter (MI355X_MICROARCH.md inter-workgroup visibility, first form)
+        // also re-arms the counter (MI355X_MICROARCH.md inter-workgroup visibility, first form).
+        // Ordering: the compiler cannot move the partial loads above the counter add, because
+        // lds_barrier() is an asm statement with a "memory" clobber between them (and the loads
+        // sit behind the branch on the add's result); on the hardware, sc1 stores drained by
+        // vmcnt(0) before the add and sc1 loads after it are the guide's measured valid form. An
+        // acquire-release add would instead cost an L2 write-back and an L1 invalidate (~1.7 us)
+        // per tile.
         const int n_sb2 = (a.K + Q8_QK - 1) / Q8_QK;
         if (sb0 != 0 || sb1 != n_sb2) {
             const int tile = rt * n_tt + tt;
@@ -1460,42 +1468,60 @@ int64_t mmq8_tiles128(const MmArgs &a) {
 }
 int mmq8_tile_tokens(const MmArgs &a) { return mmq8_tiles128(a) > 128 ? 128 : 64; }
 
-hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch) {
+// the in-place tile's launch plan (pure: the launcher and the dispatch description share it)
+struct Mmq8Plan {
+    int tt_tok, tr_rows, n_rt, n_tt, ksplit, sb_per;
+    int64_t tiles;
+    bool atomic, use_sk;
+};
+static Mmq8Plan mmq8_plan(const MmArgs &a) {
+    const Settings &S = settings();
+    Mmq8Plan p{};
     const int slices = a.ne12 * a.ne13;
     const int n_sb = (a.K + Q8_QK - 1) / Q8_QK;
     // GGML_MI355X_MMQ8_TT / _TR override (measurements; 128 tokens always run 128 rows)
-    int tt_tok = mmq8_tile_tokens(a);
-    if (const char *e = getenv("GGML_MI355X_MMQ8_TT")) tt_tok = atoi(e) == 128 ? 128 : 64;
-    int tr_rows = 128;
-    if (const char *e = getenv("GGML_MI355X_MMQ8_TR")) tr_rows = (atoi(e) == 64 && tt_tok == 64) ? 64 : 128;
-    const int n_rt = (a.N + tr_rows - 1) / tr_rows;
-    const int n_tt = (a.M + tt_tok - 1) / tt_tok;
+    p.tt_tok = mmq8_tile_tokens(a);
+    if (S.mmq8_tt != 0) p.tt_tok = S.mmq8_tt == 128 ? 128 : 64;
+    p.tr_rows = (S.mmq8_tr == 64 && p.tt_tok == 64) ? 64 : 128;
+    p.n_rt = (a.N + p.tr_rows - 1) / p.tr_rows;
+    p.n_tt = (a.M + p.tt_tok - 1) / p.tt_tok;
     // split-K over workgroups while the tile grid leaves CUs idle (>= 2 super-blocks per split)
-    const char *env = getenv("GGML_MI355X_MMQ8_KSPLIT");   // per call: tests switch it
-    const int64_t tiles = (int64_t)n_rt * n_tt * slices;
+    p.tiles = (int64_t)p.n_rt * p.n_tt * slices;
     int ksplit = 1;
-    while (tiles * ksplit * 2 <= 256 && n_sb >= 4 * ksplit) ksplit *= 2;
-    if (env) ksplit = std::max(1, std::min(atoi(env), n_sb));
-    const int sb_per = (n_sb + ksplit - 1) / ksplit;
-    ksplit = (n_sb + sb_per - 1) / sb_per;
-    const size_t img_bytes = ((size_t)slices * n_tt * (tt_tok / Q8_TOK) * n_sb * ximg_bytes_rt(type) + 255) & ~(size_t)255;
+    while (p.tiles * ksplit * 2 <= 256 && n_sb >= 4 * ksplit) ksplit *= 2;
+    if (S.mmq8_ksplit > 0) ksplit = std::max(1, std::min(S.mmq8_ksplit, n_sb));
+    p.sb_per = (n_sb + ksplit - 1) / ksplit;
+    p.ksplit = (n_sb + p.sb_per - 1) / p.sb_per;
     // exactly two halves add into dst atomically (order-independent); more go through part[]
-    static const bool no_atomic = getenv("GGML_MI355X_MMQ8_ATOMIC") && atoi(getenv("GGML_MI355X_MMQ8_ATOMIC")) == 0;
-    const bool atomic = ksplit == 2 && !no_atomic;
-    size_t part_bytes = ksplit > 1 && !atomic ? (size_t)ksplit * slices * a.M * a.N * sizeof(float) : 0;
+    p.atomic = p.ksplit == 2 && !S.mmq8_no_atomic;
     // stream-K (one slice, no split-K, 128-row tiles) where whole rounds of one tile per CU would
     // leave the last round mostly idle: e.g. 4096 x 11008 x 512, 344 128-token tiles = 1.34
     // rounds. A tile's units are then split between at most two workgroups (units per
     // workgroup >= super-blocks per tile, since tiles > workgroups). GGML_MI355X_MMQ8_SK: 0 never
     // (A/B), 1 whenever the tiles outnumber the workgroups
-    const char *sk_env = getenv("GGML_MI355X_MMQ8_SK");   // per call: tests switch it
-    const int64_t rounds = (tiles + MMQ8_SK_WGS - 1) / MMQ8_SK_WGS;
-    bool use_sk = slices == 1 && ksplit == 1 && tr_rows == 128 && tiles > MMQ8_SK_WGS && tiles <= Scratch::COUNTERS &&
-                  (double)tiles / (double)(rounds * MMQ8_SK_WGS) < 0.85;
-    if (sk_env) use_sk = atoi(sk_env) == 1 && slices == 1 && ksplit == 1 && tr_rows == 128 && tiles > MMQ8_SK_WGS &&
-                         tiles <= Scratch::COUNTERS;
+    const int64_t rounds = (p.tiles + MMQ8_SK_WGS - 1) / MMQ8_SK_WGS;
+    const bool can_sk = slices == 1 && p.ksplit == 1 && p.tr_rows == 128 && p.tiles > MMQ8_SK_WGS && p.tiles <= Scratch::COUNTERS;
+    p.use_sk = S.mmq8_sk >= 0 ? (S.mmq8_sk == 1 && can_sk) : (can_sk && (double)p.tiles / (double)(rounds * MMQ8_SK_WGS) < 0.85);
+    return p;
+}
+
+std::string mmq8_plan_text(const MmArgs &a) {
+    const Mmq8Plan p = mmq8_plan(a);
+    return "mmq8 tile=" + std::to_string(p.tr_rows) + "x" + std::to_string(p.tt_tok) + " tiles=" + std::to_string(p.tiles) +
+           " ksplit=" + std::to_string(p.ksplit) + (p.atomic ? " atomic" : "") + (p.use_sk ? " stream-k" : "");
+}
+
+hipError_t mmq8_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch) {
+    const int slices = a.ne12 * a.ne13;
+    const int n_sb = (a.K + Q8_QK - 1) / Q8_QK;
+    const Mmq8Plan pl = mmq8_plan(a);
+    const int tt_tok = pl.tt_tok, tr_rows = pl.tr_rows, n_tt = pl.n_tt, ksplit = pl.ksplit, sb_per = pl.sb_per;
+    const int64_t tiles = pl.tiles;
+    const bool atomic = pl.atomic;
+    const size_t img_bytes = ((size_t)slices * n_tt * (tt_tok / Q8_TOK) * n_sb * ximg_bytes_rt(type) + 255) & ~(size_t)255;
+    size_t part_bytes = ksplit > 1 && !atomic ? (size_t)ksplit * slices * a.M * a.N * sizeof(float) : 0;
     StreamK sk{};
-    if (use_sk) {
+    if (pl.use_sk) {
         sk.cnt = scratch.counters(st);
         sk.n_tiles = (int)tiles;
         if (sk.cnt) part_bytes = (size_t)tiles * 2 * (tt_tok == 128 ? 8 : 4) * 32 * 64 * sizeof(float);
@@ -1692,11 +1718,10 @@ hipError_t mmq8r_launch(int type, const MmArgs &a, const void *rp, int ne02, int
     const int64_t tiles = (int64_t)n_rt128 * n_tt * slices;
     int ksplit = 1;
     while (tiles * ksplit * 2 <= 256 && n_sb >= 4 * ksplit) ksplit *= 2;
-    if (const char *env = getenv("GGML_MI355X_MMQ8_KSPLIT")) ksplit = std::max(1, std::min(atoi(env), n_sb));
+    if (settings().mmq8_ksplit > 0) ksplit = std::max(1, std::min(settings().mmq8_ksplit, n_sb));
     const int sb_per = (n_sb + ksplit - 1) / ksplit;
     ksplit = (n_sb + sb_per - 1) / sb_per;
-    static const bool no_atomic = getenv("GGML_MI355X_MMQ8_ATOMIC") && atoi(getenv("GGML_MI355X_MMQ8_ATOMIC")) == 0;
-    const bool atomic = ksplit == 2 && !no_atomic;
+    const bool atomic = ksplit == 2 && !settings().mmq8_no_atomic;
     const size_t img_bytes = al256((size_t)slices * n_tt * n_sb * ximg_bytes_rt(type));
     const size_t part_bytes = ksplit > 1 && !atomic ? al256((size_t)ksplit * slices * a.M * a.N * sizeof(float)) : 0;
     const size_t rp_bytes = rp ? 0 : L.bytes;

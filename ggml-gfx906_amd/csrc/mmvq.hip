@@ -1,6 +1,9 @@
 // mmvq.hip — launchers of the quantized mat-vec kernel (mmvq_impl.h) for plain MUL_MAT and
 // MUL_MAT_ID. The fused decode-layer instantiations live in mmvq_fused.hip.
 #include "mmvq_impl.h"
+#include "settings.h"
+
+#include <string>
 
 namespace mi355x {
 
@@ -15,7 +18,7 @@ size_t mmvq_lds_bytes(int K, int nc) {
 // lanes per weight row: the width (16 or 64) that leaves the fewest idle slot lanes for this K;
 // ties go to 64 (fewer K iterations per row)
 int mmvq_pick_lpr(int K) {
-    static const int force = getenv("GGML_MI355X_LPR") ? atoi(getenv("GGML_MI355X_LPR")) : 0;   // diagnostics
+    const int force = settings().lpr;   // diagnostics
     if (force == 16 || force == 64) return force;
     const int nslots = (K + 63) / 64;
     const int u16 = 16 * ((nslots + 15) / 16), u64 = 64 * ((nslots + 63) / 64);
@@ -32,28 +35,17 @@ static hipError_t launch_one(const MmArgs &a0, int grid_y, int grid_z, hipStream
     auto kern = mmvq_kernel<T, NC, LPR, RPW, IDS, RAG, XA, BIGK>;
     MmArgs a = a0;
     a.n_it = ((a.K + 63) / 64 + LPR - 1) / LPR;
-    // more than 64 KB of dynamic LDS needs the attribute, once per instantiation. The call fails
-    // inside a stream capture: the error is returned (the capture then fails and the caller runs
-    // the graph eagerly once), and the flag is set only when the call succeeded.
-    static bool attr_set = false;   // per-instantiation
-    if (lds > 64 * 1024 && !attr_set) {
-        // 160 KB of LDS per CU minus the kernel's static arrays
-        hipFuncAttributes fa{};
-        hipError_t e = hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kern));
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)(160 * 1024 - fa.sharedSizeBytes));
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            return e;
-        }
-        attr_set = true;
-    }
+    // more than 64 KB of dynamic LDS needs the attribute, once per instantiation and device. The
+    // call fails inside a stream capture: the error is returned (the capture then fails and the
+    // caller runs the graph eagerly once, which sets it).
+    static LdsAttr attr;   // per instantiation
+    if (lds > 64 * 1024)
+        if (const hipError_t e = lds_attr_once(reinterpret_cast<const void *>(kern), attr); e != hipSuccess) return e;
     const int rows_per_group = MMVQ_WAVES * (WAVE / LPR) * RPW;
     const int n_groups = (a.N + rows_per_group - 1) / rows_per_group;
     // enough workgroups to fill 256 CUs ~4 deep; beyond that each workgroup walks more groups
     const int64_t others = (int64_t)grid_y * grid_z;
-    static const int64_t target = getenv("GGML_MI355X_MMVQ_WGS") ? atoll(getenv("GGML_MI355X_MMVQ_WGS")) : MMVQ_TARGET_WGS;
+    const int64_t target = settings().mmvq_wgs > 0 ? settings().mmvq_wgs : MMVQ_TARGET_WGS;
     // floor, not ceil: a launch just above a multiple of the resident capacity (4 workgroups of
     // 8 waves per CU = 1024) leaves a tail of workgroups that start only when others finish
     const int want = (int)std::max<int64_t>(1, target / others);
@@ -106,6 +98,21 @@ static hipError_t launch_type(const MmArgs &a, int nc, int grid_y, int grid_z, i
     if (mmvq_pick_lpr(a.K) == 16 && !is_bigk(a)) return launch_nc<T, 16, 1>(a, nc, grid_y, grid_z, st);
     if (rpw <= 1) return launch_nc<T, 64, 1>(a, nc, grid_y, grid_z, st);
     return launch_nc<T, 64, 2>(a, nc, grid_y, grid_z, st);
+}
+
+// the launch launch_type / launch_one make (the dispatch description, ggml_mi355x_mul_mat_plan)
+std::string mmvq_plan_text(const MmArgs &a, int nc, int rpw) {
+    const bool bigk = is_bigk(a);
+    const int lpr = mmvq_pick_lpr(a.K) == 16 && !bigk ? 16 : 64;
+    const int r = lpr == 16 || rpw <= 1 ? 1 : 2;
+    const int rows_per_group = MMVQ_WAVES * (WAVE / lpr) * r;
+    const int n_groups = (a.N + rows_per_group - 1) / rows_per_group;
+    const int64_t others = (int64_t)a.ne12 * a.ne13 * (a.M / nc);
+    const int64_t target = settings().mmvq_wgs > 0 ? settings().mmvq_wgs : MMVQ_TARGET_WGS;
+    const int gx = (int)std::min<int64_t>(n_groups, std::max<int64_t>(1, target / others));
+    return "mmvq nc=" + std::to_string(nc) + " lpr=" + std::to_string(lpr) + " rpw=" + std::to_string(r) +
+           (bigk ? " bigk" : "") + " grid=" + std::to_string(gx) + "x" + std::to_string(a.ne12 * a.ne13) + "x" +
+           std::to_string(a.M / nc);
 }
 
 // column-group widths that have kernels (dispatch.cpp splits M into these); groups of 4 and 8

@@ -8,6 +8,7 @@
 // Instantiated for contiguous, 16-byte-aligned activations with K % 64 == 0 and K <= 8192
 // (the GPT-2 shapes: K = n_embd or 4 n_embd); the host checks this before launching.
 #include "mmvq_impl.h"
+#include "settings.h"
 
 namespace mi355x {
 
@@ -22,17 +23,9 @@ namespace {
 template <int T, int NC, int LPR, int RPW, bool ATTN = false>
 hipError_t fused_one(const MmArgs &a0, int grid_z, hipStream_t st, bool prepare_only = false) {
     auto kern = mmvq_kernel<T, NC, LPR, RPW, false, false, true, false, true, ATTN>;
-    static bool attr_set = false;   // per-instantiation
-    if (!attr_set) {
-        // 160 KB of LDS per CU minus the static arrays (layer-norm and argmax reductions)
-        hipFuncAttributes fa{};
-        hipError_t e = hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kern));
-        if (e != hipSuccess) return e;
-        e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(160 * 1024 - fa.sharedSizeBytes));
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    // 160 KB of LDS per CU minus the static arrays (layer-norm and argmax reductions), per device
+    static LdsAttr attr;   // per instantiation
+    if (const hipError_t e = lds_attr_once(reinterpret_cast<const void *>(kern), attr); e != hipSuccess) return e;
     if (prepare_only) return hipSuccess;
     MmArgs a = a0;
     a.n_it = ((a.K + 63) / 64 + LPR - 1) / LPR;
@@ -41,8 +34,7 @@ hipError_t fused_one(const MmArgs &a0, int grid_z, hipStream_t st, bool prepare_
     // resident-capacity grid (2 workgroups of 8 waves per CU at <= 128 VGPRs): tall matrices
     // (lm_head) walk their row groups with the prefetch pipeline instead of queueing rounds of
     // workgroups; EPI_ARGMAX needs one partial slot per workgroup (ARGMAX_SLOTS)
-    static const int target = getenv("GGML_MI355X_FUSED_WGS") ? atoi(getenv("GGML_MI355X_FUSED_WGS")) : 256;
-    static const int tall = getenv("GGML_MI355X_FUSED_TALL") ? atoi(getenv("GGML_MI355X_FUSED_TALL")) : 256;
+    const int target = settings().fused_wgs, tall = settings().fused_tall;
     const int want = std::max(1, std::min(ARGMAX_SLOTS, (n_groups > 4 * target ? tall : target) / grid_z));
     dim3 grid(std::min(n_groups, want), 1, grid_z);
     hipLaunchKernelGGL(kern, grid, dim3(MMVQ_THREADS), mmvq_lds_bytes(a.K, NC), st, a);
@@ -76,8 +68,7 @@ hipError_t fused_nc_attn(const MmArgs &a, int nc, int grid_z, hipStream_t st) {
 // spread over 4x the CUs: 4.9 -> 4.0-4.4 us per launch in the drop-in decode (scripts/
 // prof_plugin_shapes.sh), ~2% on the whole token
 static int fused_lpr(const MmArgs &a) {
-    static const int maxn = getenv("GGML_MI355X_FUSED_LPR64_MAXN") ? atoi(getenv("GGML_MI355X_FUSED_LPR64_MAXN")) : 1024;
-    return a.N <= maxn ? 64 : mmvq_pick_lpr(a.K);
+    return a.N <= settings().fused_lpr64_maxn ? 64 : mmvq_pick_lpr(a.K);
 }
 
 template <int T>

@@ -30,6 +30,14 @@
 
 namespace mi355x {
 
+// measurement builds only (scripts/mmvq_exp.sh): 1 = no activation loads, 2 = no quantization
+// into LDS, 4 = no weight loads, 8 = no barrier before the dots, 16 = an issue-order s_barrier
+// between every wave's activation loads and the weight loads, 32 = weights issued before the
+// activations (not built: the activation loads are the first instructions either way)
+#ifndef MMVQ_EXP
+#define MMVQ_EXP 0
+#endif
+
 constexpr int MMVQ_WAVES = 8;
 constexpr int MMVQ_THREADS = MMVQ_WAVES * WAVE;
 
@@ -621,7 +629,10 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
         const int r0 = g * ROWS_PER_GROUP + wrow;
         const int s = min(sl + it * LPR, nslots - 1);
 #pragma unroll
-        for (int r = 0; r < RPW; ++r) f[r].template load<RAG>(wmat + (int64_t)min(r0 + r, a.N - 1) * a.nb01, s, nblk);
+        for (int r = 0; r < RPW; ++r) {
+            if constexpr (MMVQ_EXP & 4) f[r].zero();
+            else f[r].template load<RAG>(wmat + (int64_t)min(r0 + r, a.N - 1) * a.nb01, s, nblk);
+        }
     };
 
     // fused epilogue operands of this lane's output (bias[row], and dst[row] for the residual
@@ -677,7 +688,10 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
 #pragma unroll
         for (int m = 0; m < NC; ++m) {
 #pragma unroll
-            for (int r = 0; r < PRE; ++r) xblock_load<XA>(a, xcol0 + (int64_t)m * a.nb11, kb0 + r * XR_STRIDE, xa[m][r], xb[m][r]);
+            for (int r = 0; r < PRE; ++r) {
+                if constexpr (MMVQ_EXP & 1) xa[m][r] = xb[m][r] = make_float4(1.f, 2.f, 3.f, (float)threadIdx.x);
+                else xblock_load<XA>(a, xcol0 + (int64_t)m * a.nb11, kb0 + r * XR_STRIDE, xa[m][r], xb[m][r]);
+            }
         }
     }
 
@@ -707,6 +721,7 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
 
     Frag<T> fa[RPW], fb[RPW];
     int g = blockIdx.x, it = 0;                   // the unit being computed (grid.x <= n_groups)
+    if constexpr (MMVQ_EXP & 16) asm volatile("s_barrier" ::: "memory");
     load_unit(fa, g, it);
     [[maybe_unused]] EpiOps ea{}, eb{};
     if constexpr (FUSE) ea = load_epi(g);
@@ -742,7 +757,7 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
 #pragma unroll
     for (int r = 0; r < PRE; ++r) {
         const int kb = kb0 + r * XR_STRIDE;
-        if (kb < nxblk) {
+        if (kb < nxblk && !(MMVQ_EXP & 2)) {
 #pragma unroll
             for (int m = 0; m < NC; ++m)
                 xblock_store<T>(Kpad, kb, xa[m][r], xb[m][r], sm.xq + (size_t)m * Kpad, sm.xd + m * nxblk,
@@ -764,7 +779,7 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
 #ifdef MMVQ_FENCE_BARRIER   // A/B measurement builds only (scripts/ab_singles.sh)
     __syncthreads();
 #else
-    lds_barrier();
+    if constexpr (!(MMVQ_EXP & 8)) lds_barrier();
 #endif
     if (stamp) a.stamps[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
 
@@ -851,6 +866,7 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
     if (ng >= n_groups) {
         // single unit per workgroup (e.g. a 4096-row matrix at K <= 4096): no prefetch at all
         compute_unit(fa, g, it, ea);
+        if (wstamp) wst[3] = __builtin_amdgcn_s_memrealtime();   // diagnostics: dots stored
     } else {
         // prefetches are unconditional (clamped to the current unit once the walk ends: a
         // repeat of addresses already in flight, served on-chip) so the load stream never sits

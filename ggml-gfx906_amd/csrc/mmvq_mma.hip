@@ -43,6 +43,9 @@
 #endif
 
 #include "mmvq_impl.h"
+#include "settings.h"
+
+#include <string>
 
 namespace mi355x {
 
@@ -611,9 +614,14 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
         }
     };
     mma_f2 acc[RT][2] = {};   // tile t, rows 4g + {0, 1}, {2, 3}
-    auto compute = [&](auto &w, Xf &x) __attribute__((always_inline)) {
+    // sl: the local step. Its blocks past K (the last step of a Q4_0 / Q8_0 row whose K is not a
+    // multiple of 128) were loaded from whatever follows the row (the next row, a view's padding):
+    // their codes meet zero activation codes, and their weight scales are zeroed here, so a
+    // non-finite f16 there cannot turn 0 * d into NaN
+    auto compute = [&](auto &w, Xf &x, int sl) __attribute__((always_inline)) {
         pin(x.c);
         pin(x.s);
+        const bool blk_live = T == T_Q4_0 || T == T_Q8_0 ? ((s0 + sl) * MMA_STEP_K + 32 * g < a.K) : true;
 #pragma unroll
         for (int t = 0; t < RT; ++t) {
             long A[4];
@@ -621,6 +629,8 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
             // publish this lane's block-g scales, [block g][k][row c]
             float o[NSC];
             w[t].sc(o, g);
+#pragma unroll
+            for (int k = 0; k < NSC; ++k) o[k] = blk_live ? o[k] : 0.f;
             float *ws = wsc[wave][t];
 #pragma unroll
             for (int k = 0; k < NSC; ++k) ws[(g * NSC + k) * 16 + c] = o[k];
@@ -696,7 +706,7 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
                 load_x(X[(k + D - 1) % D], sl);
             }
             __builtin_amdgcn_sched_barrier(0);
-            compute(F[k], X[k]);
+            compute(F[k], X[k], step_of(i));
         };
         mma_run_steps<D>(step, std::make_integer_sequence<int, NSTEP>{});
     } else {
@@ -728,8 +738,8 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
             MmaHalf<T, TOK> H0[RT], H1[RT];
 #pragma unroll
             for (int t = 0; t < RT; ++t) F[k][t].split(H0[t], H1[t]);
-            compute(H0, X[k][0]);
-            compute(H1, X[k][1]);
+            compute(H0, X[k][0], step_of(2 * j));
+            compute(H1, X[k][1], step_of(2 * j + 1));
         };
         mma_run_steps<DP>(pstep, std::make_integer_sequence<int, NSTEP / 2>{});
     }
@@ -776,10 +786,6 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
 // ------------------------------------------------------------------------------------------
 static int mma_steps(const MmArgs &a) { return (a.K + MMA_STEP_K - 1) / MMA_STEP_K; }
 static int mma_tok_of(const MmArgs &a) { return a.M <= 4 ? 4 : 8; }
-static int mma_env(const char *k, int dflt) {
-    const char *e = getenv(k);
-    return e ? atoi(e) : dflt;
-}
 // steps of a K part (even: a K-quant super-block's two halves stay in one part)
 static int mma_part_steps(const MmArgs &a, int kh) {
     const int S = mma_steps(a);
@@ -808,11 +814,11 @@ struct MmaPlan {
 static MmaPlan mma_plan(int type, const MmArgs &a) {
     const int S = mma_steps(a);
     MmaPlan p;
-    const int pe = mma_env("GGML_MI355X_MMA_PAIR", -1);
+    const int pe = settings().mma_pair;
     const bool want = pe >= 0 ? pe == 1 : (type == T_Q4_0 || (type == T_Q8_0 && (a.K < 8192 || a.K >= 12288)));
     p.pr = want && mma_pair_aligned(type, a);
-    p.kh = (p.pr ? S >= 64 : S >= 32) && mma_env("GGML_MI355X_MMA_KH", 2) != 1 ? 2 : 1;
-    const int re = mma_env("GGML_MI355X_MMA_RT", 0);
+    p.kh = (p.pr ? S >= 64 : S >= 32) && settings().mma_kh != 1 ? 2 : 1;
+    const int re = settings().mma_rt;
     if (type == T_Q5_K || (type == T_Q8_0 && p.pr)) p.rt = 1;
     else if (re == 1 || re == 2) p.rt = re;
     else if (p.pr && p.kh == 1) p.rt = a.N >= 12288 ? 2 : 1;
@@ -830,10 +836,32 @@ static int mma_nstep(int part) {
 // the column image of a part lives in LDS next to the kernel's static arrays (<= 32 KB)
 constexpr int MMA_LDS_IMG = 160 * 1024 - 32 * 1024 - 128;
 
+// the run mma_run launches for a part: pairs round it up to an even length (0: none fits)
+static int mma_run_len(int part, bool pr) {
+    const int ns = mma_nstep(part);
+    return pr && ns > 0 ? (ns + 1) & ~1 : ns;
+}
+
+// exactly the launcher's conditions: a run for the part, the part's image in LDS, and the run's
+// steps within the image mma_main accepts (paired runs of part 97..102 at 8 tokens, or 193..204
+// at 4, round past it: e.g. Q4_0 K = 25600 at 5..8 columns, Q4_K K = 49408 at 3)
 bool mmvq_mma_supported(int type, const MmArgs &a) {
-    const int part = mma_part_steps(a, mma_plan(type, a).kh);
-    return (type == T_Q4_0 || type == T_Q8_0 || type == T_Q4_K || type == T_Q5_K) && a.M >= 1 && a.M <= 8 &&
-           mma_nstep(part) > 0 && part * mma_tok_of(a) * 160 <= MMA_LDS_IMG;
+    if (!(type == T_Q4_0 || type == T_Q8_0 || type == T_Q4_K || type == T_Q5_K) || a.M < 1 || a.M > 8) return false;
+    const MmaPlan pl = mma_plan(type, a);
+    const int part = mma_part_steps(a, pl.kh);
+    const int ns = mma_run_len(part, pl.pr);
+    const int sb = mma_tok_of(a) * 160;   // mma_step_bytes<TOK>()
+    return ns > 0 && part * sb <= MMA_LDS_IMG && MMA_KS * ns * sb <= MMA_LDS_IMG + 16 * sb;
+}
+
+// the launch mma_tok makes (the dispatch description, ggml_mi355x_mul_mat_plan)
+std::string mmvq_mma_plan_text(int type, const MmArgs &a) {
+    const MmaPlan pl = mma_plan(type, a);
+    const int part = mma_part_steps(a, pl.kh);
+    int rt = pl.rt;
+    if (type == T_Q5_K || (type == T_Q8_0 && pl.pr)) rt = 1;
+    return "mma tok=" + std::to_string(mma_tok_of(a)) + " kh=" + std::to_string(pl.kh) + " rt=" + std::to_string(rt) +
+           (pl.pr ? " paired" : "") + " run=" + std::to_string(mma_run_len(part, pl.pr)) + " cols=" + std::to_string(a.M);
 }
 
 size_t mmvq_mma_img_bytes(int, const MmArgs &a) {
@@ -847,19 +875,9 @@ static hipError_t mma_main(const MmArgs &a, const uint8_t *img, int S, int part,
     } else {
         auto kern = mmvq_mma_kernel<T, TOK, RT, NS, PR>;
         const size_t lds = (size_t)part * mma_step_bytes<TOK>() + 128;
-        static bool attr_set = false;   // per instantiation; > 64 KB of dynamic LDS needs the attribute
-        if (lds > 64 * 1024 && !attr_set) {
-            hipFuncAttributes fa{};
-            hipError_t e = hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kern));
-            if (e == hipSuccess)
-                e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)(160 * 1024 - fa.sharedSizeBytes));
-            if (e != hipSuccess) {
-                (void)hipGetLastError();
-                return e;
-            }
-            attr_set = true;
-        }
+        static LdsAttr attr;   // per instantiation and device; > 64 KB of dynamic LDS needs the attribute
+        if (lds > 64 * 1024)
+            if (const hipError_t e = lds_attr_once(reinterpret_cast<const void *>(kern), attr); e != hipSuccess) return e;
         hipLaunchKernelGGL(kern, dim3((a.N + 16 * RT - 1) / (16 * RT), a.ne12 * a.ne13, kh), dim3(MMA_KS * WAVE), lds, st, a, img, S, part);
         return hipSuccess;
     }
@@ -867,9 +885,7 @@ static hipError_t mma_main(const MmArgs &a, const uint8_t *img, int S, int part,
 
 template <int T, int TOK, int RT, bool PR>
 static hipError_t mma_run(const MmArgs &a, const uint8_t *img, int S, int part, int kh, hipStream_t st) {
-    int ns = mma_nstep(part);
-    if constexpr (PR) ns = (ns + 1) & ~1;   // (pairs: even runs)
-    switch (ns) {
+    switch (mma_run_len(part, PR)) {   // (pairs: even runs)
         case 1: if constexpr (!PR) return mma_main<T, TOK, RT, 1, PR>(a, img, S, part, kh, st); else break;
         case 2: return mma_main<T, TOK, RT, 2, PR>(a, img, S, part, kh, st);
         case 3: if constexpr (!PR) return mma_main<T, TOK, RT, 3, PR>(a, img, S, part, kh, st); else break;

@@ -21,6 +21,9 @@
 #include <type_traits>
 
 #include "mmvq_impl.h"
+#include "settings.h"
+
+#include <string>
 
 namespace mi355x {
 
@@ -391,24 +394,15 @@ static hipError_t ring_one(const MmArgs &a0, uint8_t *img, hipStream_t st) {
     // without spills (two rows of Q8_0 / Q5_K, or of Q4_K at 8 columns, do not: 2 there), unless
     // GGML_MI355X_RING_DEPTH=2
     constexpr int D = pre_depth<T, NC, RPW>();
-    static const int depth_env = getenv("GGML_MI355X_RING_DEPTH") ? atoi(getenv("GGML_MI355X_RING_DEPTH")) : 3;
-    const bool d3 = D == 3 && depth_env != 2;
+    const bool d3 = D == 3 && settings().ring_depth != 2;
     const void *kern;
     if constexpr (PRE)
         kern = d3 ? reinterpret_cast<const void *>(mmvq_ring_pre_kernel<T, NC, RPW, RAG, WAVES, D>)
                   : reinterpret_cast<const void *>(mmvq_ring_pre_kernel<T, NC, RPW, RAG, WAVES, 2>);
     else kern = reinterpret_cast<const void *>(mmvq_ring_kernel<T, NC, RPW, RAG, XA, WAVES>);
-    static bool attr_set[2] = {false, false};   // per instantiation and depth; set once the call succeeded
-    if (lds > 64 * 1024 && !attr_set[d3]) {
-        hipFuncAttributes fa{};
-        hipError_t e = hipFuncGetAttributes(&fa, kern);
-        if (e == hipSuccess) e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(160 * 1024 - fa.sharedSizeBytes));
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            return e;
-        }
-        attr_set[d3] = true;
-    }
+    static LdsAttr attr[2];   // per instantiation, depth and device; set once the call succeeded
+    if (lds > 64 * 1024)
+        if (const hipError_t e = lds_attr_once(kern, attr[d3]); e != hipSuccess) return e;
     MmArgs a = a0;
     const int nslots = ((a.K + 63) & ~63) / 64;
     a.n_it = (nslots + 63) / 64;
@@ -418,7 +412,7 @@ static hipError_t ring_one(const MmArgs &a0, uint8_t *img, hipStream_t st) {
     // one round of resident workgroups (LDS-bound: 160 KiB / ring; at most 32 waves per CU);
     // more workgroups would re-quantize (or re-copy) the same chunks for fewer rows each
     const int per_cu = std::max(1, std::min(32 / (THREADS / WAVE), (int)(160 * 1024 / (lds + 1024))));
-    static const int64_t target_env = getenv("GGML_MI355X_RING_WGS") ? atoll(getenv("GGML_MI355X_RING_WGS")) : 0;
+    const int64_t target_env = settings().ring_wgs;
     const int64_t target = target_env > 0 ? target_env : 256 * per_cu;
     const int want = (int)std::max<int64_t>(1, target / ((int64_t)grid_y * grid_z));
     const dim3 grid(std::min(n_groups, want), grid_y, grid_z);
@@ -474,6 +468,15 @@ static hipError_t ring_type(const MmArgs &a, int nc, int rpw, uint8_t *img, hipS
         case 4: return ring_flags<T, 4, 2, false>(a, nullptr, st);
         default: return hipErrorInvalidValue;
     }
+}
+
+// the kernel ring_type picks (the dispatch description, ggml_mi355x_mul_mat_plan)
+std::string mmvq_ring_plan_text(int type, const MmArgs &a, int nc, int rpw, bool pre) {
+    int r;
+    if (pre) r = (type != T_Q5_K && type != T_Q6_K && rpw > 1) ? 2 : 1;
+    else r = (nc == 8 || rpw <= 1 || type == T_Q6_K) ? 1 : 2;
+    return std::string(pre ? "ring-pre" : "ring") + " nc=" + std::to_string(nc) + " rpw=" + std::to_string(r) +
+           " cols=" + std::to_string(a.M);
 }
 
 // bytes of the pre-quantized image of one nc-column group (prequant path)

@@ -8,6 +8,7 @@ missing or no gfx950 device is present the calls raise.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 import subprocess
@@ -74,6 +75,9 @@ def lib():
         L.ggml_mi355x_repack_size.argtypes = [P, C.POINTER(C.c_size_t)]
         L.ggml_mi355x_repack.argtypes = [P, C.c_void_p, C.c_size_t, C.c_void_p]
         L.ggml_mi355x_mul_mat_repacked.argtypes = [P, C.c_void_p, P, P, C.c_void_p]
+        L.ggml_mi355x_supports_mul_mat_id.argtypes = [P, P, P]
+        L.ggml_mi355x_mul_mat_plan.argtypes = [P, P, C.c_int, C.c_char_p, C.c_size_t]
+        L.ggml_mi355x_reload_settings.restype = C.c_int
         L.ggml_mi355x_device_error.restype = C.c_int
         L.ggml_mi355x_strerror.restype = C.c_char_p
         L.ggml_mi355x_strerror.argtypes = [C.c_int]
@@ -176,6 +180,43 @@ def mul_mat_id(a: MmTensor, b: MmTensor, ids: MmTensor, d: MmTensor, stream=None
 
 def dequantize(t: int, src_ptr: int, dst_ptr: int, n: int, stream=None) -> None:
     _check(lib().ggml_mi355x_dequantize(t, src_ptr, dst_ptr, n, _stream_ptr(stream)), "dequantize")
+
+
+def reload_settings() -> None:
+    """re-read the GGML_MI355X_* knobs (the library reads them once otherwise)"""
+    lib().ggml_mi355x_reload_settings()
+
+
+@contextlib.contextmanager
+def knobs(**env):
+    """set GGML_MI355X_* knobs (None = unset) for the calls inside the block, then restore them"""
+    saved = {k: os.environ.get(k) for k in env}
+    try:
+        for k, v in env.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = str(v)
+        reload_settings()
+        yield
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        reload_settings()
+
+
+def mul_mat_plan(a: MmTensor, b: MmTensor, repacked: bool = False) -> str:
+    """the kernel launches mul_mat would make for these operands (no launch, no GPU needed)"""
+    buf = C.create_string_buffer(512)
+    _check(lib().ggml_mi355x_mul_mat_plan(C.byref(a), C.byref(b), 1 if repacked else 0, buf, len(buf)), "mul_mat_plan")
+    return buf.value.decode()
+
+
+def supports_mul_mat_id(a: MmTensor, b: MmTensor, ids: MmTensor) -> bool:
+    return bool(lib().ggml_mi355x_supports_mul_mat_id(C.byref(a), C.byref(b), C.byref(ids)))
 
 
 def device_count() -> int:

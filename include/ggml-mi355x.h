@@ -143,6 +143,24 @@ GGML_MI355X_API int ggml_mi355x_mul_mat_repacked(const ggml_mi355x_tensor *src0,
  * (replaces the MUL_MAT arm of ggml_backend_cuda_device_supports_op, ggml-cuda.cu:3270-3330). */
 GGML_MI355X_API int ggml_mi355x_supports_mul_mat(const ggml_mi355x_tensor *src0, const ggml_mi355x_tensor *src1);
 
+/* Same predicate the backend's supports_op uses for MUL_MAT_ID (the MUL_MAT_ID arm of
+ * ggml_backend_cuda_device_supports_op, ggml-cuda.cu:3270-3330): as [K,N,n_expert], b, ids as for
+ * ggml_mi355x_mul_mat_id; true exactly when ggml_mi355x_mul_mat_id accepts the geometry. */
+GGML_MI355X_API int ggml_mi355x_supports_mul_mat_id(const ggml_mi355x_tensor *as, const ggml_mi355x_tensor *b,
+                                                    const ggml_mi355x_tensor *ids);
+
+/* The kernel launches ggml_mi355x_mul_mat (repacked != 0: ggml_mi355x_mul_mat_repacked) would make
+ * for these operands, as text into buf (e.g. "mmvq nc=1 lpr=64 rpw=1 grid=512x1x1", "mma tok=8 ...",
+ * "mmq8 tile=128x64 ..."). Launches nothing and touches no device memory (data pointers are only
+ * checked for alignment), so it runs without a GPU: tests pin the dispatch of the benchmark and
+ * reference-perf shapes with it. No reference counterpart (the CUDA backend's choice is internal). */
+GGML_MI355X_API int ggml_mi355x_mul_mat_plan(const ggml_mi355x_tensor *src0, const ggml_mi355x_tensor *src1, int repacked,
+                                             char *buf, size_t len);
+
+/* Re-read the GGML_MI355X_* tuning and diagnostics variables (read once otherwise):
+ * tests and benches that switch one between calls call this after changing the environment. */
+GGML_MI355X_API int ggml_mi355x_reload_settings(void);
+
 /* number of gfx950 devices visible to this process */
 GGML_MI355X_API int ggml_mi355x_device_count(void);
 

@@ -1,17 +1,34 @@
-"""Scan a gfx950 ISA listing (hipcc -S) for VALU reads of MFMA results and report the wait states
-between each MFMA and the first VALU instruction that reads one of its result registers.
+"""Scan a gfx950 ISA listing (hipcc --cuda-device-only -S) for the MFMA -> VALU dependences and
+check each against the wait states the compiler's gfx950 hazard model requires.
 
   python scripts/mfma_hazard_scan.py file.s [kernel-substring]
 
-Wait states are counted as the ISA does: one per issued instruction, N+1 per `s_nop N`
-(s_waitcnt and other SOPP count one). Only straight-line distance inside one basic block is
-measured (a label resets the scan), which is where the compiler's hazard recognizer places nops.
+The model (ROCm 7.2 llc, probed with `llc -mcpu=gfx950 -run-pass=post-RA-hazard-rec` on MIR
+pairs, scripts/mfma_hazard_probe.py; profiles/r06_mfma_hazards.txt):
+  v_mfma_i32_32x32x32_i8 (8 passes)  RAW 12  WAW 12  WAR-srcC 7
+  v_mfma_i32_16x16x32_i8 (4 passes)  RAW  8  WAW  8  WAR-srcC 3
+  (v_pk_fma_f32 and v_fma_f32 alike; a VALU write -> MFMA source needs 2)
+RAW: a VALU reads an MFMA's result; WAW: a VALU writes a register an MFMA in flight writes; WAR:
+a VALU writes a register an MFMA in flight reads as its C input. Wait states are counted as the
+ISA counts them: one per issued instruction, N+1 per `s_nop N`. The scan runs the listing in
+order across labels (fall-through) and, for every backward branch, once more from the branch
+target with the state at the branch (loop back-edges). It prints, per category and VALU class
+(packed f32 = v_pk_*, the rest scalar), the number of dependences, the minimum distance and
+every violation of the model.
 """
 import re
 import sys
-from collections import Counter
+from collections import defaultdict
 
+REQ = {  # mnemonic substring -> (RAW, WAW, WAR on srcC)
+    "v_mfma_i32_32x32x32_i8": (12, 12, 7),
+    "v_mfma_i32_32x32x16_i8": (12, 12, 7),
+    "v_mfma_i32_16x16x32_i8": (8, 8, 3),
+    "v_mfma_f32_32x32x16_f16": (12, 12, 7),
+    "v_mfma_f32_16x16x32_f16": (8, 8, 3),
+}
 RANGE = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
+HORIZON = 24
 
 
 def regs(tok: str) -> set:
@@ -24,36 +41,71 @@ def regs(tok: str) -> set:
     return out
 
 
-def scan(lines):
-    live = []          # (mfma line, dst regs, wait states since)
-    report = []
+def parse(lines):
+    insts, labels = [], {}
     for ln, line in lines:
-        s = line.strip()
-        if not s or s.startswith(";") or s.startswith("."):
-            if s.endswith(":") or s.startswith(".LBB"):
-                live = []
+        s = line.split(";")[0].strip()
+        if not s or s.startswith("."):
+            if s.startswith(".LBB") and s.endswith(":"):
+                labels[s[:-1]] = len(insts)
             continue
         if s.endswith(":"):
-            live = []
+            labels[s[:-1]] = len(insts)
             continue
         op = s.split()[0]
-        args = s[len(op):].split(";")[0]
-        parts = [p.strip() for p in args.split(",")]
-        ws = 1
-        if op == "s_nop":
-            ws = int(parts[0], 0) + 1
-        if op.startswith("v_") and not op.startswith("v_mfma"):
-            srcs = set()
-            for p in parts[1:]:
-                srcs |= regs(p)
-            for (mln, dst, w) in live:
-                if srcs & dst:
-                    report.append((op, w, mln, ln))
-            live = [(m, d - srcs, w) for (m, d, w) in live if d - srcs]   # first read only
-        live = [(m, d, w + ws) for (m, d, w) in live]
-        if op.startswith("v_mfma"):
-            live.append((ln, regs(parts[0]), 0))
-    return report
+        parts = [p.strip() for p in s[len(op):].split(",")] if len(s) > len(op) else []
+        insts.append((ln, op, parts))
+    return insts, labels
+
+
+def req_of(op):
+    for k, v in REQ.items():
+        if op.startswith(k):
+            return v
+    return (12, 12, 7) if op.startswith("v_mfma") else None
+
+
+def step(state, inst, stats, viol):
+    ln, op, parts = inst
+    ws = int(parts[0], 0) + 1 if op == "s_nop" else 1
+    if op.startswith("v_") and not op.startswith("v_mfma") and parts and parts[0]:
+        cls = "packed" if op.startswith("v_pk_") else "scalar"
+        dst = regs(parts[0])
+        src = set()
+        for p in parts[1:]:
+            src |= regs(p)
+        for (mln, mop, mdst, msrcc, w, rq) in state:
+            for cat, hit, need in (("RAW", src & mdst, rq[0]), ("WAW", dst & mdst, rq[1]), ("WAR-srcC", dst & msrcc, rq[2])):
+                if hit and w < 64:
+                    key = (cat, cls)
+                    stats[key][0] += 1
+                    stats[key][1] = min(stats[key][1], w)
+                    if w < need:
+                        viol.append((cat, cls, op, w, need, mln, ln))
+    state = [(m, mo, d, c, w + ws, rq) for (m, mo, d, c, w, rq) in state if w + ws < HORIZON]
+    if op.startswith("v_mfma"):
+        rq = req_of(op)
+        state.append((ln, op, regs(parts[0]), regs(parts[3]) if len(parts) > 3 else set(), 0, rq))
+    return state
+
+
+def scan(lines):
+    insts, labels = parse(lines)
+    stats = defaultdict(lambda: [0, 1 << 30])
+    viol = []
+    state = []
+    for i, inst in enumerate(insts):
+        state = step(state, inst, stats, viol)
+        op, parts = inst[1], inst[2]
+        if op.startswith("s_cbranch") or op == "s_branch":
+            tgt = labels.get(parts[0]) if parts else None
+            if tgt is not None and tgt <= i and state:   # back-edge: the loop head after the tail
+                st = list(state)
+                for j in range(tgt, min(len(insts), tgt + HORIZON)):
+                    st = step(st, insts[j], stats, viol)
+                    if not st:
+                        break
+    return stats, viol
 
 
 def main():
@@ -61,16 +113,16 @@ def main():
     pat = sys.argv[2] if len(sys.argv) > 2 else None
     lines, on = [], pat is None
     for i, l in enumerate(open(path), 1):
-        if pat and re.match(r"^_Z\w*:", l):
-            on = pat in l
+        if re.match(r"^_Z\w*:", l):
+            on = pat is None or pat in l
         if on:
             lines.append((i, l))
-    rep = scan(lines)
-    by_op = {}
-    for op, w, _, _ in rep:
-        by_op.setdefault(op, Counter())[w] += 1
-    for op, c in sorted(by_op.items()):
-        print(f"{op:24s} first-read wait states: min {min(c)}  histogram {dict(sorted(c.items()))}")
+    stats, viol = scan(lines)
+    for (cat, cls), (n, mn) in sorted(stats.items()):
+        print(f"{cat:9s} {cls:7s} dependences {n:7d}  min wait states {mn}")
+    print(f"violations of the model: {len(viol)}")
+    for v in viol[:20]:
+        print("  %s %s %s at %d < %d (mfma line %d, valu line %d)" % v)
 
 
 if __name__ == "__main__":

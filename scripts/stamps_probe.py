@@ -35,7 +35,7 @@ rpw = int(os.environ.get("GGML_MI355X_RPW", "0")) or (2 if N * BATCH >= 16384 el
 rows_per_wg = 8 * rpw
 nwg = min((N + rows_per_wg - 1) // rows_per_wg, max(1, (1024 + BATCH - 1) // BATCH))
 buf = np.zeros(4 * 65536 + nwg * 8 * 4, np.uint64)   # workgroup stamps, then per-wave stamps
-wa, wq = [], []
+wa, wq, wd = [], [], []
 spans, xs, ds, es, starts, clk = [], [], [], [], [], []
 for i in range(16):
     for j in range(63 if BATCH == 1 else 3):   # measure a launch inside a back-to-back run
@@ -46,6 +46,7 @@ for i in range(16):
     w = buf[4 * 65536:].reshape(nwg, 8, 4).astype(np.int64)   # per wave: start, x arrived, x quantized
     wa.append(np.median((w[:, :, 1] - w[:, :, 0]) * 10))
     wq.append(np.median((w[:, :, 2] - w[:, :, 1]) * 10))
+    wd.append(np.median((w[:, :, 3] - w[:, :, 2]) * 10))
     clk.append(np.median((s[:, 5] - s[:, 4]) / np.maximum(1, (s[:, 3] - s[:, 0]) * 10)))
     t0 = s[:, 0].min()
     spans.append((s[:, 3].max() - t0) * 10)
@@ -58,4 +59,5 @@ print(f"  kernel span (first start -> last end) ns: median {np.median(spans):.0f
 print(f"  start offsets ns (median, max over WGs): {np.median(starts, axis=0)}")
 print(f"  shader clock during the workgroup (memtime/realtime): {np.median(clk):.2f} GHz")
 print(f"  per-WG median ns: start->x_ready {np.median(xs):.0f}  x_ready->end {np.median(ds):.0f}")
-print(f"  per-wave median ns: start->activations in registers {np.median(wa):.0f}  ->quantized {np.median(wq):.0f}")
+print(f"  per-wave median ns: start->activations in registers {np.median(wa):.0f}  ->quantized {np.median(wq):.0f}"
+      f"  ->dots stored {np.median(wd):.0f}")

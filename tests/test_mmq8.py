@@ -1,6 +1,7 @@
 """GPU parity of the int8 MFMA mat-mat path (csrc/mmq8.hip) against the CPU oracle.
 
-The path is forced with GGML_MI355X_MMQ=i8 (read on every call). Its activations are quantized
+Every case with more than 8 tokens runs the int8 tile (the only mat-mat path); the fixture
+force_i8 runs it on the weights in place and on a per-call repacked copy. Its activations are quantized
 exactly like the CPU backend's Q8_K blocks (quantize_row_q8_K_ref, reference
 src/ggml-quants.c:2555-2591) and its block dot products are exact int32 sums, so:
   * Q4_K / Q5_K / Q6_K: the oracle (ggml_vec_dot_q4_K_q8_K / _q5_K_ / _q6_K_ semantics on the
@@ -10,8 +11,6 @@ src/ggml-quants.c:2555-2591) and its block dot products are exact int32 sums, so
     NMSE <= 5e-4 (the reference's MUL_MAT bar, test-backend-ops.cpp:3106-3108), and against the
     exact float64 product of the bit-exact dequantized weights within the activation rounding.
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -28,21 +27,11 @@ TIGHT = {qref.Q4_K: 1e-9, qref.Q5_K: 1e-9, qref.Q6_K: 1e-9, qref.Q4_0: 5e-4, qre
 
 
 @pytest.fixture(autouse=True, params=["inplace", "repack"])
-def force_i8(request):
+def force_i8(request, mm):
     """every case runs twice: on the in-place int8 tile (mmq8_kernel) and on the tile over a
     per-call repacked copy of the weights (repack_kernel + mmq8r_kernel, GGML_MI355X_MMQ_REPACK_MIN)"""
-    saved = {k: os.environ.get(k) for k in ("GGML_MI355X_MMQ", "GGML_MI355X_MMQ_REPACK_MIN")}
-    os.environ["GGML_MI355X_MMQ"] = "i8"
-    if request.param == "repack":
-        os.environ["GGML_MI355X_MMQ_REPACK_MIN"] = "9"
-    else:
-        os.environ.pop("GGML_MI355X_MMQ_REPACK_MIN", None)
-    yield request.param
-    for k, v in saved.items():
-        if v is None:
-            os.environ.pop(k, None)
-        else:
-            os.environ[k] = v
+    with mm.knobs(GGML_MI355X_MMQ_REPACK_MIN=9 if request.param == "repack" else None):
+        yield request.param
 
 
 def exact(t, w, N, K, x, M_):
@@ -51,22 +40,12 @@ def exact(t, w, N, K, x, M_):
 
 
 def case(mm, t, N, M_, K, seed=1, ksplit=None, tt=None, sk=None, ret_got=False):
-    if ksplit is not None:
-        os.environ["GGML_MI355X_MMQ8_KSPLIT"] = str(ksplit)
-    if tt is not None:
-        os.environ["GGML_MI355X_MMQ8_TT"] = str(tt)
-    if sk is not None:
-        os.environ["GGML_MI355X_MMQ8_SK"] = str(sk)
-    try:
-        w = qref.quantize(t, qref.fill_uniform(N * K, seed), n_per_row=K)
-        x = qref.fill_uniform(M_ * K, seed + 1)
-        a = G.Operand(t, w, [K, N, 1, 1], qref.contiguous_nb(t, [K, N, 1, 1]))
-        b = G.Operand(qref.F32, x, [K, M_, 1, 1], qref.contiguous_nb(qref.F32, [K, M_, 1, 1]))
+    w = qref.quantize(t, qref.fill_uniform(N * K, seed), n_per_row=K)
+    x = qref.fill_uniform(M_ * K, seed + 1)
+    a = G.Operand(t, w, [K, N, 1, 1], qref.contiguous_nb(t, [K, N, 1, 1]))
+    b = G.Operand(qref.F32, x, [K, M_, 1, 1], qref.contiguous_nb(qref.F32, [K, M_, 1, 1]))
+    with mm.knobs(GGML_MI355X_MMQ8_KSPLIT=ksplit, GGML_MI355X_MMQ8_TT=tt, GGML_MI355X_MMQ8_SK=sk):
         got = run_mul_mat(mm, a, b, [N, M_, 1, 1])
-    finally:
-        os.environ.pop("GGML_MI355X_MMQ8_KSPLIT", None)
-        os.environ.pop("GGML_MI355X_MMQ8_TT", None)
-        os.environ.pop("GGML_MI355X_MMQ8_SK", None)
     assert np.all(np.isfinite(got))
     want = G.oracle_mul_mat(a, b, [N, M_, 1, 1])
     err = qref.nmse(got, want)
@@ -92,28 +71,6 @@ def test_mmq8_ksplit(mm, t, ksplit):
     """split-K over workgroups (fixed-order reduce), with a super-block count the splits do not
     divide evenly"""
     case(mm, t, 192, 96, 256 * 5, seed=7, ksplit=ksplit)
-
-
-@pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])
-@pytest.mark.parametrize("shape", [(4224, 1024, 768, None), (8192, 640, 512, None), (4160, 1152, 1024, None),
-                                   (8320, 520, 256, None), (4224, 1024, 768, 64)],
-                         ids=lambda s: "x".join(map(str, s[:3])) + (f"_tt{s[3]}" if s[3] else ""))
-def test_mmq8_stream_k(mm, t, shape, force_i8):
-    """stream-K (GGML_MI355X_MMQ8_SK=1): more 128-row tiles than the 256 workgroups, so the
-    (tile, super-block) units split unevenly and tiles are finished by a second workgroup through
-    the write-through partial + counter hand-off; against the oracle, bit-identical on a second
-    run (two operands per tile: the order of arrival does not change the sum) and within the
-    fp32 scale-sum order of the plain tiles (SK=0)"""
-    if force_i8 == "repack":
-        pytest.skip("stream-K is the in-place tile's")
-    N, M_, K, tt = shape
-    if qref.BLCK[t] == 256 and K % 256:
-        K = 768
-    g1 = case(mm, t, N, M_, K, seed=13, sk=1, tt=tt, ret_got=True)
-    g2 = case(mm, t, N, M_, K, seed=13, sk=1, tt=tt, ret_got=True)
-    assert np.array_equal(g1.view(np.uint32), g2.view(np.uint32)), "stream-K result not repeatable"
-    g0 = case(mm, t, N, M_, K, seed=13, sk=0, tt=tt, ret_got=True)
-    assert qref.nmse(g1, g0) <= 1e-9
 
 
 @pytest.mark.parametrize("t", TYPES, ids=lambda t: qref.NAMES[t])

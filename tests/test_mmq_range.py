@@ -3,7 +3,6 @@ layout) converts every scale to f32, so it is exact at any M, including the K = 
 (tests/test_mmq8.py covers M = 200 and 512 for all five types). (The f16 tiles that overflowed
 past d > 511 were removed in round 5.) Checked against the CPU oracle on rows mixing ordinary and
 huge scales."""
-import os
 
 import numpy as np
 import pytest
@@ -25,18 +24,11 @@ def mm():
     return M
 
 
-@pytest.fixture(params=["i8", "default"])
-def path(request):
-    old = os.environ.get("GGML_MI355X_MMQ")
-    if request.param == "default":
-        os.environ.pop("GGML_MI355X_MMQ", None)
-    else:
-        os.environ["GGML_MI355X_MMQ"] = request.param
-    yield request.param
-    if old is None:
-        os.environ.pop("GGML_MI355X_MMQ", None)
-    else:
-        os.environ["GGML_MI355X_MMQ"] = old
+@pytest.fixture(params=["inplace", "repack"])
+def path(request, mm):
+    """the int8 tile on the weights in place, and on a per-call repacked copy"""
+    with mm.knobs(GGML_MI355X_MMQ_REPACK_MIN=9 if request.param == "repack" else None):
+        yield request.param
 
 
 @pytest.mark.parametrize("t,big", [(qref.Q8_0, 7.0e4), (qref.Q4_K, 2.0e3), (qref.Q4_0, 1.0e5)])

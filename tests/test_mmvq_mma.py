@@ -15,8 +15,6 @@ forms); ragged rows (N % 16 != 0); Q4_0 / Q8_0 K that ends inside a 128-step (K 
 broadcast batch slices (ne12 = 2 * ne02); every per-wave step run (K = 4096 .. 28672) with one and
 two K parts; one or two row tiles per workgroup; paired and unpaired steps; bitwise repeatability.
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -42,16 +40,8 @@ def operands(t, N, M_, K, seed, ne2=(1, 1)):
 
 
 def run_with(mm, a, b, out_ne, env):
-    saved = {k: os.environ.get(k) for k in env}
-    os.environ.update({k: str(v) for k, v in env.items()})
-    try:
+    with mm.knobs(**env):
         return run_mul_mat(mm, a, b, out_ne)
-    finally:
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
 
 
 def check(mm, t, N, M_, K, seed=3, ne2=(1, 1), oracle=True):
@@ -78,9 +68,43 @@ def test_mma_columns(mm, t, M_):
 @pytest.mark.parametrize("t", [qref.Q4_0, qref.Q8_0], ids=lambda t: qref.NAMES[t])
 @pytest.mark.parametrize("K", [32, 64, 96, 160, 4160])
 def test_mma_partial_step(mm, t, K):
-    """the last 128-step holds 1..3 live blocks: activation codes past K are zero, the weight
-    loads clamp to the row's last block"""
+    """the last 128-step holds 1..3 live blocks: activation codes past K are zero; the weight
+    loads of the blocks past K read whatever follows the row (the next row, here), and the
+    kernel zeroes those blocks' weight scales"""
     check(mm, t, 37, 4, K)
+
+
+@pytest.mark.parametrize("t", [qref.Q4_0, qref.Q8_0], ids=lambda t: qref.NAMES[t])
+@pytest.mark.parametrize("K", [160, 4160])
+def test_mma_partial_step_padded_rows(mm, t, K):
+    """a strided view whose row padding (nb01 > row bytes) holds f16 infinities where
+    the blocks past K would have their scale d: those blocks must not turn 0 * d into NaN"""
+    N, M_ = 40, 4
+    rowb = K // 32 * qref.TSIZE[t]
+    pad = 4 * qref.TSIZE[t]
+    w = qref.quantize(t, qref.fill_uniform(N * K, 5), n_per_row=K).view(np.uint8).reshape(N, rowb)
+    buf = np.tile(np.array([0x00, 0x7C], np.uint8), N * (rowb + pad) // 2 + 1)[:N * (rowb + pad)].reshape(N, rowb + pad)
+    buf[:, :rowb] = w
+    nb = [qref.TSIZE[t], rowb + pad, (rowb + pad) * N, (rowb + pad) * N]
+    a = G.Operand(t, buf.ravel(), [K, N, 1, 1], nb)
+    x = qref.fill_uniform(M_ * K, 6)
+    b = G.Operand(qref.F32, x, [K, M_, 1, 1], qref.contiguous_nb(qref.F32, [K, M_, 1, 1]))
+    out_ne = [N, M_, 1, 1]
+    got = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 1})
+    assert np.all(np.isfinite(got))
+    assert qref.nmse(got, G.oracle_mul_mat(a, b, out_ne)) <= 5e-4
+
+
+@pytest.mark.parametrize("t,M_,K", [(qref.Q4_0, 5, 25600), (qref.Q4_K, 3, 49408), (qref.Q4_0, 8, 25600)])
+def test_mma_rule_shapes_past_the_image(mm, t, M_, K):
+    """the default rule takes these column counts at these K, but the MFMA run
+    the launcher would need (paired runs rounded up to even, 14 steps at 4 tokens) does not fit
+    its LDS image; mmvq_mma_supported now says so and the call runs on the VALU kernels instead
+    of failing (tests/test_dispatch_plan.py pins the choice)"""
+    a, b, out_ne = operands(t, 64, M_, K, 21)
+    got = run_mul_mat(mm, a, b, out_ne)
+    assert np.all(np.isfinite(got))
+    assert qref.nmse(got, G.oracle_mul_mat(a, b, out_ne, threads=16)) <= 5e-4
 
 
 @pytest.mark.parametrize("t", [qref.Q4_K, qref.Q5_K], ids=lambda t: qref.NAMES[t])

@@ -7,7 +7,6 @@ sums, so against the CPU oracle NMSE <= 1e-9 for the K-quants and the reference'
 Q4_0 / Q8_0 (activations blocked per 256 here, per 32 on the CPU). The repacked copy made once
 and the per-call repack (GGML_MI355X_MMQ_REPACK_MIN) run the same kernel on the same bytes, so
 they agree bit for bit."""
-import os
 
 import numpy as np
 import pytest
@@ -85,15 +84,8 @@ def test_repacked_equals_per_call_repack(mm, t):
     from test_gpu_parity import run_mul_mat
     a, b, out_ne = operands(t, 256, 200, 1024, seed=11)
     once = run_repacked(mm, a, b, out_ne)
-    old = os.environ.get("GGML_MI355X_MMQ_REPACK_MIN")
-    os.environ["GGML_MI355X_MMQ_REPACK_MIN"] = "9"
-    try:
+    with mm.knobs(GGML_MI355X_MMQ_REPACK_MIN=9):
         per_call = run_mul_mat(mm, a, b, out_ne)
-    finally:
-        if old is None:
-            os.environ.pop("GGML_MI355X_MMQ_REPACK_MIN", None)
-        else:
-            os.environ["GGML_MI355X_MMQ_REPACK_MIN"] = old
     np.testing.assert_array_equal(once.view(np.uint32), per_call.view(np.uint32))
 
 
