@@ -409,6 +409,22 @@ int main(int argc, char **argv) {
     gen_mul_mat(GGML_TYPE_Q4_0, 8192, 5, 4096, 1, 1, 1, 1, id4, false);
     gen_mul_mat(GGML_TYPE_Q4_K, 8192, 8, 4096, 1, 1, 1, 1, id4, false);
 
+    // round 6: the MFMA mat-vec's forms at K = 8192 / 28672 (one and two K parts, paired and
+    // unpaired steps, 4- and 8-token column packing), the shapes whose MFMA run would not fit the
+    // launcher's image (paired Q4_0 K = 25600 at 5..8 columns, Q4_K K = 49408 at 3: the VALU kernels
+    // take them) and Q6_K at the reference perf harness's 8-column shape in full
+    // (test-backend-ops.cpp:6195-6202, N = 4096, K = 14336)
+    gen_mul_mat(GGML_TYPE_Q4_0, 256, 5, 8192, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q4_K, 256, 3, 8192, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q8_0, 256, 8, 8192, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q4_0, 256, 8, 28672, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q8_0, 256, 5, 28672, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q4_K, 256, 8, 28672, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q5_K, 256, 8, 28672, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q4_0, 64, 5, 25600, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q4_K, 64, 3, 49408, 1, 1, 1, 1, id4, false);
+    gen_mul_mat(GGML_TYPE_Q6_K, 4096, 8, 14336, 1, 1, 1, 1, id4, false);
+
     std::string path = g_dir + "/manifest.json";
     FILE *f = fopen(path.c_str(), "w");
     fprintf(f, "{\n\"generator\": \"oracle/gen_golden.cpp linked to oracle/_ref/libggml-ref.so (reference sources, oracle/ref.mk)\",\n"
