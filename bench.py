@@ -182,6 +182,18 @@ def measured_traffic(key: str):
         return None
 
 
+def measured_rocprof(key: str):
+    """the headline kernel's rocprofv3 durations from the committed profile of the same command at
+    the round's final HEAD (profiles/headline_rocprof.json, scripts/rocprof_headline.py); None
+    when absent"""
+    try:
+        with open(os.path.join(ROOT, "profiles", "headline_rocprof.json")) as f:
+            r = json.load(f)[key]
+    except (OSError, KeyError, ValueError):
+        return None
+    return {k: r[k] for k in ("mean_us", "median_us", "launches", "frac_mean", "frac_median", "summary", "round") if k in r}
+
+
 def rowsplit_configs(torch, world: int, rank: int, reps: int = 20) -> dict:
     """configs.*_rowsplit: ONE matrix row-sharded over the `world` ranks (rowsplit.py, the
     split-buffer partition) and dst all-gathered over RCCL every call — strong scaling of a
@@ -686,6 +698,7 @@ def main() -> None:
                          "traffic": measured_traffic("q4_0_4096x4096_m1_b64") if BATCH == 64 else None,
                          "traffic_source": "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE, x2 gfx950 correction)",
                          "launch_us": round(kernel_us, 3), "launch_us_basis": "HIP events around the timed region",
+                         "rocprof": measured_rocprof("q4_0_4096x4096_m1_b64") if BATCH == 64 else None,
                          "alg_bytes_per_launch": g.bytes,
                          "frac_of_measured_copy_bw": round(achieved / HBM_MEASURED_GBS, 4)},
             "cpu_baseline": cpu,

@@ -101,15 +101,22 @@ int type_bytes(int t) {
 bool is_hot_quant(int t) { return type_blck(t) != 0; }
 
 // rows per wave for the mat-vec. Every workgroup quantizes its column(s) of src1 once, so
-// more rows per workgroup amortize that; fewer rows give more workgroups. A single 4096-row
-// matrix needs all 512 workgroups of RPW=1 to cover 256 CUs twice; batched / taller problems
-// (rows x batch) switch to 2 and 4 rows per wave.
+// more rows per workgroup amortize that (the activation loads and their quantization are the
+// critical path of a single-matrix launch, profiles/r06_single_launch_decomposition.txt); fewer
+// rows give more workgroups. Two rows per wave from 4096 rows (x batch) on, i.e. from one
+// 16-row workgroup per CU: single 4096 x 4096 Q4_0 4.91 vs 5.06-5.51 us, 4096 x 11008 Q4_K
+// 8.7 vs 9.5, Q5_K 10.5-11.1 vs 11.6-11.8 (profiles/r06_singles_ab.txt, rocprof means, two
+// interleaved rounds; round 5's rule switched at 16384).
 // Q6_K keeps one row per wave: its two-row kernel needs 133 VGPRs, which leaves one 8-wave
-// workgroup per CU instead of two (Q6_K 4096x11008 x24: 169 vs 178 us, profiles/r03_q6k_rpw.txt).
-static int pick_rpw(int type, int64_t rows_total) {
+// workgroup per CU instead of two (Q6_K 4096x11008 x24: 169 vs 178 us, profiles/r03_q6k_rpw.txt;
+// single 4096 x 11008: 13.5-13.8 vs 12.6-12.8 us, profiles/r06_singles_ab.txt).
+// one_col: the rule above is for single-column launches of the whole-K kernel (what was
+// measured); column groups and the chunked-K kernels (mmvq_ring.hip) keep round 5's switch at
+// 16384 rows.
+static int pick_rpw(int type, int64_t rows_total, bool one_col) {
     if (settings().rpw > 0) return settings().rpw;
     if (type == T_Q6_K) return 1;
-    return rows_total >= 16384 ? 2 : 1;
+    return rows_total >= (one_col ? 4096 : 16384) ? 2 : 1;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -216,7 +223,8 @@ static int mma_min_cols(int type, int K, int N, int slices) {
 // that would run (ggml_mi355x_mul_mat_plan; scratch then counts as available)
 static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st, Scratch *scratch = nullptr,
                            std::string *plan = nullptr) {
-    const int rpw = pick_rpw(type, (int64_t)m.N * m.ne12 * m.ne13);
+    const int64_t rows_total = (int64_t)m.N * m.ne12 * m.ne13;
+    const int rpw = pick_rpw(type, rows_total, false), rpw_one = pick_rpw(type, rows_total, true);
     const bool have_scratch = scratch != nullptr || plan != nullptr;
     auto note = [&](const std::string &s) {
         if (!plan->empty()) *plan += "; ";
@@ -264,10 +272,10 @@ static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st
             while (nc > 1 && (!mmvq_has_nc(nc) || mmvq_lds_bytes(m.K, nc) > LDS_LIMIT || m.K > mmvq_max_k_for_nc(nc))) --nc;
             g.M = nc;
             if (plan) {
-                note(mmvq_plan_text(g, nc, rpw));
+                note(mmvq_plan_text(g, nc, nc == 1 ? rpw_one : rpw));
                 e = hipSuccess;
             } else {
-                e = mmvq_launch(type, g, nc, rpw, st);
+                e = mmvq_launch(type, g, nc, nc == 1 ? rpw_one : rpw, st);
             }
         }
         if (e != hipSuccess) return e;

@@ -31,9 +31,8 @@
 namespace mi355x {
 
 // measurement builds only (scripts/mmvq_exp.sh): 1 = no activation loads, 2 = no quantization
-// into LDS, 4 = no weight loads, 8 = no barrier before the dots, 16 = an issue-order s_barrier
-// between every wave's activation loads and the weight loads, 32 = weights issued before the
-// activations (not built: the activation loads are the first instructions either way)
+// into LDS, 4 = no weight loads, 8 = no barrier before the dots, 16 = no issue-order barrier
+// (profiles/r06_single_launch_decomposition.txt)
 #ifndef MMVQ_EXP
 #define MMVQ_EXP 0
 #endif
@@ -721,7 +720,12 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
 
     Frag<T> fa[RPW], fb[RPW];
     int g = blockIdx.x, it = 0;                   // the unit being computed (grid.x <= n_groups)
-    if constexpr (MMVQ_EXP & 16) asm volatile("s_barrier" ::: "memory");
+    // issue order: every wave's activation loads ahead of every wave's weight loads. A plain
+    // s_barrier (no waitcnt: gfx950 barriers do not drain memory) between the two; without it the
+    // late waves' activations queue in the CU's load path behind the early waves' weights, and
+    // the workgroup's quantization barrier waits for them (single 4096 x 4096 Q4_K launch:
+    // activations in registers 1080 -> 720 ns after the wave's start, 5.96 -> 5.74 us)
+    if constexpr (!FUSE && !(MMVQ_EXP & 16)) asm volatile("s_barrier" ::: "memory");
     load_unit(fa, g, it);
     [[maybe_unused]] EpiOps ea{}, eb{};
     if constexpr (FUSE) ea = load_epi(g);

@@ -29,6 +29,7 @@ squash() {  # squash <dir>
 [ -x scripts/hbm_probe ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o scripts/hbm_probe scripts/hbm_probe.hip || exit 1
 [ -s $O/bench.log ] || step bench 600 python bench.py
 step prof_bench 600 $RP -d $O/bench -o run -- python bench.py --no-extra --cpu-seconds 1
+python scripts/rocprof_headline.py $(find $O/bench -name '*kernel_trace.csv' | head -1) $O/headline_rocprof.json $R profiles/${R}_bench_trace_summary.txt > /dev/null
 squash $O/bench
 step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_fetch -o pmc -- python bench.py --no-extra --no-gpt2 --cpu-seconds 1 --steps 5 --warmup 1
 python scripts/traffic_from_pmc.py $(find $O/pmc_fetch -name '*counter_collection.csv' | head -1) $O/traffic.json $R > /dev/null

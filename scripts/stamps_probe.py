@@ -31,7 +31,7 @@ L.ggml_mi355x_debug_stamps.argtypes = [C.c_void_p, C.c_size_t]
 g = bench.MatVecSet(torch, t, K, N, Mc, BATCH, 64 if BATCH == 1 else 2)
 g.launch(0)
 torch.cuda.synchronize()
-rpw = int(os.environ.get("GGML_MI355X_RPW", "0")) or (2 if N * BATCH >= 16384 else 1)
+rpw = int(os.environ.get("GGML_MI355X_RPW", "0")) or (2 if N * BATCH >= 4096 and tname != "q6_K" else 1)
 rows_per_wg = 8 * rpw
 nwg = min((N + rows_per_wg - 1) // rows_per_wg, max(1, (1024 + BATCH - 1) // BATCH))
 buf = np.zeros(4 * 65536 + nwg * 8 * 4, np.uint64)   # workgroup stamps, then per-wave stamps
