@@ -166,22 +166,42 @@ __device__ __forceinline__ void q8_dma16(__amdgpu_buffer_rsrc_t r, uint8_t *lds_
 // gathered from src1 (slot % ne11, token) as mmq_convert_x does; padding positions are zeros.
 // zero_dst: also clear dst (the 2-way split-K kernel adds both halves into it): the wave of
 // (token, super-block sb) clears columns [sb * ceil(N / n_sb), ...) of the token's row.
-// UPW units (token, super-block) per wave, unit u = wave * UPW + i -> token u / n_sb, super-block
-// u % n_sb (a wave's units are consecutive super-blocks of one token: one contiguous run of the
-// row), all UPW loads issued before the first is quantized. One unit per wave (UPW = 1, the MOE
-// gather) launched 8192 waves for 512 tokens x 16 super-blocks, and the dispatch of that many
-// waves, not the 10 MB moved, set the kernel's 6-7 us (profiles/r06_quant_x_upw.txt).
-// grid.x = ceil(units / (4 UPW)) workgroups of 4 waves; units = (64-token images) * 64 * n_sb.
-template <int T, int UPW>
-__device__ __forceinline__ void q8x_unit(const MmArgs &a, uint8_t *__restrict__ ximg, int n_tt, int n_sb, int slice, int tok,
-                                         int sb, const float (&v)[4], int zero_dst) {
+// grid.x = (64-token images) * 16 * n_sb: 4 tokens (waves) of one super-block per workgroup.
+template <int T, bool MOE = false>
+__global__ __launch_bounds__(256) void mmq8_quant_x(const MmArgs a, uint8_t *__restrict__ ximg, int n_tt, int n_sb,
+                                                    const Moe8 moe, int zero_dst) {
     constexpr int XB = ximg_bytes<T>();
     const int lane = threadIdx.x & 63;
+    const int tok = (blockIdx.x / n_sb) * 4 + (threadIdx.x >> 6), sb = blockIdx.x % n_sb;
+    const int slice = blockIdx.y;
     const int i12 = slice % a.ne12, i13 = slice / a.ne12;
-    if (zero_dst && tok < a.M) {
+    if (!MOE && zero_dst && tok < a.M) {
         const int chunk = (a.N + n_sb - 1) / n_sb, c1 = min(a.N, (sb + 1) * chunk);
         float *drow = reinterpret_cast<float *>(a.dst + (int64_t)i12 * a.nb2 + (int64_t)i13 * a.nb3 + (int64_t)tok * a.nb1);
         for (int c = sb * chunk + lane; c < c1; c += 64) drow[c] = 0.f;
+    }
+    const uint8_t *row = nullptr;
+    if constexpr (MOE) {
+        int e, q0, cnt;
+        if (!moe8_tile(moe, tok >> 6, e, q0, cnt)) return;   // (uniform: 4 tokens of one tile)
+        if ((tok & 63) < cnt) {
+            const int pair = moe.pos_pair[q0 + (tok & 63)];
+            row = a.x + (int64_t)((pair % moe.n_used) % a.ne11_b) * a.nb11 + (int64_t)(pair / moe.n_used) * a.nb12;
+        }
+    } else if (tok < a.M) {
+        row = a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13 + (int64_t)tok * a.nb11;
+    }
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    const int k0 = sb * Q8_QK + 4 * lane;
+    if (row != nullptr && k0 < a.K) {   // (K % 32 == 0: a lane's 4 values are all in or all out)
+        const float *src = reinterpret_cast<const float *>(row) + k0;
+        if (a.x_aligned16) {
+            const float4 f = *reinterpret_cast<const float4 *>(src);
+            v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = src[i];
+        }
     }
     // the signed value of largest |x|, first k on ties (the reference's strict '>'): (|x|, k, x)
     // reduced with max |x|, then min k — a total order, so the butterfly gives every lane the
@@ -224,61 +244,6 @@ __device__ __forceinline__ void q8x_unit(const MmArgs &a, uint8_t *__restrict__ 
     }
     if (lane == 0) *reinterpret_cast<float *>(img + XI_DX + tl * 4) = d;
 }
-
-template <int T, bool MOE = false, int UPW = 1>
-__global__ __launch_bounds__(256) void mmq8_quant_x(const MmArgs a, uint8_t *__restrict__ ximg, int n_tt, int n_sb,
-                                                    const Moe8 moe, int zero_dst) {
-    static_assert(!MOE || UPW == 1, "the MOE gather runs one unit per wave");
-    const int lane = threadIdx.x & 63;
-    const int slice = blockIdx.y;
-    const int i12 = slice % a.ne12, i13 = slice / a.ne12;
-    const int64_t n_units = (int64_t)n_tt * Q8_TOK * n_sb;
-    const int64_t u0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * UPW;
-    float v[UPW][4];
-    int tok[UPW], sb[UPW];
-    bool live[UPW];
-#pragma unroll
-    for (int i = 0; i < UPW; ++i) {
-        const int64_t u = u0 + i;
-        live[i] = u < n_units;
-        tok[i] = (int)(u / n_sb);
-        sb[i] = (int)(u % n_sb);
-        v[i][0] = v[i][1] = v[i][2] = v[i][3] = 0.f;
-        const uint8_t *row = nullptr;
-        if constexpr (MOE) {
-            int e, q0, cnt;
-            if (!moe8_tile(moe, tok[i] >> 6, e, q0, cnt)) {   // (uniform: the wave's token's tile)
-                live[i] = false;
-                continue;
-            }
-            if ((tok[i] & 63) < cnt) {
-                const int pair = moe.pos_pair[q0 + (tok[i] & 63)];
-                row = a.x + (int64_t)((pair % moe.n_used) % a.ne11_b) * a.nb11 + (int64_t)(pair / moe.n_used) * a.nb12;
-            }
-        } else if (live[i] && tok[i] < a.M) {
-            row = a.x + (int64_t)i12 * a.nb12 + (int64_t)i13 * a.nb13 + (int64_t)tok[i] * a.nb11;
-        }
-        const int k0 = sb[i] * Q8_QK + 4 * lane;
-        if (row != nullptr && k0 < a.K) {   // (K % 32 == 0: a lane's 4 values are all in or all out)
-            const float *src = reinterpret_cast<const float *>(row) + k0;
-            if (a.x_aligned16) {
-                const float4 f = *reinterpret_cast<const float4 *>(src);
-                v[i][0] = f.x; v[i][1] = f.y; v[i][2] = f.z; v[i][3] = f.w;
-            } else {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) v[i][q] = src[q];
-            }
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < UPW; ++i)
-        if (live[i]) q8x_unit<T, UPW>(a, ximg, n_tt, n_sb, slice, tok[i], sb[i], v[i], MOE ? 0 : zero_dst);
-}
-
-// units per wave of a plain (non-MOE) quantizer launch: 8 once that still leaves >= 512 waves
-constexpr int Q8X_UPW = 8;
-static int64_t q8x_units(int n_img, int n_sb) { return (int64_t)n_img * Q8_TOK * n_sb; }
-static bool q8x_wide(int n_img, int n_sb) { return q8x_units(n_img, n_sb) >= 512 * Q8X_UPW; }
 
 // ------------------------------------------------------------------------------------------
 // weight staging. Every thread loads its tasks of the row tile's super-block into registers one
@@ -1457,22 +1422,12 @@ bool mmq8_images_fit(int type, const MmArgs &a) {
 }
 
 template <int T>
-static void q8x_launch(const MmArgs &a, uint8_t *ximg, int n_img, int n_sb, int slices, bool atomic, hipStream_t st) {
-    const int64_t units = q8x_units(n_img, n_sb);
-    if (q8x_wide(n_img, n_sb))
-        hipLaunchKernelGGL((mmq8_quant_x<T, false, Q8X_UPW>), dim3((unsigned)((units + 4 * Q8X_UPW - 1) / (4 * Q8X_UPW)), slices),
-                           dim3(256), 0, st, a, ximg, n_img, n_sb, Moe8{}, atomic ? 1 : 0);
-    else
-        hipLaunchKernelGGL((mmq8_quant_x<T, false, 1>), dim3((unsigned)((units + 3) / 4), slices), dim3(256), 0, st, a, ximg, n_img,
-                           n_sb, Moe8{}, atomic ? 1 : 0);
-}
-
-template <int T>
 static void launch8(const MmArgs &a, uint8_t *ximg, int tr_rows, int tt_tok, int n_tt, int slices, int ksplit,
                     int sb_per, float *part, bool atomic, const StreamK &sk, hipStream_t st) {
     const int n_sb = (a.K + Q8_QK - 1) / Q8_QK;
     const int n_img = n_tt * (tt_tok / Q8_TOK);   // 64-token images per slice (tokens past M: zeros)
-    q8x_launch<T>(a, ximg, n_img, n_sb, slices, atomic, st);
+    hipLaunchKernelGGL(mmq8_quant_x<T>, dim3((unsigned)(n_img * (Q8_TOK / 4) * n_sb), slices), dim3(256), 0, st, a, ximg,
+                       n_img, n_sb, Moe8{}, atomic ? 1 : 0);
     const int64_t row_b = (int64_t)a.K / QT<T>::blck * QT<T>::bytes;
     const uint32_t w_extent = (uint32_t)((int64_t)(a.N - 1) * a.nb01 + row_b);   // (the kernel rounds it up)
     const int n_rt = (a.N + tr_rows - 1) / tr_rows;
@@ -1738,7 +1693,8 @@ template <int T>
 static void launch8r(const MmArgs &a, const RpArgs &r, uint8_t *ximg, int n_tt, int slices, int ksplit, int sb_per,
                      float *part, bool atomic, hipStream_t st) {
     const int n_sb = r.n_sb;
-    q8x_launch<T>(a, ximg, n_tt, n_sb, slices, atomic, st);
+    hipLaunchKernelGGL(mmq8_quant_x<T>, dim3((unsigned)(n_tt * (Q8_TOK / 4) * n_sb), slices), dim3(256), 0, st, a, ximg,
+                       n_tt, n_sb, Moe8{}, atomic ? 1 : 0);
     const int n_rt128 = (a.N + 127) / 128;
     const unsigned gx = (unsigned)(n_rt128 * ksplit * n_tt);
     const int flags = ((gx % 8 == 0) ? 1 : 0) | (atomic ? 4 : 0);

@@ -16,3 +16,10 @@ for L in HEAD QX; do
   rm -f $(find $d -name '*kernel_trace.csv')
 done
 timeout -k 10 1200 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_mmq8.py tests/test_mmq8_stream_k.py tests/test_gpu_parity.py -k "mmq8 or mm_17 or mm_18 or mmid" > $O/tests.txt 2>&1; echo "tests rc=$?" >> $O/tests.txt
+S="q4_0:4096:4096:3:16 q4_0:4096:4096:8:16 q8_0:4096:4096:5:16 q4_K:4096:4096:3:16 q4_K:4096:4096:5:16 q4_K:4096:4096:8:16 q5_K:4096:4096:8:16"
+for rep in 1 2; do
+  timeout -k 10 180 env GGML_MI355X_MMA=0 python scripts/mmvq_bench.py $S >> $O/fuse.txt 2>&1 || exit 1
+  timeout -k 10 180 env GGML_MI355X_MMA=2 GGML_MI355X_MMA_FUSE=0 python scripts/mmvq_bench.py $S >> $O/fuse.txt 2>&1 || exit 1
+  timeout -k 10 180 env GGML_MI355X_MMA=2 GGML_MI355X_MMA_FUSE=1 python scripts/mmvq_bench.py $S >> $O/fuse.txt 2>&1 || exit 1
+done
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_mmvq_mma.py > $O/tests_mma.txt 2>&1; echo "tests rc=$?" >> $O/tests_mma.txt
