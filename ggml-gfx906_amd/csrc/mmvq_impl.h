@@ -724,8 +724,10 @@ __global__ __launch_bounds__(MMVQ_THREADS) void mmvq_kernel(const MmArgs a) {
     // s_barrier (no waitcnt: gfx950 barriers do not drain memory) between the two; without it the
     // late waves' activations queue in the CU's load path behind the early waves' weights, and
     // the workgroup's quantization barrier waits for them (single 4096 x 4096 Q4_K launch:
-    // activations in registers 1080 -> 720 ns after the wave's start, 5.96 -> 5.74 us)
-    if constexpr (!FUSE && !(MMVQ_EXP & 16)) asm volatile("s_barrier" ::: "memory");
+    // activations in registers 1080 -> 720 ns after the wave's start, 5.96 -> 5.74 us; batched
+    // launches within +-1 %, profiles/r06_mmvq_barrier_batched.txt). Not Q6_K: 24 stacked
+    // 4096 x 11008 matrices 167-169 us with it, 164-167 without.
+    if constexpr (!FUSE && T != T_Q6_K && !(MMVQ_EXP & 16)) asm volatile("s_barrier" ::: "memory");
     load_unit(fa, g, it);
     [[maybe_unused]] EpiOps ea{}, eb{};
     if constexpr (FUSE) ea = load_epi(g);
