@@ -68,9 +68,9 @@ std::string mmvq_plan_text(const MmArgs &a, int nc, int rpw);
 std::string mmvq_ring_plan_text(int type, const MmArgs &a, int nc, int rpw, bool pre);
 std::string mmvq_mma_plan_text(int type, const MmArgs &a);
 std::string mmq8_plan_text(const MmArgs &a);
-bool mmvq_solo_supported(const MmArgs &a);
+bool mmvq_solo_default(int type, const MmArgs &a);
 hipError_t mmvq_solo_launch(int type, const MmArgs &a, hipStream_t st);
-std::string mmvq_solo_plan_text(const MmArgs &a);
+std::string mmvq_solo_plan_text(int type, const MmArgs &a);
 
 // mat-mat kernel family: the int8 MFMA tile (csrc/mmq8.hip). It takes every K and every
 // 2-byte-aligned Q4_0 / Q8_0 / Q6_K layout (16-B aligned Q4_K / Q5_K) and is exact in the block
@@ -274,9 +274,9 @@ static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st
             nc = mmvq_bigk(m.K) ? 1 : std::min(ncols, 8);
             while (nc > 1 && (!mmvq_has_nc(nc) || mmvq_lds_bytes(m.K, nc) > LDS_LIMIT || m.K > mmvq_max_k_for_nc(nc))) --nc;
             g.M = nc;
-            const bool solo = nc == 1 && settings().solo > 0 && mmvq_solo_supported(g);
+            const bool solo = nc == 1 && mmvq_solo_default(type, g);
             if (plan) {
-                note(solo ? mmvq_solo_plan_text(g) : mmvq_plan_text(g, nc, nc == 1 ? rpw_one : rpw));
+                note(solo ? mmvq_solo_plan_text(type, g) : mmvq_plan_text(g, nc, nc == 1 ? rpw_one : rpw));
                 e = hipSuccess;
             } else if (solo) {
                 e = mmvq_solo_launch(type, g, st);

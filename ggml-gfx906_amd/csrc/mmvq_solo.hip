@@ -189,16 +189,28 @@ bool mmvq_solo_supported(const MmArgs &a) {
     return a.M == 1 && a.ne12 == 1 && a.ne13 == 1 && a.K % 64 == 0 && a.K >= 64 && a.K <= 4096;
 }
 
-int mmvq_solo_rows(const MmArgs &) { return settings().solo > 1 ? settings().solo : 4; }
+// the default (settings().solo < 0): from 4096 rows (>= 512 waves at 8 rows), where it was
+// measured against the 8-wave kernel (profiles/r06_solo_singles_ab.txt, rocprof means of single
+// launches, two rounds): 8 rows per wave Q4_0 4096^2 5.14-5.20 vs 5.33-5.39 us, Q4_K 4096^2
+// 5.30-5.32 vs 5.47-5.54, Q4_K / Q5_K x 11008 equal within noise; Q6_K x 11008 with 4 rows
+// 11.5-11.6 vs 12.7-13.0. Two rows per wave are 1.4-1.7x slower (the column is re-read per wave).
+bool mmvq_solo_default(int type, const MmArgs &a) {
+    const int s = settings().solo;
+    if (s == 0 || !mmvq_solo_supported(a)) return false;
+    return s > 0 || (a.N >= 4096 && type != T_Q8_0);
+}
 
-std::string mmvq_solo_plan_text(const MmArgs &a) {
-    const int r = mmvq_solo_rows(a);
+static int solo_rows_default(int type) { return type == T_Q6_K ? 4 : 8; }
+int mmvq_solo_rows(int type, const MmArgs &) { return settings().solo > 1 ? settings().solo : solo_rows_default(type); }
+
+std::string mmvq_solo_plan_text(int type, const MmArgs &a) {
+    const int r = mmvq_solo_rows(type, a);
     return "mmvq-solo rows=" + std::to_string(r) + " grid=" + std::to_string((a.N + r - 1) / r);
 }
 
 hipError_t mmvq_solo_launch(int type, const MmArgs &a, hipStream_t st) {
     if (!mmvq_solo_supported(a)) return hipErrorInvalidValue;
-    const int r = mmvq_solo_rows(a);
+    const int r = mmvq_solo_rows(type, a);
     switch (type) {
         case T_Q4_0: return solo_type<T_Q4_0>(a, r, st);
         case T_Q8_0: return solo_type<T_Q8_0>(a, r, st);

@@ -32,7 +32,7 @@ static Settings load_settings() {
     s.mma_pair = i("GGML_MI355X_MMA_PAIR", -1);
     s.mma_kh = i("GGML_MI355X_MMA_KH", 2);
     s.mma_rt = i("GGML_MI355X_MMA_RT", 0);
-    s.solo = i("GGML_MI355X_SOLO", 0);
+    s.solo = i("GGML_MI355X_SOLO", -1);
     s.mmq_repack_min = i("GGML_MI355X_MMQ_REPACK_MIN", 1 << 30);
     s.mmq_rp_all = i("GGML_MI355X_MMQ_RP_ALL", 0) == 1;
     s.mmq8_tt = i("GGML_MI355X_MMQ8_TT", 0);

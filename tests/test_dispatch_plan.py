@@ -32,15 +32,18 @@ def plan(t, K, N, cols, mats=1, repacked=False, addr=0x100000):
 # (name, type, K, N, columns, matrices per call) -> plan text
 PLANS = {
     # BASELINE configs[1] and the north-star shape: one matrix per launch, M = 1
-    ("q4_0", 4096, 4096, 1, 1): "mmvq nc=1 lpr=64 rpw=2 grid=256x1x1",
-    ("q4_K", 4096, 4096, 1, 1): "mmvq nc=1 lpr=64 rpw=2 grid=256x1x1",
+    ("q4_0", 4096, 4096, 1, 1): "mmvq-solo rows=8 grid=512",
+    ("q4_K", 4096, 4096, 1, 1): "mmvq-solo rows=8 grid=512",
+    ("q8_0", 4096, 4096, 1, 1): "mmvq nc=1 lpr=64 rpw=2 grid=256x1x1",
     # bench.py headline: 64 stacked matrices per MUL_MAT
     ("q4_0", 4096, 4096, 1, 64): "mmvq nc=1 lpr=64 rpw=2 grid=32x64x1",
     ("q4_K", 4096, 4096, 1, 64): "mmvq nc=1 lpr=64 rpw=2 grid=32x64x1",
     # BASELINE configs[2]: 4096 x 11008 k-quants, M = 1
-    ("q4_K", 4096, 11008, 1, 1): "mmvq nc=1 lpr=64 rpw=2 grid=688x1x1",
-    ("q5_K", 4096, 11008, 1, 1): "mmvq nc=1 lpr=64 rpw=2 grid=688x1x1",
-    ("q6_K", 4096, 11008, 1, 1): "mmvq nc=1 lpr=64 rpw=1 grid=1376x1x1",
+    ("q4_K", 4096, 11008, 1, 1): "mmvq-solo rows=8 grid=1376",
+    ("q5_K", 4096, 11008, 1, 1): "mmvq-solo rows=8 grid=1376",
+    ("q6_K", 4096, 11008, 1, 1): "mmvq-solo rows=4 grid=2752",
+    # below 4096 rows the 8-wave kernel (two rows per wave from 4096 rows on)
+    ("q4_K", 4096, 2048, 1, 1): "mmvq nc=1 lpr=64 rpw=1 grid=256x1x1",
     # BASELINE configs[3]: the int8 MFMA tile
     ("q8_0", 4096, 4096, 512, 1): "mmq8 tile=128x64 tiles=256 ksplit=1",
 }
