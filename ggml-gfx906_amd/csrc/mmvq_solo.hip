@@ -83,6 +83,10 @@ __global__ __launch_bounds__(WAVE) void mmvq_solo_kernel(const MmArgs a) {
     const uint8_t *wmat = a.w;
     const float *x = reinterpret_cast<const float *>(a.x);
     const int nblk = a.K / QT<T>::blck;
+    // diagnostics (GGML_MI355X_STAMPS): per wave start / activations in registers / quantized /
+    // end (s_memrealtime) and the shader clock (s_memtime), scripts/solo_stamps.py
+    unsigned long long *const st = a.stamps != nullptr && lane == 0 ? a.stamps + (int64_t)blockIdx.x * 8 : nullptr;
+    if (st) { st[0] = __builtin_amdgcn_s_memrealtime(); st[4] = __builtin_amdgcn_s_memtime(); }
 
     // ---- the slot's 64 activations first (four 16-value parts), then the R rows' weights
     float xv[4][16];
@@ -107,6 +111,11 @@ __global__ __launch_bounds__(WAVE) void mmvq_solo_kernel(const MmArgs a) {
 
     // ---- quantize the slot in registers: X[16] dwords in part order (parts 0..3 = the Frag's
     // j), dx / sx as Frag::dot expects them
+    if (st) {   // (the probe consumes this lane's first and last activation: all have landed)
+        float probe = xv[0][0] + xv[3][15];
+        asm volatile("" : "+v"(probe));
+        st[1] = __builtin_amdgcn_s_memrealtime() + (probe == 12345.f);
+    }
     uint32_t X[16];
     float dx[NX], sx[NX];
     if constexpr (T == T_Q6_K) {
@@ -151,6 +160,11 @@ __global__ __launch_bounds__(WAVE) void mmvq_solo_kernel(const MmArgs a) {
         }
     }
 
+    if (st) {
+        uint32_t probe = X[0] ^ X[15];
+        asm volatile("" : "+v"(probe));
+        st[2] = __builtin_amdgcn_s_memrealtime() + (probe == 12345u);
+    }
     // ---- dots and the cross-lane sum
     const float live = lane < nslots ? 1.f : 0.f;
     float acc[V];
@@ -162,6 +176,7 @@ __global__ __launch_bounds__(WAVE) void mmvq_solo_kernel(const MmArgs a) {
     constexpr int SHIFT = 6 - Log2<V>::v;
     const int idx = lane >> SHIFT;
     if ((lane & ((1 << SHIFT) - 1)) == 0 && idx < R && r0 + idx < a.N) reinterpret_cast<float *>(a.dst)[r0 + idx] = sum;
+    if (st) { st[3] = __builtin_amdgcn_s_memrealtime(); st[5] = __builtin_amdgcn_s_memtime(); }
 }
 
 template <int T, int R>
