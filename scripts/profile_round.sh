@@ -5,6 +5,11 @@
 #   scripts/profile_round.sh r02
 set -u
 R=${1:-r02}
+# PART=a: bench line, its rocprof profile and the PMC passes; PART=b: everything else (each part
+# fits one gpurun call); default both
+PART=${PART:-all}
+in_a() { [ "$PART" = all ] || [ "$PART" = a ]; }
+in_b() { [ "$PART" = all ] || [ "$PART" = b ]; }
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/prof_$R
 mkdir -p $O
@@ -27,6 +32,7 @@ squash() {  # squash <dir>
 }
 # the HBM floor probe (built here when the tree does not carry the binary)
 [ -x scripts/hbm_probe ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o scripts/hbm_probe scripts/hbm_probe.hip || exit 1
+if in_a; then
 [ -s $O/bench.log ] || step bench 600 python bench.py
 step prof_bench 600 $RP -d $O/bench -o run -- python bench.py --no-extra --cpu-seconds 1
 python scripts/rocprof_headline.py $(find $O/bench -name '*kernel_trace.csv' | head -1) $O/headline_rocprof.json $R profiles/${R}_bench_trace_summary.txt > /dev/null
@@ -38,6 +44,8 @@ squash $O/pmc_fetch
 step pmc_write 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_write -o pmc -- python bench.py --no-extra --no-gpt2 --cpu-seconds 1 --steps 5 --warmup 1
 python scripts/pmc_summary.py $O/pmc_write > $O/pmc_write_summary.txt
 squash $O/pmc_write
+fi
+if in_b; then
 step prof_singles 300 $RP -d $O/singles -o run -- python scripts/prof_singles.py
 squash $O/singles
 step prof_mmq 300 $RP -d $O/mmq -o run -- python scripts/mmq_bench.py q8_0:4096:4096:512 q4_K:4096:4096:512 q6_K:4096:11008:512 q4_K:4096:4096:32 q8_0:4096:4096:2048
@@ -54,5 +62,6 @@ step floor_stream 120 $RP -d $O/floor_stream -o run -- scripts/hbm_probe s
 squash $O/floor_stream
 step floor_mv 120 $RP -d $O/floor_mv -o run -- python scripts/prof_singles.py 128 q4_K:4096:64
 squash $O/floor_mv
+fi
 du -sh $O
 echo "=== done"
