@@ -33,6 +33,7 @@ hipError_t mmvq_ring_launch(int type, const MmArgs &a, int nc, int rpw, uint8_t 
 hipError_t mmvq_mma_launch(int type, const MmArgs &a, uint8_t *img, hipStream_t st);
 size_t mmvq_mma_img_bytes(int type, const MmArgs &a);
 bool mmvq_mma_supported(int type, const MmArgs &a);
+bool mmvq_mma_one_part(int type, const MmArgs &a);
 size_t mmvq_ring_img_bytes(const MmArgs &a, int nc);
 hipError_t dequant_launch(int type, const void *src, float *dst, int64_t n, hipStream_t st);
 struct RowsArgs {
@@ -193,31 +194,34 @@ static int ring_pre_min() {
 }
 
 // the int8 MFMA mat-vec (mmvq_mma.hip: the weights read once, the columns packed
-// block-diagonally into the MFMA's 16 columns, flat in the column count). From a sweep against
-// the per-column VALU kernels (profiles/r05_mma_sweep2.txt, r05_mma_k4096.txt: 5 shapes x 4 types x 3..8 columns,
-// single matrices), the first column count from which it is used:
-//   Q4_0  K >= 8192 or N >= 8192: 4 (paired steps, mmvq_mma.hip mma_plan)
-//   Q8_0  K >= 8192: 3; else N >= 8192: 5 (paired below K = 8192 and from 12288)
-// (K and N both below 8192, e.g. 4096 x 4096: within run-to-run noise of the VALU kernels at 5..6
-// columns and ~10 % slower at 8: VALU)
-//   Q4_K  K >= 8192: 3; else N >= 8192: 4; else 5
-//   Q5_K  K < 8192: 5; K < 12288: 3; else 8
-// (the K-quant rows from profiles/r05_mma_sweep3.txt, after their loads per step were halved);
-// everywhere else the VALU kernels are as fast or faster (0.56-0.99x where it is used).
-// GGML_MI355X_MMA=N: from N columns on for every type it takes; 0: never.
-static int mma_min_cols(int type, int K, int N, int slices) {
+// block-diagonally into the MFMA's 16 columns, flat in the column count) against the per-column
+// VALU kernels, from hipGraph periods of back-to-back calls (profiles/r06_mma_plan_sweep.txt:
+// 4 types x 10 shapes K x N from 4096 to 28672 x 3..8 columns, Infinity-Cache-cold weights; the
+// round-5 rule came from eager launches, host-bound at these sizes). Used from
+//   Q4_0  3 columns at K >= 11008, N >= 14336 or K, N >= 8192; else 4 at K or N >= 8192; else 5
+//   Q8_0  3 columns at K >= 11008; else 5
+//   Q4_K  3 at K >= 8192; else 4 at N >= 8192; else 5
+//   Q5_K  K < 8192: 5; to K = 16384 3 where the plan keeps one K part (its image fits the LDS;
+//         elsewhere the VALU kernels win up to 7 columns: 27.4 vs 28.8 us at 28672 x 4096), and 8
+// e.g. Q4_0 4096 x 4096 at 5..8 columns 8.4 vs 10.1-12.0 us, Q8_0 14336 x 4096 at 3..8 18.5 vs
+// 20.3-23.0, Q5_K 14336 x 4096 at 3..8 17.5 vs 18.5-22.3 (the plan's one-K-part forms,
+// profiles/r06_mma_plan_sweep.txt); everywhere else the VALU kernels are as fast or within 3 %. GGML_MI355X_MMA=N: from N columns on for every type it
+// takes; 0: never.
+static bool use_mma(int type, const MmArgs &g) {
+    const int K = g.K, N = g.N, cols = g.M;
     const int v = settings().mma;
-    if (v >= 0) return v == 0 ? 1 << 30 : v;
-    constexpr int NEVER = 1 << 30;
-    if (slices > 1) return NEVER;   // (8 batch slices: 2-4 % slower than the VALU kernels)
-    if (K < 4096) return NEVER;     // (outside the swept range; below 32 steps most of a workgroup's
+    if (v >= 0) return v != 0 && cols >= v;
+    if (g.ne12 * g.ne13 > 1) return false;   // (8 batch slices: 2-4 % slower than the VALU kernels)
+    if (K < 4096) return false;     // (outside the swept range; below 32 steps most of a workgroup's
                                     // 16 waves would idle, e.g. GPT-2's lm_head at K = 768)
     switch (type) {
-        case T_Q4_0: return K >= 8192 || N >= 8192 ? 4 : NEVER;
-        case T_Q8_0: return K >= 8192 ? 3 : N >= 8192 ? 5 : NEVER;
-        case T_Q4_K: return K >= 8192 ? 3 : N >= 8192 ? 4 : 5;
-        case T_Q5_K: return K < 8192 ? 5 : K < 12288 ? 3 : 8;
-        default: return NEVER;
+        case T_Q4_0:
+            if (K >= 11008 || N >= 14336 || (K >= 8192 && N >= 8192)) return cols >= 3;
+            return cols >= (K >= 8192 || N >= 8192 ? 4 : 5);
+        case T_Q8_0: return cols >= (K >= 11008 ? 3 : 5);
+        case T_Q4_K: return cols >= (K >= 8192 ? 3 : N >= 8192 ? 4 : 5);
+        case T_Q5_K: return K < 8192 ? cols >= 5 : cols >= 8 || (cols >= 3 && K <= 16384 && mmvq_mma_one_part(type, g));
+        default: return false;
     }
 }
 
@@ -233,11 +237,12 @@ static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st
         if (!plan->empty()) *plan += "; ";
         *plan += s;
     };
-    if (have_scratch && ncols >= mma_min_cols(type, m.K, m.N, m.ne12 * m.ne13) && ncols <= 8) {
-        MmArgs g = m;
-        g.x = m.x + (int64_t)c0 * m.nb11;
-        g.dst = m.dst + (int64_t)c0 * m.nb1;
-        g.M = ncols;
+    MmArgs gm = m;
+    gm.x = m.x + (int64_t)c0 * m.nb11;
+    gm.dst = m.dst + (int64_t)c0 * m.nb1;
+    gm.M = ncols;
+    if (have_scratch && ncols >= 1 && ncols <= 8 && use_mma(type, gm)) {
+        const MmArgs &g = gm;
         // (nullptr inside a capture that would grow the scratch: the kernels below take it)
         if (mmvq_mma_supported(type, g)) {
             if (plan) {

@@ -799,14 +799,52 @@ static bool mma_pair_aligned(int type, const MmArgs &a) {
     return a.nb01 == row && row % 4 == 0 && a.nb02 % 4 == 0 && a.nb03 % 4 == 0 && (reinterpret_cast<uintptr_t>(a.w) & 3) == 0;
 }
 
-// the launch plan (profiles/r05_mma_sweep2.txt, r05_mma_k4096.txt):
+// steps per wave: the smallest run that covers the part over the 16 waves (0: too long)
+static constexpr int MMA_RUNS[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14};
+static int mma_nstep(int part) {
+    for (int ns : MMA_RUNS)
+        if (MMA_KS * ns >= part) return ns;
+    return 0;
+}
+// the run mma_run launches for a part: pairs round it up to an even length (0: none fits)
+static int mma_run_len(int part, bool pr) {
+    const int ns = mma_nstep(part);
+    return pr && ns > 0 ? (ns + 1) & ~1 : ns;
+}
+
+// the column image of a part lives in LDS next to the kernel's static arrays (wsc: 4 KiB x RT x
+// scales per block, red: 1 KiB x RT x TOK), after which come the 128 zero bytes; 256 bytes of
+// slack for alignment
+static constexpr int mma_nsc(int type) { return type == T_Q4_K || type == T_Q5_K ? 2 : 1; }
+static constexpr int mma_lds_img(int nsc, int tok, int rt) { return 160 * 1024 - (4096 * nsc + 1024 * tok) * rt - 128 - 256; }
+
+// exactly the launcher's conditions for a part of `part` steps: a run for it, its image in LDS,
+// and the run's steps within the image mma_main accepts (paired runs of part 97..102 at 8
+// tokens, or 193..204 at 4, round past it with two tiles: e.g. Q4_0 K = 25600 at 5..8 columns,
+// Q4_K K = 49408 at 3)
+static bool mma_part_fits(int type, const MmArgs &a, int part, bool pr, int rt) {
+    const int ns = mma_run_len(part, pr), tok = mma_tok_of(a), sb = tok * 160;   // mma_step_bytes<TOK>()
+    const int img = mma_lds_img(mma_nsc(type), tok, rt);
+    return ns > 0 && part * sb <= img && MMA_KS * ns * sb <= img + 16 * sb;
+}
+
+// the launch plan, from hipGraph periods of back-to-back calls (scripts/mv_graph.py through
+// scripts/mv_sweep.sh: 4 types x 10 shapes x 3..8 columns, weights Infinity-Cache-cold and warm,
+// profiles/r06_mma_plan_sweep.txt; round 5 chose from eager launches, whose period the host's
+// launch rate bounded):
 //   pr  paired steps: Q4_0 always, Q8_0 below K = 8192 and from 12288 (at 11008 the unpaired
 //       form with two tiles wins), where the rows allow it;
-//   kh  K parts: 2 when each part keeps >= 32 steps for pairs (every wave a pair; at K = 4096 two
-//       parts would idle half the waves), >= 16 unpaired (from K = 4096);
-//   rt  16-row tiles per workgroup: Q5_K and Q8_0 pairs 1 (registers); unsplit Q4_0 pairs 2 from
-//       N = 12288 (enough workgroups), else 1; otherwise 2.
-// GGML_MI355X_MMA_PAIR / _KH / _RT force (measurements; _KH=1 and _RT=1/2 as before)
+//   kh  one K part wherever the whole column image fits the workgroup's LDS: 0.85-0.95x the
+//       two-part time (no dst zeroing in the pre-pass, no atomic adds, a wave walks twice the
+//       steps); two parts only for images that do not fit (e.g. Q4_0 at 5..8 columns from K =
+//       15104 with one tile, 13184 with two),
+//       as before where each part keeps >= 32 steps for pairs, >= 16 unpaired, and for Q5_K with
+//       K and N below 8192 (one tile per workgroup: 512 two-part workgroups beat 256);
+//   rt  16-row tiles per workgroup: Q5_K and Q8_0 pairs 1 (registers); with one K part 2 when
+//       N >= 8192 at K >= 8192, or N >= 12288, else 1 (one tile per workgroup doubles the
+//       workgroups: Q8_0 11008 x 4096 15.6 vs 23.3 us with two); with two parts 2.
+// GGML_MI355X_MMA_PAIR / _KH / _RT force (measurements: _KH=1 one part, =2 two parts where the
+// steps allow; _RT=1/2)
 struct MmaPlan {
     int kh, rt;
     bool pr;
@@ -817,41 +855,25 @@ static MmaPlan mma_plan(int type, const MmArgs &a) {
     const int pe = settings().mma_pair;
     const bool want = pe >= 0 ? pe == 1 : (type == T_Q4_0 || (type == T_Q8_0 && (a.K < 8192 || a.K >= 12288)));
     p.pr = want && mma_pair_aligned(type, a);
-    p.kh = (p.pr ? S >= 64 : S >= 32) && settings().mma_kh != 1 ? 2 : 1;
-    const int re = settings().mma_rt;
-    if (type == T_Q5_K || (type == T_Q8_0 && p.pr)) p.rt = 1;
-    else if (re == 1 || re == 2) p.rt = re;
-    else if (p.pr && p.kh == 1) p.rt = a.N >= 12288 ? 2 : 1;
-    else p.rt = 2;
+    const bool two_ok = p.pr ? S >= 64 : S >= 32;
+    const int ke = settings().mma_kh, re = settings().mma_rt;
+    auto rt_of = [&](int want) { return type == T_Q5_K || (type == T_Q8_0 && p.pr) ? 1 : re == 1 || re == 2 ? re : want; };
+    const int rt1 = rt_of((a.N >= 8192 && a.K >= 8192) || a.N >= 12288 ? 2 : 1);
+    if (ke == 1) p.kh = 1;
+    else if (ke == 2) p.kh = two_ok ? 2 : 1;
+    else if (type == T_Q5_K && a.K < 8192 && a.N < 8192) p.kh = two_ok ? 2 : 1;   // (one tile per workgroup: 512 beat 256)
+    else p.kh = two_ok && !mma_part_fits(type, a, S, p.pr, rt1) ? 2 : 1;
+    p.rt = p.kh == 1 ? rt1 : rt_of(2);
     return p;
 }
 
-// steps per wave: the smallest run that covers the part over the 16 waves (0: too long)
-static constexpr int MMA_RUNS[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14};
-static int mma_nstep(int part) {
-    for (int ns : MMA_RUNS)
-        if (MMA_KS * ns >= part) return ns;
-    return 0;
-}
-// the column image of a part lives in LDS next to the kernel's static arrays (<= 32 KB)
-constexpr int MMA_LDS_IMG = 160 * 1024 - 32 * 1024 - 128;
+// the plan keeps the K range in one part (dispatch.cpp use_mma)
+bool mmvq_mma_one_part(int type, const MmArgs &a) { return mma_plan(type, a).kh == 1; }
 
-// the run mma_run launches for a part: pairs round it up to an even length (0: none fits)
-static int mma_run_len(int part, bool pr) {
-    const int ns = mma_nstep(part);
-    return pr && ns > 0 ? (ns + 1) & ~1 : ns;
-}
-
-// exactly the launcher's conditions: a run for the part, the part's image in LDS, and the run's
-// steps within the image mma_main accepts (paired runs of part 97..102 at 8 tokens, or 193..204
-// at 4, round past it: e.g. Q4_0 K = 25600 at 5..8 columns, Q4_K K = 49408 at 3)
 bool mmvq_mma_supported(int type, const MmArgs &a) {
     if (!(type == T_Q4_0 || type == T_Q8_0 || type == T_Q4_K || type == T_Q5_K) || a.M < 1 || a.M > 8) return false;
     const MmaPlan pl = mma_plan(type, a);
-    const int part = mma_part_steps(a, pl.kh);
-    const int ns = mma_run_len(part, pl.pr);
-    const int sb = mma_tok_of(a) * 160;   // mma_step_bytes<TOK>()
-    return ns > 0 && part * sb <= MMA_LDS_IMG && MMA_KS * ns * sb <= MMA_LDS_IMG + 16 * sb;
+    return mma_part_fits(type, a, mma_part_steps(a, pl.kh), pl.pr, pl.rt);
 }
 
 // the launch mma_tok makes (the dispatch description, ggml_mi355x_mul_mat_plan)
@@ -870,7 +892,8 @@ size_t mmvq_mma_img_bytes(int, const MmArgs &a) {
 
 template <int T, int TOK, int RT, int NS, bool PR>
 static hipError_t mma_main(const MmArgs &a, const uint8_t *img, int S, int part, int kh, hipStream_t st) {
-    if constexpr (MMA_KS * NS * mma_step_bytes<TOK>() > MMA_LDS_IMG + 16 * mma_step_bytes<TOK>()) {
+    constexpr int IMG = mma_lds_img(MmaW<T, TOK>::NSC, TOK, RT);
+    if constexpr (MMA_KS * NS * mma_step_bytes<TOK>() > IMG + 16 * mma_step_bytes<TOK>()) {
         return hipErrorInvalidValue;   // (runs whose image cannot fit: never selected)
     } else {
         auto kern = mmvq_mma_kernel<T, TOK, RT, NS, PR>;
@@ -907,7 +930,8 @@ static hipError_t mma_tok(const MmArgs &a, uint8_t *img, hipStream_t st) {
     const MmaPlan pl = mma_plan(T, a);
     const int S = mma_steps(a), kh = pl.kh, part = mma_part_steps(a, kh);
     const dim3 pg(S, a.ne12 * a.ne13);
-    if (a.x_aligned16) hipLaunchKernelGGL((mma_prequant<TOK, true>), pg, dim3(TOK * 16), 0, st, a, img, kh == 2);
+    if (settings().diag & 256) {   // (measurement: no pre-pass)
+    } else if (a.x_aligned16) hipLaunchKernelGGL((mma_prequant<TOK, true>), pg, dim3(TOK * 16), 0, st, a, img, kh == 2);
     else hipLaunchKernelGGL((mma_prequant<TOK, false>), pg, dim3(TOK * 16), 0, st, a, img, kh == 2);
     hipError_t e;
     if constexpr (T == T_Q5_K) e = mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);

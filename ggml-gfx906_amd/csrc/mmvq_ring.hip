@@ -417,7 +417,7 @@ static hipError_t ring_one(const MmArgs &a0, uint8_t *img, hipStream_t st) {
     const int want = (int)std::max<int64_t>(1, target / ((int64_t)grid_y * grid_z));
     const dim3 grid(std::min(n_groups, want), grid_y, grid_z);
     if constexpr (PRE) {   // one column group per launch (grid_z == 1): quantized once, then the mat-vec
-        hipLaunchKernelGGL((mmvq_prequant<T, XA, NC>), dim3(a.n_it, NC, grid_y), dim3(512), 0, st, a, img);
+        if (!(settings().diag & 256)) hipLaunchKernelGGL((mmvq_prequant<T, XA, NC>), dim3(a.n_it, NC, grid_y), dim3(512), 0, st, a, img);
         if (d3) hipLaunchKernelGGL((mmvq_ring_pre_kernel<T, NC, RPW, RAG, WAVES, D>), grid, dim3(THREADS), lds, st, a, (const uint8_t *)img);
         else hipLaunchKernelGGL((mmvq_ring_pre_kernel<T, NC, RPW, RAG, WAVES, 2>), grid, dim3(THREADS), lds, st, a, (const uint8_t *)img);
     } else {

@@ -30,7 +30,7 @@ static Settings load_settings() {
     s.ring_wgs = l("GGML_MI355X_RING_WGS", 0);
     s.mma = i("GGML_MI355X_MMA", -1);
     s.mma_pair = i("GGML_MI355X_MMA_PAIR", -1);
-    s.mma_kh = i("GGML_MI355X_MMA_KH", 2);
+    s.mma_kh = i("GGML_MI355X_MMA_KH", 0);
     s.mma_rt = i("GGML_MI355X_MMA_RT", 0);
     s.solo = i("GGML_MI355X_SOLO", -1);
     s.mmq_repack_min = i("GGML_MI355X_MMQ_REPACK_MIN", 1 << 30);

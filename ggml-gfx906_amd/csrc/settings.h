@@ -22,7 +22,7 @@ struct Settings {
     int64_t ring_wgs = 0;         // GGML_MI355X_RING_WGS: grid of the chunked kernel (0 = one round)
     int mma = -1;                 // GGML_MI355X_MMA: MFMA mat-vec from N columns (0 never, -1 rule)
     int mma_pair = -1;            // GGML_MI355X_MMA_PAIR: 0/1 force unpaired / paired steps (-1 plan)
-    int mma_kh = 2;               // GGML_MI355X_MMA_KH: 1 = one K part
+    int mma_kh = 0;               // GGML_MI355X_MMA_KH: 1 / 2 force one / two K parts (0 plan)
     int mma_rt = 0;               // GGML_MI355X_MMA_RT: 1/2 row tiles per workgroup (0 plan)
     int solo = -1;                // GGML_MI355X_SOLO: single-wave kernel for one column (-1 rule, 0 off, 1 on, n rows per wave)
     // ---- mat-mat (ne11 > 8)
@@ -53,7 +53,8 @@ struct Settings {
     // ---- diagnostics
     bool stamps = false;          // GGML_MI355X_STAMPS: per-workgroup s_memrealtime stamps
     int stamp_mv = -1;            // GGML_MI355X_STAMP_MV: which fused mat-vec of a step to stamp
-    int diag = 0;                 // GGML_MI355X_DIAG
+    int diag = 0;                 // GGML_MI355X_DIAG (measurements; results wrong): bit 0 no activation loads,
+                                  // bit 1 no weight loads, bit 8 (256) no mat-vec column pre-pass launch
 };
 
 // the current snapshot (the first call reads the environment)

@@ -51,31 +51,31 @@ PLANS = {
 PERF = {
     ("q4_0", 1): "ring nc=1 rpw=1 cols=1",
     ("q4_0", 2): "ring nc=2 rpw=1 cols=2",
-    ("q4_0", 3): "ring-pre nc=4 rpw=1 cols=3",
-    ("q4_0", 4): "mma tok=4 kh=2 rt=2 paired run=4 cols=4",
-    ("q4_0", 5): "mma tok=8 kh=2 rt=2 paired run=4 cols=5",
-    ("q4_0", 8): "mma tok=8 kh=2 rt=2 paired run=4 cols=8",
+    ("q4_0", 3): "mma tok=4 kh=1 rt=1 paired run=8 cols=3",
+    ("q4_0", 4): "mma tok=4 kh=1 rt=1 paired run=8 cols=4",
+    ("q4_0", 5): "mma tok=8 kh=1 rt=1 paired run=8 cols=5",
+    ("q4_0", 8): "mma tok=8 kh=1 rt=1 paired run=8 cols=8",
     ("q4_0", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
     ("q8_0", 1): "ring nc=1 rpw=1 cols=1",
     ("q8_0", 2): "ring nc=2 rpw=1 cols=2",
-    ("q8_0", 3): "mma tok=4 kh=2 rt=1 paired run=4 cols=3",
-    ("q8_0", 4): "mma tok=4 kh=2 rt=1 paired run=4 cols=4",
-    ("q8_0", 5): "mma tok=8 kh=2 rt=1 paired run=4 cols=5",
-    ("q8_0", 8): "mma tok=8 kh=2 rt=1 paired run=4 cols=8",
+    ("q8_0", 3): "mma tok=4 kh=1 rt=1 paired run=8 cols=3",
+    ("q8_0", 4): "mma tok=4 kh=1 rt=1 paired run=8 cols=4",
+    ("q8_0", 5): "mma tok=8 kh=1 rt=1 paired run=8 cols=5",
+    ("q8_0", 8): "mma tok=8 kh=1 rt=1 paired run=8 cols=8",
     ("q8_0", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
     ("q4_K", 1): "ring nc=1 rpw=1 cols=1",
     ("q4_K", 2): "ring nc=2 rpw=1 cols=2",
-    ("q4_K", 3): "mma tok=4 kh=2 rt=2 run=4 cols=3",
-    ("q4_K", 4): "mma tok=4 kh=2 rt=2 run=4 cols=4",
-    ("q4_K", 5): "mma tok=8 kh=2 rt=2 run=4 cols=5",
-    ("q4_K", 8): "mma tok=8 kh=2 rt=2 run=4 cols=8",
+    ("q4_K", 3): "mma tok=4 kh=1 rt=1 run=7 cols=3",
+    ("q4_K", 4): "mma tok=4 kh=1 rt=1 run=7 cols=4",
+    ("q4_K", 5): "mma tok=8 kh=1 rt=1 run=7 cols=5",
+    ("q4_K", 8): "mma tok=8 kh=1 rt=1 run=7 cols=8",
     ("q4_K", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
     ("q5_K", 1): "ring nc=1 rpw=1 cols=1",
     ("q5_K", 2): "ring nc=2 rpw=1 cols=2",
-    ("q5_K", 3): "ring-pre nc=4 rpw=1 cols=3",
-    ("q5_K", 4): "ring-pre nc=4 rpw=1 cols=4",
-    ("q5_K", 5): "ring-pre nc=8 rpw=1 cols=5",
-    ("q5_K", 8): "mma tok=8 kh=2 rt=1 run=4 cols=8",
+    ("q5_K", 3): "mma tok=4 kh=1 rt=1 run=7 cols=3",
+    ("q5_K", 4): "mma tok=4 kh=1 rt=1 run=7 cols=4",
+    ("q5_K", 5): "mma tok=8 kh=1 rt=1 run=7 cols=5",
+    ("q5_K", 8): "mma tok=8 kh=1 rt=1 run=7 cols=8",
     ("q5_K", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
     ("q6_K", 1): "ring nc=1 rpw=1 cols=1",
     ("q6_K", 2): "ring nc=2 rpw=1 cols=2",
@@ -85,6 +85,34 @@ PERF = {
     ("q6_K", 8): "ring-pre nc=8 rpw=1 cols=8",
     ("q6_K", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
 }
+
+
+# the MFMA mat-vec rule's branches (dispatch.cpp use_mma, mmvq_mma.hip mma_plan; round-6 graph
+# sweep profiles/r06_mma_plan_sweep.txt): (name, K, N, columns) -> plan text
+MMA_RULE = {
+    ("q4_0", 4096, 4096, 4): "mmvq nc=4 lpr=64 rpw=1 grid=512x1x1",           # small: VALU up to 4
+    ("q4_0", 4096, 4096, 5): "mma tok=8 kh=1 rt=1 paired run=2 cols=5",       # one K part, one tile
+    ("q4_0", 8192, 8192, 3): "mma tok=4 kh=1 rt=2 paired run=4 cols=3",       # two tiles at N, K >= 8192
+    ("q4_0", 4096, 14336, 8): "mma tok=8 kh=1 rt=2 paired run=2 cols=8",      # two tiles at N >= 12288
+    ("q8_0", 11008, 4096, 3): "mma tok=4 kh=1 rt=1 run=6 cols=3",             # unpaired, one tile
+    ("q8_0", 8192, 4096, 4): "ring-pre nc=4 rpw=1 cols=4",                    # K < 11008: from 5
+    ("q8_0", 8192, 4096, 5): "mma tok=8 kh=1 rt=1 run=4 cols=5",
+    ("q4_K", 4096, 14336, 8): "mma tok=8 kh=1 rt=2 run=2 cols=8",
+    ("q4_K", 14336, 4096, 8): "mma tok=8 kh=1 rt=1 run=7 cols=8",             # one tile: one part fits
+    ("q4_K", 24576, 4096, 8): "mma tok=8 kh=2 rt=2 run=6 cols=8",             # image past LDS: two parts
+    ("q4_K", 28672, 4096, 8): "ring-pre nc=8 rpw=1 cols=8",                   # no part size fits: VALU
+    ("q5_K", 4096, 4096, 5): "mma tok=8 kh=2 rt=1 run=1 cols=5",              # Q5_K small: two parts
+    ("q5_K", 8192, 4096, 5): "mma tok=8 kh=1 rt=1 run=4 cols=5",
+    ("q5_K", 14336, 4096, 3): "mma tok=4 kh=1 rt=1 run=7 cols=3",
+    ("q5_K", 14336, 4096, 5): "mma tok=8 kh=1 rt=1 run=7 cols=5",
+    ("q5_K", 28672, 4096, 3): "ring-pre nc=4 rpw=1 cols=3",                   # past K = 16384: VALU to 7
+}
+
+
+def test_mma_rule(lib):
+    for (name, K, N, cols), want in MMA_RULE.items():
+        got = plan(TYPES[name], K, N, cols)
+        assert got == want, f"{name} K={K} N={N} cols={cols}: {got!r}"
 
 
 def test_baseline_shapes(lib):
@@ -130,9 +158,11 @@ def test_settings_reload(lib):
 
 
 def test_mma_refused_shapes_take_valu(lib):
-    """paired Q4_0 at K = 25600 with 5..8 columns and Q4_K at K = 49408 with 3
-    columns would need an MFMA run longer than the launcher's LDS image: the plan must not pick
-    the MFMA mat-vec there (the launcher would refuse it)"""
+    """paired Q4_0 at K = 25600 with 5..8 columns and Q4_K past K = 55296 with 3
+    columns would need an MFMA run longer than the launcher's LDS image (since round 6 sized per
+    instantiation: its static arrays, 12-32 KB, are what the image cannot use): the plan must
+    not pick the MFMA mat-vec there (the launcher would refuse it)"""
     assert not plan(M.Q4_0, 25600, 4096, 5).startswith("mma")
-    assert not plan(M.Q4_K, 49408, 4096, 3).startswith("mma")
+    assert not plan(M.Q4_K, 55552, 4096, 3).startswith("mma")
+    assert plan(M.Q4_K, 55296, 4096, 3).startswith("mma")
     assert plan(M.Q4_0, 24576, 4096, 5).startswith("mma")   # (just below: still taken)

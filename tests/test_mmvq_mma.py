@@ -95,12 +95,14 @@ def test_mma_partial_step_padded_rows(mm, t, K):
     assert qref.nmse(got, G.oracle_mul_mat(a, b, out_ne)) <= 5e-4
 
 
-@pytest.mark.parametrize("t,M_,K", [(qref.Q4_0, 5, 25600), (qref.Q4_K, 3, 49408), (qref.Q4_0, 8, 25600)])
+@pytest.mark.parametrize("t,M_,K", [(qref.Q4_0, 5, 25600), (qref.Q4_K, 3, 49408), (qref.Q4_K, 3, 55296), (qref.Q4_K, 3, 55552),
+                                    (qref.Q4_0, 8, 25600), (qref.Q8_0, 8, 14336), (qref.Q5_K, 5, 14336)])
 def test_mma_rule_shapes_past_the_image(mm, t, M_, K):
-    """the default rule takes these column counts at these K, but the MFMA run
-    the launcher would need (paired runs rounded up to even, 14 steps at 4 tokens) does not fit
-    its LDS image; mmvq_mma_supported now says so and the call runs on the VALU kernels instead
-    of failing (tests/test_dispatch_plan.py pins the choice)"""
+    """at the edges of the LDS image (paired runs rounded up to even, 14 steps
+    at 4 tokens; since round 6 the image is what the instantiation's static arrays leave, so the
+    one-part plans of K = 14336 at 8 tokens and the two-part run of Q4_K K = 55296 fit while
+    K = 55552 does not) the plan and the launcher agree: the MFMA kernel where it fits, the VALU
+    kernels elsewhere, never a failed launch (tests/test_dispatch_plan.py pins the choices)"""
     a, b, out_ne = operands(t, 64, M_, K, 21)
     got = run_mul_mat(mm, a, b, out_ne)
     assert np.all(np.isfinite(got))
