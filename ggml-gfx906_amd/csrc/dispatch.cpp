@@ -114,13 +114,23 @@ bool is_hot_quant(int t) { return type_blck(t) != 0; }
 // Q6_K keeps one row per wave: its two-row kernel needs 133 VGPRs, which leaves one 8-wave
 // workgroup per CU instead of two (Q6_K 4096x11008 x24: 169 vs 178 us, profiles/r03_q6k_rpw.txt;
 // single 4096 x 11008: 13.5-13.8 vs 12.6-12.8 us, profiles/r06_singles_ab.txt).
-// one_col: the rule above is for single-column launches of the whole-K kernel (what was
-// measured); column groups and the chunked-K kernels (mmvq_ring.hip) keep round 5's switch at
-// 16384 rows.
-static int pick_rpw(int type, int64_t rows_total, bool one_col) {
+// Round 6, from hipGraph periods of back-to-back calls (profiles/r06_valu_plan_sweep.txt; the
+// rule above came from rocprof kernel durations): two rows from 4096 rows also for the whole-K
+// kernel's groups of 2..4 columns (Q4_0 4096^2 at 4 columns 5.7 vs 7.0 us, Q4_K 4096 x 11008 at 3
+// 12.9 vs 14.4) and for the chunked-K kernel's column pairs (Q4_K 14336 x 4096 at 2 columns 11.5
+// vs 12.9, Q4_0 4096 x 11008 9.5 vs 10.8); its single columns only for Q4_K / Q5_K (Q4_K 14336 x
+// 4096 9.4 vs 10.1; Q8_0 there 14.2 vs 13.6 with one row); its groups of 4 / 8 columns keep the
+// switch at 16384 rows (Q6_K 4096 x 14336 at 3 columns 22.9 vs 20.5 with two); Q8_0 / Q5_K groups
+// of 3..4 columns keep one row from 12288 rows (Q5_K 4096 x 14336 at 3 columns 20.2 vs 18.9).
+static int pick_rpw(int type, int64_t rows_total, int nc, bool ring) {
     if (settings().rpw > 0) return settings().rpw;
     if (type == T_Q6_K) return 1;
-    return rows_total >= (one_col ? 4096 : 16384) ? 2 : 1;
+    if (ring) {
+        if (nc == 1) return (type == T_Q4_K || type == T_Q5_K) && rows_total >= 4096 ? 2 : 1;
+        return rows_total >= (nc == 2 ? 4096 : 16384) ? 2 : 1;
+    }
+    if (nc >= 3 && nc <= 4 && (type == T_Q8_0 || type == T_Q5_K) && rows_total >= 12288) return 1;
+    return rows_total >= (nc <= 4 ? 4096 : 16384) ? 2 : 1;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -231,7 +241,6 @@ static bool use_mma(int type, const MmArgs &g) {
 static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st, Scratch *scratch = nullptr,
                            std::string *plan = nullptr) {
     const int64_t rows_total = (int64_t)m.N * m.ne12 * m.ne13;
-    const int rpw = pick_rpw(type, rows_total, false), rpw_one = pick_rpw(type, rows_total, true);
     const bool have_scratch = scratch != nullptr || plan != nullptr;
     auto note = [&](const std::string &s) {
         if (!plan->empty()) *plan += "; ";
@@ -267,12 +276,12 @@ static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st
             g.M = take;
             uint8_t *img = nullptr;
             if (plan) {
-                note(mmvq_ring_plan_text(type, g, nc, rpw, nc >= ring_pre_min()));
+                note(mmvq_ring_plan_text(type, g, nc, pick_rpw(type, rows_total, nc, true), nc >= ring_pre_min()));
                 e = hipSuccess;
             } else {
                 if (nc >= ring_pre_min() && scratch != nullptr)   // (nullptr inside a capture that would grow it)
                     img = static_cast<uint8_t *>(scratch->get(mmvq_ring_img_bytes(g, nc), st));
-                e = mmvq_ring_launch(type, g, nc, rpw, img, st);
+                e = mmvq_ring_launch(type, g, nc, pick_rpw(type, rows_total, nc, true), img, st);
             }
             nc = take;
         } else {
@@ -281,12 +290,12 @@ static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st
             g.M = nc;
             const bool solo = nc == 1 && mmvq_solo_default(type, g);
             if (plan) {
-                note(solo ? mmvq_solo_plan_text(type, g) : mmvq_plan_text(g, nc, nc == 1 ? rpw_one : rpw));
+                note(solo ? mmvq_solo_plan_text(type, g) : mmvq_plan_text(g, nc, pick_rpw(type, rows_total, nc, false)));
                 e = hipSuccess;
             } else if (solo) {
                 e = mmvq_solo_launch(type, g, st);
             } else {
-                e = mmvq_launch(type, g, nc, nc == 1 ? rpw_one : rpw, st);
+                e = mmvq_launch(type, g, nc, pick_rpw(type, rows_total, nc, false), st);
             }
         }
         if (e != hipSuccess) return e;

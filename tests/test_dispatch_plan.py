@@ -31,9 +31,10 @@ def plan(t, K, N, cols, mats=1, repacked=False, addr=0x100000):
 
 # (name, type, K, N, columns, matrices per call) -> plan text
 PLANS = {
-    # BASELINE configs[1] and the north-star shape: one matrix per launch, M = 1
-    ("q4_0", 4096, 4096, 1, 1): "mmvq-solo rows=8 grid=512",
-    ("q4_K", 4096, 4096, 1, 1): "mmvq-solo rows=8 grid=512",
+    # BASELINE configs[1] and the north-star shape: one matrix per launch, M = 1 (graph periods
+    # put the 8-wave kernel ahead of the single-wave one at 4096 rows, mmvq_solo.hip)
+    ("q4_0", 4096, 4096, 1, 1): "mmvq nc=1 lpr=64 rpw=2 grid=256x1x1",
+    ("q4_K", 4096, 4096, 1, 1): "mmvq nc=1 lpr=64 rpw=2 grid=256x1x1",
     ("q8_0", 4096, 4096, 1, 1): "mmvq nc=1 lpr=64 rpw=2 grid=256x1x1",
     # bench.py headline: 64 stacked matrices per MUL_MAT
     ("q4_0", 4096, 4096, 1, 64): "mmvq nc=1 lpr=64 rpw=2 grid=32x64x1",
@@ -50,28 +51,28 @@ PLANS = {
 # test-backend-ops perf (tests/test-backend-ops.cpp:6195-6202): K = 14336, N = 4096, (type, bs)
 PERF = {
     ("q4_0", 1): "ring nc=1 rpw=1 cols=1",
-    ("q4_0", 2): "ring nc=2 rpw=1 cols=2",
+    ("q4_0", 2): "ring nc=2 rpw=2 cols=2",
     ("q4_0", 3): "mma tok=4 kh=1 rt=1 paired run=8 cols=3",
     ("q4_0", 4): "mma tok=4 kh=1 rt=1 paired run=8 cols=4",
     ("q4_0", 5): "mma tok=8 kh=1 rt=1 paired run=8 cols=5",
     ("q4_0", 8): "mma tok=8 kh=1 rt=1 paired run=8 cols=8",
     ("q4_0", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
     ("q8_0", 1): "ring nc=1 rpw=1 cols=1",
-    ("q8_0", 2): "ring nc=2 rpw=1 cols=2",
+    ("q8_0", 2): "ring nc=2 rpw=2 cols=2",
     ("q8_0", 3): "mma tok=4 kh=1 rt=1 paired run=8 cols=3",
     ("q8_0", 4): "mma tok=4 kh=1 rt=1 paired run=8 cols=4",
     ("q8_0", 5): "mma tok=8 kh=1 rt=1 paired run=8 cols=5",
     ("q8_0", 8): "mma tok=8 kh=1 rt=1 paired run=8 cols=8",
     ("q8_0", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
-    ("q4_K", 1): "ring nc=1 rpw=1 cols=1",
-    ("q4_K", 2): "ring nc=2 rpw=1 cols=2",
+    ("q4_K", 1): "ring nc=1 rpw=2 cols=1",
+    ("q4_K", 2): "ring nc=2 rpw=2 cols=2",
     ("q4_K", 3): "mma tok=4 kh=1 rt=1 run=7 cols=3",
     ("q4_K", 4): "mma tok=4 kh=1 rt=1 run=7 cols=4",
     ("q4_K", 5): "mma tok=8 kh=1 rt=1 run=7 cols=5",
     ("q4_K", 8): "mma tok=8 kh=1 rt=1 run=7 cols=8",
     ("q4_K", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
-    ("q5_K", 1): "ring nc=1 rpw=1 cols=1",
-    ("q5_K", 2): "ring nc=2 rpw=1 cols=2",
+    ("q5_K", 1): "ring nc=1 rpw=2 cols=1",
+    ("q5_K", 2): "ring nc=2 rpw=2 cols=2",
     ("q5_K", 3): "mma tok=4 kh=1 rt=1 run=7 cols=3",
     ("q5_K", 4): "mma tok=4 kh=1 rt=1 run=7 cols=4",
     ("q5_K", 5): "mma tok=8 kh=1 rt=1 run=7 cols=5",
@@ -90,7 +91,7 @@ PERF = {
 # the MFMA mat-vec rule's branches (dispatch.cpp use_mma, mmvq_mma.hip mma_plan; round-6 graph
 # sweep profiles/r06_mma_plan_sweep.txt): (name, K, N, columns) -> plan text
 MMA_RULE = {
-    ("q4_0", 4096, 4096, 4): "mmvq nc=4 lpr=64 rpw=1 grid=512x1x1",           # small: VALU up to 4
+    ("q4_0", 4096, 4096, 4): "mmvq nc=4 lpr=64 rpw=2 grid=256x1x1",           # small: VALU up to 4
     ("q4_0", 4096, 4096, 5): "mma tok=8 kh=1 rt=1 paired run=2 cols=5",       # one K part, one tile
     ("q4_0", 8192, 8192, 3): "mma tok=4 kh=1 rt=2 paired run=4 cols=3",       # two tiles at N, K >= 8192
     ("q4_0", 4096, 14336, 8): "mma tok=8 kh=1 rt=2 paired run=2 cols=8",      # two tiles at N >= 12288
