@@ -208,9 +208,11 @@ static int ring_pre_min() {
 // VALU kernels, from hipGraph periods of back-to-back calls (profiles/r06_mma_plan_sweep.txt:
 // 4 types x 10 shapes K x N from 4096 to 28672 x 3..8 columns, Infinity-Cache-cold weights; the
 // round-5 rule came from eager launches, host-bound at these sizes). Used from
-//   Q4_0  3 columns at K >= 11008, N >= 14336 or K, N >= 8192; else 4 at K or N >= 8192; else 5
+//   Q4_0  K < 8192: 5; else 3 at K >= 11008 or N >= 8192, else 4
 //   Q8_0  3 columns at K >= 11008; else 5
-//   Q4_K  3 at K >= 8192; else 4 at N >= 8192; else 5
+//   Q4_K  3 at K >= 8192; else 5
+// (below K = 8192 the whole-K VALU kernel with 16-lane rows, mmvq.hip lanes_per_row, takes 3..4
+// columns: Q4_0 4096 x 14336 at 3 10.6 vs 14.7 us, Q4_K at 4 12.5 vs 17.2)
 //   Q5_K  K < 8192: 5; to K = 16384 3 where the plan keeps one K part (its image fits the LDS;
 //         elsewhere the VALU kernels win up to 7 columns: 27.4 vs 28.8 us at 28672 x 4096), and 8
 // e.g. Q4_0 4096 x 4096 at 5..8 columns 8.4 vs 10.1-12.0 us, Q8_0 14336 x 4096 at 3..8 18.5 vs
@@ -226,10 +228,10 @@ static bool use_mma(int type, const MmArgs &g) {
                                     // 16 waves would idle, e.g. GPT-2's lm_head at K = 768)
     switch (type) {
         case T_Q4_0:
-            if (K >= 11008 || N >= 14336 || (K >= 8192 && N >= 8192)) return cols >= 3;
-            return cols >= (K >= 8192 || N >= 8192 ? 4 : 5);
+            if (K < 8192) return cols >= 5;
+            return cols >= (K >= 11008 || N >= 8192 ? 3 : 4);
         case T_Q8_0: return cols >= (K >= 11008 ? 3 : 5);
-        case T_Q4_K: return cols >= (K >= 8192 ? 3 : N >= 8192 ? 4 : 5);
+        case T_Q4_K: return cols >= (K >= 8192 ? 3 : 5);
         case T_Q5_K: return K < 8192 ? cols >= 5 : cols >= 8 || (cols >= 3 && K <= 16384 && mmvq_mma_one_part(type, g));
         default: return false;
     }

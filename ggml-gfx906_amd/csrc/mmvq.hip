@@ -92,10 +92,30 @@ static hipError_t launch_nc(const MmArgs &a, int nc, int grid_y, int grid_z, hip
     }
 }
 
-// 16-lane rows only with one row per lane group (the small-K decode shapes)
+// lanes per row of a launch, from hipGraph periods of back-to-back calls
+// (profiles/r06_valu_plan_sweep.txt; mmvq_pick_lpr alone chose by idle slot lanes):
+//  * below 6144 rows 64 from K = 1088 on, even where that leaves slot lanes idle: an 8-wave
+//    workgroup then covers 8 or 16 rows instead of 32, and short matrices get the workgroups to
+//    fill the chip (Q4_0 3072 x 768 3.2 vs 4.3 us, Q6_K 3072 x 768 at 4 columns 5.4 vs 8.2);
+//  * from 6144 rows 16 for groups of 2..8 columns, also where both widths use every slot lane
+//    (K = 4096): four rows per wave share each activation read and a workgroup serves twice the
+//    rows, so its staging of the columns (load and quantization of nc x K values) is spread over
+//    twice the weight bytes (Q6_K 4096 x 14336 at 8 columns 25.4 vs 43.8 us, Q5_K at 3 13.7 vs
+//    19.2); single columns keep mmvq_pick_lpr's width there (Q4_0 2048 x 14336 5.8 vs 7.5 us
+//    with 16, 4096 x 11008 7.6 vs 8.2 with 64);
+//  * K <= 1024: mmvq_pick_lpr's width.
+static int lanes_per_row(const MmArgs &a, int nc) {
+    if (is_bigk(a)) return 64;
+    const int l = mmvq_pick_lpr(a.K);
+    if (settings().lpr == 16 || settings().lpr == 64 || a.K <= 1024) return l;
+    if (a.N >= 6144) return nc >= 2 ? 16 : l;
+    return 64;
+}
+
+// 16-lane rows only with one row per lane group
 template <int T>
 static hipError_t launch_type(const MmArgs &a, int nc, int grid_y, int grid_z, int rpw, hipStream_t st) {
-    if (mmvq_pick_lpr(a.K) == 16 && !is_bigk(a)) return launch_nc<T, 16, 1>(a, nc, grid_y, grid_z, st);
+    if (lanes_per_row(a, nc) == 16) return launch_nc<T, 16, 1>(a, nc, grid_y, grid_z, st);
     if (rpw <= 1) return launch_nc<T, 64, 1>(a, nc, grid_y, grid_z, st);
     return launch_nc<T, 64, 2>(a, nc, grid_y, grid_z, st);
 }
@@ -103,7 +123,7 @@ static hipError_t launch_type(const MmArgs &a, int nc, int grid_y, int grid_z, i
 // the launch launch_type / launch_one make (the dispatch description, ggml_mi355x_mul_mat_plan)
 std::string mmvq_plan_text(const MmArgs &a, int nc, int rpw) {
     const bool bigk = is_bigk(a);
-    const int lpr = mmvq_pick_lpr(a.K) == 16 && !bigk ? 16 : 64;
+    const int lpr = lanes_per_row(a, nc);
     const int r = lpr == 16 || rpw <= 1 ? 1 : 2;
     const int rows_per_group = MMVQ_WAVES * (WAVE / lpr) * r;
     const int n_groups = (a.N + rows_per_group - 1) / rows_per_group;

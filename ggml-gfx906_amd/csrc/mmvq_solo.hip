@@ -204,19 +204,26 @@ bool mmvq_solo_supported(const MmArgs &a) {
     return a.M == 1 && a.ne12 == 1 && a.ne13 == 1 && a.K % 64 == 0 && a.K >= 64 && a.K <= 4096;
 }
 
-// the default (settings().solo < 0): Q4_K / Q5_K from 8192 rows, Q6_K from 4096. Measured first as
+// the default (settings().solo < 0): Q8_0 and Q6_K from K = 1536 (or up to 1024 rows), Q4_K /
+// Q5_K from 8192 rows. Measured first as
 // rocprof kernel durations (profiles/r06_solo_singles_ab.txt: 8 rows per wave Q4_0 4096^2
 // 5.14-5.20 vs 5.33-5.39 us for the 8-wave kernel, Q4_K 4096^2 5.30-5.32 vs 5.47-5.54), then as
 // hipGraph periods of back-to-back calls, what a decode graph runs (profiles/r06_valu_plan_sweep.txt):
 // there the 8-wave kernel is ahead at 4096 rows (Q4_0 4096^2 4.51 vs 4.75 us, Q4_K 4.67 vs 4.90,
 // Q5_K 5.23 vs 5.74, and Q4_0 at 11008 rows) and this kernel from 11008 rows for the K-quants
 // (Q4_K 4096 x 11008 8.48 vs 8.83, Q5_K 10.17 vs 10.32, Q6_K 11.12 vs 12.18, and at 14336 rows;
-// Q6_K already at 4096 rows: 2048 x 4096 4.98 vs 5.51, 4096^2 5.62 vs 5.73).
+// Q6_K already at 4096 rows: 2048 x 4096 4.98 vs 5.51, 4096^2 5.62 vs 5.73, and short
+// matrices: 3072 x 768 3.4 vs 4.0 with 64-lane rows; Q8_0 at every shape measured: 4096^2 5.26
+// vs 5.55, 3072 x 768 3.19 vs 3.41, 4096 x 11008 11.56 vs 12.16; but at K = 768, where a wave
+// has 12 slots, 768 x 50257 16.4 vs 10.2). Q4_0 / Q4_K / Q5_K below 8192 rows: the 8-wave kernel
+// with 64-lane rows is ahead (mmvq.hip lanes_per_row).
 // Two rows per wave are 1.4-1.7x slower (the column is re-read per wave).
 bool mmvq_solo_default(int type, const MmArgs &a) {
     const int s = settings().solo;
     if (s == 0 || !mmvq_solo_supported(a)) return false;
-    return s > 0 || (type == T_Q6_K && a.N >= 4096) || (a.N >= 8192 && (type == T_Q4_K || type == T_Q5_K));
+    if (s > 0) return true;
+    if (type == T_Q8_0 || type == T_Q6_K) return a.K >= 1536 || a.N <= 1024;   // (K = 768: 12 of 64 lanes live)
+    return a.N >= 8192 && (type == T_Q4_K || type == T_Q5_K);
 }
 
 static int solo_rows_default(int type) { return type == T_Q6_K ? 4 : 8; }

@@ -35,7 +35,7 @@ PLANS = {
     # put the 8-wave kernel ahead of the single-wave one at 4096 rows, mmvq_solo.hip)
     ("q4_0", 4096, 4096, 1, 1): "mmvq nc=1 lpr=64 rpw=2 grid=256x1x1",
     ("q4_K", 4096, 4096, 1, 1): "mmvq nc=1 lpr=64 rpw=2 grid=256x1x1",
-    ("q8_0", 4096, 4096, 1, 1): "mmvq nc=1 lpr=64 rpw=2 grid=256x1x1",
+    ("q8_0", 4096, 4096, 1, 1): "mmvq-solo rows=8 grid=512",
     # bench.py headline: 64 stacked matrices per MUL_MAT
     ("q4_0", 4096, 4096, 1, 64): "mmvq nc=1 lpr=64 rpw=2 grid=32x64x1",
     ("q4_K", 4096, 4096, 1, 64): "mmvq nc=1 lpr=64 rpw=2 grid=32x64x1",
