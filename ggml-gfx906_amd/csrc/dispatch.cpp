@@ -65,7 +65,7 @@ int64_t mmq8_tiles128(const MmArgs &a);
 hipError_t mmq8r_launch(int type, const MmArgs &a, const void *rp, int ne02, int n_mat, hipStream_t st, Scratch &scratch);
 bool mmq8_id_supported(int type, const MmArgs &a);
 hipError_t mmq8_id_launch(int type, const MmArgs &a, hipStream_t st, Scratch &scratch);
-std::string mmvq_plan_text(const MmArgs &a, int nc, int rpw);
+std::string mmvq_plan_text(int type, const MmArgs &a, int nc, int rpw);
 std::string mmvq_ring_plan_text(int type, const MmArgs &a, int nc, int rpw, bool pre);
 std::string mmvq_mma_plan_text(int type, const MmArgs &a);
 std::string mmq8_plan_text(const MmArgs &a);
@@ -292,7 +292,7 @@ static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st
             g.M = nc;
             const bool solo = nc == 1 && mmvq_solo_default(type, g);
             if (plan) {
-                note(solo ? mmvq_solo_plan_text(type, g) : mmvq_plan_text(g, nc, pick_rpw(type, rows_total, nc, false)));
+                note(solo ? mmvq_solo_plan_text(type, g) : mmvq_plan_text(type, g, nc, pick_rpw(type, rows_total, nc, false)));
                 e = hipSuccess;
             } else if (solo) {
                 e = mmvq_solo_launch(type, g, st);

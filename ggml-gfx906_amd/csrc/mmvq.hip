@@ -27,7 +27,15 @@ int mmvq_pick_lpr(int K) {
 
 int mmvq_rows_per_group(int lpr, int rpw) { return MMVQ_WAVES * (WAVE / lpr) * rpw; }
 
-constexpr int64_t MMVQ_TARGET_WGS = 2048;   // two rounds of 4 resident 8-wave workgroups per CU (scripts/mmvq_sweep.sh)
+// workgroups a launch aims at (beyond that each walks more row groups): 2048 (scripts/mmvq_sweep.sh,
+// round 2), 4096 for Q4_0 / Q4_K, whose kernels keep more waves resident (7 / 5 per SIMD against
+// 3-4): on the bench's stacked launches Q4_0 4096^2 x 64 101.4-101.9 vs 103.7-104.2 us, Q4_K 103.8
+// vs 106.8, Q4_K 4096 x 11008 x 24 103.6 vs 105.6, while Q5_K x 24 takes 143 vs 131 and Q6_K 171
+// vs 165 (profiles/r06_mmvq_wgs_ab.txt, three interleaved rounds)
+static int64_t mmvq_target_wgs(int type) {
+    if (settings().mmvq_wgs > 0) return settings().mmvq_wgs;
+    return type == T_Q4_0 || type == T_Q4_K ? 4096 : 2048;
+}
 
 template <int T, int NC, int LPR, int RPW, bool IDS, bool RAG, bool XA, bool BIGK>
 static hipError_t launch_one(const MmArgs &a0, int grid_y, int grid_z, hipStream_t st) {
@@ -45,7 +53,7 @@ static hipError_t launch_one(const MmArgs &a0, int grid_y, int grid_z, hipStream
     const int n_groups = (a.N + rows_per_group - 1) / rows_per_group;
     // enough workgroups to fill 256 CUs ~4 deep; beyond that each workgroup walks more groups
     const int64_t others = (int64_t)grid_y * grid_z;
-    const int64_t target = settings().mmvq_wgs > 0 ? settings().mmvq_wgs : MMVQ_TARGET_WGS;
+    const int64_t target = mmvq_target_wgs(T);
     // floor, not ceil: a launch just above a multiple of the resident capacity (4 workgroups of
     // 8 waves per CU = 1024) leaves a tail of workgroups that start only when others finish
     const int want = (int)std::max<int64_t>(1, target / others);
@@ -121,14 +129,14 @@ static hipError_t launch_type(const MmArgs &a, int nc, int grid_y, int grid_z, i
 }
 
 // the launch launch_type / launch_one make (the dispatch description, ggml_mi355x_mul_mat_plan)
-std::string mmvq_plan_text(const MmArgs &a, int nc, int rpw) {
+std::string mmvq_plan_text(int type, const MmArgs &a, int nc, int rpw) {
     const bool bigk = is_bigk(a);
     const int lpr = lanes_per_row(a, nc);
     const int r = lpr == 16 || rpw <= 1 ? 1 : 2;
     const int rows_per_group = MMVQ_WAVES * (WAVE / lpr) * r;
     const int n_groups = (a.N + rows_per_group - 1) / rows_per_group;
     const int64_t others = (int64_t)a.ne12 * a.ne13 * (a.M / nc);
-    const int64_t target = settings().mmvq_wgs > 0 ? settings().mmvq_wgs : MMVQ_TARGET_WGS;
+    const int64_t target = mmvq_target_wgs(type);
     const int gx = (int)std::min<int64_t>(n_groups, std::max<int64_t>(1, target / others));
     return "mmvq nc=" + std::to_string(nc) + " lpr=" + std::to_string(lpr) + " rpw=" + std::to_string(r) +
            (bigk ? " bigk" : "") + " grid=" + std::to_string(gx) + "x" + std::to_string(a.ne12 * a.ne13) + "x" +

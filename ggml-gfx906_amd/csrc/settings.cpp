@@ -23,7 +23,7 @@ static Settings load_settings() {
     Settings s;
     s.rpw = i("GGML_MI355X_RPW", 0);
     s.lpr = i("GGML_MI355X_LPR", 0);
-    s.mmvq_wgs = l("GGML_MI355X_MMVQ_WGS", 2048);
+    s.mmvq_wgs = l("GGML_MI355X_MMVQ_WGS", 0);
     s.ring = i("GGML_MI355X_RING", 1);
     s.ring_pre = i("GGML_MI355X_RING_PRE", 1);
     s.ring_depth = i("GGML_MI355X_RING_DEPTH", 3);

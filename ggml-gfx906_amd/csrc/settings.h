@@ -15,7 +15,7 @@ struct Settings {
     // ---- mat-vec (ne11 <= 8)
     int rpw = 0;                  // GGML_MI355X_RPW: rows per wave (0 = pick_rpw's rule)
     int lpr = 0;                  // GGML_MI355X_LPR: 16 / 64 lanes per row (0 = by K)
-    int64_t mmvq_wgs = 2048;      // GGML_MI355X_MMVQ_WGS: target workgroups of a batched mat-vec
+    int64_t mmvq_wgs = 0;         // GGML_MI355X_MMVQ_WGS: target workgroups of a batched mat-vec (0 per type)
     int ring = 1;                 // GGML_MI355X_RING: 0 never the chunked-K kernel, 1 rule, 2 also 1 column
     int ring_pre = 1;             // GGML_MI355X_RING_PRE: 0 never pre-quantize, 1 from 4 columns, 2 from 2
     int ring_depth = 3;           // GGML_MI355X_RING_DEPTH: weight sets in flight (2 or 3)

@@ -37,8 +37,8 @@ PLANS = {
     ("q4_K", 4096, 4096, 1, 1): "mmvq nc=1 lpr=64 rpw=2 grid=256x1x1",
     ("q8_0", 4096, 4096, 1, 1): "mmvq-solo rows=8 grid=512",
     # bench.py headline: 64 stacked matrices per MUL_MAT
-    ("q4_0", 4096, 4096, 1, 64): "mmvq nc=1 lpr=64 rpw=2 grid=32x64x1",
-    ("q4_K", 4096, 4096, 1, 64): "mmvq nc=1 lpr=64 rpw=2 grid=32x64x1",
+    ("q4_0", 4096, 4096, 1, 64): "mmvq nc=1 lpr=64 rpw=2 grid=64x64x1",
+    ("q4_K", 4096, 4096, 1, 64): "mmvq nc=1 lpr=64 rpw=2 grid=64x64x1",
     # BASELINE configs[2]: 4096 x 11008 k-quants, M = 1
     ("q4_K", 4096, 11008, 1, 1): "mmvq-solo rows=8 grid=1376",
     ("q5_K", 4096, 11008, 1, 1): "mmvq-solo rows=8 grid=1376",
