@@ -215,6 +215,9 @@ static int ring_pre_min() {
 // columns: Q4_0 4096 x 14336 at 3 10.6 vs 14.7 us, Q4_K at 4 12.5 vs 17.2)
 //   Q5_K  K < 8192: 5; to K = 16384 3 where the plan keeps one K part (its image fits the LDS;
 //         elsewhere the VALU kernels win up to 7 columns: 27.4 vs 28.8 us at 28672 x 4096), and 8
+//   Q6_K  K < 8192: 5; 3 from K = 12288, or from 8192 at N >= 8192; else 8 (profiles/r06_q6k_mma.txt:
+//         14336 x 4096 at 3..8 columns 18.0-18.4 vs 21.3-27.3 us, 4096 x 4096 at 5..8 9.7-9.9 vs
+//         13.2-14.2; at 11008 x 4096 the VALU kernels stay ahead to 5 columns)
 // e.g. Q4_0 4096 x 4096 at 5..8 columns 8.4 vs 10.1-12.0 us, Q8_0 14336 x 4096 at 3..8 18.5 vs
 // 20.3-23.0, Q5_K 14336 x 4096 at 3..8 17.5 vs 18.5-22.3 (the plan's one-K-part forms,
 // profiles/r06_mma_plan_sweep.txt); everywhere else the VALU kernels are as fast or within 3 %. GGML_MI355X_MMA=N: from N columns on for every type it
@@ -233,6 +236,7 @@ static bool use_mma(int type, const MmArgs &g) {
         case T_Q8_0: return cols >= (K >= 11008 ? 3 : 5);
         case T_Q4_K: return cols >= (K >= 8192 ? 3 : 5);
         case T_Q5_K: return K < 8192 ? cols >= 5 : cols >= 8 || (cols >= 3 && K <= 16384 && mmvq_mma_one_part(type, g));
+        case T_Q6_K: return cols >= (K >= 12288 || (K >= 8192 && N >= 8192) ? 3 : K >= 8192 ? 8 : 5);
         default: return false;
     }
 }

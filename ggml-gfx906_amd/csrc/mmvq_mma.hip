@@ -434,6 +434,98 @@ template <int TOK> struct MmaW<T_Q5_K, TOK> {
     }
 };
 
+// Q6_K: step s = half h = s & 1 of super-block s >> 1 (128 elements: ql bytes 64h .. 64h + 63,
+// qh bytes 128 + 32h .. + 31, scales 192 + 8h .. + 7, d at 208). Block j of the half is element
+// l = 0..31 of quadrant j: the low (j < 2) or high nibble of ql run j & 1 (32 B at 64h + 32 (j & 1)),
+// bits 2j, 2j + 1 of qh byte l, scale 8h + 2j + l / 16 (so each 32-block has two scales, one per
+// 16-element half). Codes are stored signed (q - 32 fits int8), so no offset term is left.
+// Two 16-B loads per lane and step (the load instructions bound the kernel: separate 2-byte scale
+// and d loads cost 15 %, profiles/r06_q6k_mma.txt):
+//   ql: TOK 4: lane g (block g) loads half g >> 1 of run g & 1 and trades with lane g ^ 2
+//       (run_whole32); TOK 8: lane g (half g & 1 of block 2p + (g >> 1) for pairs p = 0, 1: the
+//       same run, nibble p) loads bytes 16 (g & 1) .. + 15 of run g >> 1, then run_half;
+//   second piece: lanes 0 / 1 the qh run's halves, lane 2 the scale bytes 192..207, lane 3 bytes
+//       194..209 (the last 14 scales and d); one swap32 leaves qh half g & 1 and the scale window
+//       of lane 2 + (g & 1) on every lane, and in either window block g's two scales are dword
+//       2h + (g >> 1), low half; d reaches the even lanes by one swap16.
+// Super-blocks are 2-byte aligned, so the 16-B pieces may be too (the memory path takes them at
+// the same rate here: 4-byte aligned pieces measured no faster).
+__device__ __forceinline__ void run_whole32(const uint32_t (&own)[4], uint32_t (&q)[8]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t A = own[k], B = own[k];
+        swap32(A, B);   // (lanes g < 2 loaded bytes 0..15, g >= 2 bytes 16..31)
+        q[k] = B;
+        q[4 + k] = A;
+    }
+}
+// 4 signed codes (q - 32) from 4 ql nibbles at shift sft and 4 qh bit pairs at shift hb
+__device__ __forceinline__ uint32_t q6_codes(uint32_t ql, uint32_t qh, int sft, int hb) {
+    const uint32_t u = ((ql >> sft) & NIB) | (((qh >> hb) & 0x03030303u) << 4);   // 0..63 per byte
+    return (u + 0x60606060u) ^ 0x80808080u;                                         // (u + 96) - 128
+}
+template <int TOK> struct MmaW<T_Q6_K, TOK> {
+    static constexpr int NSC = 2;
+    uint32_t QV[4], MV[4], S, D;
+    int h;
+    __device__ static uint32_t step_off(int s) { return 210u * (uint32_t)(s >> 1); }
+    // a = the ql piece, b = the second piece
+    __device__ static MmaLanes lanes(int r, int g, int h, uint32_t nb01, uint32_t) {
+        const uint32_t row = r * nb01;
+        const uint32_t ql = TOK == 4 ? 32 * (g & 1) + 16 * (g >> 1) : 32 * (g >> 1) + 16 * (g & 1);
+        const uint32_t m = g < 2 ? 128 + 32 * h + 16 * g : 192 + 2 * (g - 2);
+        return {row + 64 * h + ql, row + m, 0};
+    }
+    __device__ inline void load(__amdgpu_buffer_rsrc_t rs, const MmaLanes &lo) {
+        bl16(rs, lo.a, QV);
+        bl16(rs, lo.b, MV);
+    }
+    __device__ inline void frags(long (&A)[4], int g, const MmaLanes &) {
+        pin(QV);
+        pin(MV);
+        uint32_t H[4], W[4];   // qh half g & 1; the scale window of lane 2 + (g & 1)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t a = MV[k], b = MV[k];
+            swap32(a, b);
+            H[k] = b;
+            W[k] = a;
+        }
+        uint32_t dw = W[3], dn = W[3];
+        swap16(dw, dn);   // (even lanes: the odd partner's bytes 206..209; odd lanes keep their own)
+        D = dw >> 16;
+        const uint32_t w0 = h ? W[2] : W[0], w1 = h ? W[3] : W[1];
+        S = (g & 2 ? w1 : w0) & 0xffffu;
+        if constexpr (TOK == 4) {
+            uint32_t Q[8], QH[8];
+            run_whole32(QV, Q);
+            run_whole(H, QH);
+            const int sft = 4 * (g >> 1), hb = 2 * g;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int o = 2 * (m >> 1) + 4 * (m & 1);
+                A[m] = pack2(q6_codes(Q[o], QH[o], sft, hb), q6_codes(Q[o + 1], QH[o + 1], sft, hb));
+            }
+        } else {
+            uint32_t Q[4], QH[4];
+            run_half(QV, Q);
+            run_half(H, QH);
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const int sft = 4 * p, hb = 2 * (2 * p + (g >> 1));
+                A[2 * p] = pack2(q6_codes(Q[0], QH[0], sft, hb), q6_codes(Q[1], QH[1], sft, hb));
+                A[2 * p + 1] = pack2(q6_codes(Q[2], QH[2], sft, hb), q6_codes(Q[3], QH[3], sft, hb));
+            }
+        }
+    }
+    // d * sc of the two halves of block g (S, D: from frags)
+    __device__ inline void sc(float *o, int) const {
+        const float d = h2f((uint16_t)D);
+        o[0] = d * (float)(int8_t)(S & 0xff);
+        o[1] = d * (float)(int8_t)(S >> 8);
+    }
+};
+
 // ------------------------------------------------------------------------------------------
 // Paired steps (Q4_0 / Q8_0, 4-byte-aligned contiguous rows): lane g loads blocks 2g and 2g + 1
 // of a double step (8 blocks of its row, 256 k) as one aligned window — half the load
@@ -561,7 +653,10 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
     const MmaLanes lo0 = W::lanes(c, g, wave & 1, nb01, (uint32_t)(reinterpret_cast<uintptr_t>(wtile) & 3));
     MmaLanes lo[RT];
 #pragma unroll
-    for (int t = 0; t < RT; ++t) lo[t] = {lo0.a + 16 * t * nb01, lo0.b + 16 * t * nb01, lo0.c + (t && (T == T_Q5_K) ? 16 * t * nb01 : 0)};
+    for (int t = 0; t < RT; ++t) {
+        const uint32_t dt = 16 * t * nb01;
+        lo[t] = {lo0.a + dt, lo0.b + dt, lo0.c + (T == T_Q5_K ? dt : 0u)};
+    }
     if constexpr (T == T_Q4_0 || T == T_Q8_0) {
 #pragma unroll
         for (int t = 0; t < RT; ++t) lo[t].c = lo0.c;   // (the funnel shift: 16 rows apart keep the alignment)
@@ -637,6 +732,28 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
             const i32x4_t zero = {0, 0, 0, 0};
 #pragma unroll
             for (int p = 0; p < P; ++p) {
+                if constexpr (T == T_Q6_K) {
+                    // a block's two 16-element halves have scales of their own: one MFMA chain per
+                    // half (TOK 4: chunks 0, 2 | 1, 3; TOK 8: MFMA q is half q), then
+                    // acc += dx * (s0 * R0 + s1 * R1) for rows 4g + i, token bt, block p G + bg
+                    i32x4_t R0 = zero, R1 = zero;
+#pragma unroll
+                    for (int q = 0; q < Qn; ++q) {
+                        const int ci = TOK == 4 ? 2 * q : 4 * p + 2 * q;
+                        const long B = pack2(x.c[ci], x.c[ci + 1]);
+                        if ((TOK == 4 ? q & 1 : q) == 0) R0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(A[p * Qn + q], B, R0, 0, 0, 0);
+                        else R1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(A[p * Qn + q], B, R1, 0, 0, 0);
+                    }
+                    const float *rs = ws + (p * G + bg) * NSC * 16 + 4 * g;
+                    const float4 s4 = *reinterpret_cast<const float4 *>(rs), t4 = *reinterpret_cast<const float4 *>(rs + 16);
+                    const mma_f2 xd = {x.s[p].x, x.s[p].x};
+                    const mma_f2 s0[2] = {{s4.x, s4.y}, {s4.z, s4.w}}, s1[2] = {{t4.x, t4.y}, {t4.z, t4.w}};
+                    const mma_f2 r0[2] = {{(float)R0[0], (float)R0[1]}, {(float)R0[2], (float)R0[3]}};
+                    const mma_f2 r1[2] = {{(float)R1[0], (float)R1[1]}, {(float)R1[2], (float)R1[3]}};
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) acc[t][h] = __builtin_elementwise_fma(xd, __builtin_elementwise_fma(s0[h], r0[h], s1[h] * r1[h]), acc[t][h]);
+                    continue;
+                }
                 i32x4_t R = zero;
 #pragma unroll
                 for (int q = 0; q < Qn; ++q) {
@@ -815,7 +932,7 @@ static int mma_run_len(int part, bool pr) {
 // the column image of a part lives in LDS next to the kernel's static arrays (wsc: 4 KiB x RT x
 // scales per block, red: 1 KiB x RT x TOK), after which come the 128 zero bytes; 256 bytes of
 // slack for alignment
-static constexpr int mma_nsc(int type) { return type == T_Q4_K || type == T_Q5_K ? 2 : 1; }
+static constexpr int mma_nsc(int type) { return type == T_Q4_K || type == T_Q5_K || type == T_Q6_K ? 2 : 1; }
 static constexpr int mma_lds_img(int nsc, int tok, int rt) { return 160 * 1024 - (4096 * nsc + 1024 * tok) * rt - 128 - 256; }
 
 // exactly the launcher's conditions for a part of `part` steps: a run for it, its image in LDS,
@@ -857,11 +974,11 @@ static MmaPlan mma_plan(int type, const MmArgs &a) {
     p.pr = want && mma_pair_aligned(type, a);
     const bool two_ok = p.pr ? S >= 64 : S >= 32;
     const int ke = settings().mma_kh, re = settings().mma_rt;
-    auto rt_of = [&](int want) { return type == T_Q5_K || (type == T_Q8_0 && p.pr) ? 1 : re == 1 || re == 2 ? re : want; };
+    auto rt_of = [&](int want) { return type == T_Q5_K || type == T_Q6_K || (type == T_Q8_0 && p.pr) ? 1 : re == 1 || re == 2 ? re : want; };
     const int rt1 = rt_of((a.N >= 8192 && a.K >= 8192) || a.N >= 12288 ? 2 : 1);
     if (ke == 1) p.kh = 1;
     else if (ke == 2) p.kh = two_ok ? 2 : 1;
-    else if (type == T_Q5_K && a.K < 8192 && a.N < 8192) p.kh = two_ok ? 2 : 1;   // (one tile per workgroup: 512 beat 256)
+    else if ((type == T_Q5_K || type == T_Q6_K) && a.K < 8192 && a.N < 8192) p.kh = two_ok ? 2 : 1;   // (one tile per workgroup: 512 beat 256)
     else p.kh = two_ok && !mma_part_fits(type, a, S, p.pr, rt1) ? 2 : 1;
     p.rt = p.kh == 1 ? rt1 : rt_of(2);
     return p;
@@ -871,7 +988,7 @@ static MmaPlan mma_plan(int type, const MmArgs &a) {
 bool mmvq_mma_one_part(int type, const MmArgs &a) { return mma_plan(type, a).kh == 1; }
 
 bool mmvq_mma_supported(int type, const MmArgs &a) {
-    if (!(type == T_Q4_0 || type == T_Q8_0 || type == T_Q4_K || type == T_Q5_K) || a.M < 1 || a.M > 8) return false;
+    if (!(type == T_Q4_0 || type == T_Q8_0 || type == T_Q4_K || type == T_Q5_K || type == T_Q6_K) || a.M < 1 || a.M > 8) return false;
     const MmaPlan pl = mma_plan(type, a);
     return mma_part_fits(type, a, mma_part_steps(a, pl.kh), pl.pr, pl.rt);
 }
@@ -881,7 +998,7 @@ std::string mmvq_mma_plan_text(int type, const MmArgs &a) {
     const MmaPlan pl = mma_plan(type, a);
     const int part = mma_part_steps(a, pl.kh);
     int rt = pl.rt;
-    if (type == T_Q5_K || (type == T_Q8_0 && pl.pr)) rt = 1;
+    if (type == T_Q5_K || type == T_Q6_K || (type == T_Q8_0 && pl.pr)) rt = 1;
     return "mma tok=" + std::to_string(mma_tok_of(a)) + " kh=" + std::to_string(pl.kh) + " rt=" + std::to_string(rt) +
            (pl.pr ? " paired" : "") + " run=" + std::to_string(mma_run_len(part, pl.pr)) + " cols=" + std::to_string(a.M);
 }
@@ -934,7 +1051,7 @@ static hipError_t mma_tok(const MmArgs &a, uint8_t *img, hipStream_t st) {
     } else if (a.x_aligned16) hipLaunchKernelGGL((mma_prequant<TOK, true>), pg, dim3(TOK * 16), 0, st, a, img, kh == 2);
     else hipLaunchKernelGGL((mma_prequant<TOK, false>), pg, dim3(TOK * 16), 0, st, a, img, kh == 2);
     hipError_t e;
-    if constexpr (T == T_Q5_K) e = mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
+    if constexpr (T == T_Q5_K || T == T_Q6_K) e = mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
     else if constexpr (T == T_Q8_0) {
         if (pl.pr) e = mma_run<T, TOK, 1, true>(a, img, S, part, kh, st);   // (two tiles of pairs would spill)
         else e = pl.rt == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
@@ -958,7 +1075,8 @@ hipError_t mmvq_mma_launch(int type, const MmArgs &a, uint8_t *img, hipStream_t 
         case T_Q8_0: return mma_type<T_Q8_0>(a, img, st);
         case T_Q4_K: return mma_type<T_Q4_K>(a, img, st);
         case T_Q5_K: return mma_type<T_Q5_K>(a, img, st);
-        default: return hipErrorInvalidValue;   // (Q6_K stays on the VALU kernels)
+        case T_Q6_K: return mma_type<T_Q6_K>(a, img, st);
+        default: return hipErrorInvalidValue;
     }
 }
 

@@ -80,10 +80,10 @@ PERF = {
     ("q5_K", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
     ("q6_K", 1): "ring nc=1 rpw=1 cols=1",
     ("q6_K", 2): "ring nc=2 rpw=1 cols=2",
-    ("q6_K", 3): "ring-pre nc=4 rpw=1 cols=3",
-    ("q6_K", 4): "ring-pre nc=4 rpw=1 cols=4",
-    ("q6_K", 5): "ring-pre nc=8 rpw=1 cols=5",
-    ("q6_K", 8): "ring-pre nc=8 rpw=1 cols=8",
+    ("q6_K", 3): "mma tok=4 kh=1 rt=1 run=7 cols=3",
+    ("q6_K", 4): "mma tok=4 kh=1 rt=1 run=7 cols=4",
+    ("q6_K", 5): "mma tok=8 kh=1 rt=1 run=7 cols=5",
+    ("q6_K", 8): "mma tok=8 kh=1 rt=1 run=7 cols=8",
     ("q6_K", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
 }
 
@@ -107,6 +107,14 @@ MMA_RULE = {
     ("q5_K", 14336, 4096, 3): "mma tok=4 kh=1 rt=1 run=7 cols=3",
     ("q5_K", 14336, 4096, 5): "mma tok=8 kh=1 rt=1 run=7 cols=5",
     ("q5_K", 28672, 4096, 3): "ring-pre nc=4 rpw=1 cols=3",                   # past K = 16384: VALU to 7
+    # Q6_K (round 6, profiles/r06_q6k_mma.txt)
+    ("q6_K", 4096, 4096, 3): "mmvq nc=3 lpr=64 rpw=1 grid=512x1x1",           # K < 8192: from 5
+    ("q6_K", 4096, 4096, 5): "mma tok=8 kh=2 rt=1 run=1 cols=5",              # small: two parts
+    ("q6_K", 11008, 4096, 5): "ring-pre nc=8 rpw=1 cols=5",                   # 8192 <= K < 12288, N < 8192: 8
+    ("q6_K", 11008, 4096, 8): "mma tok=8 kh=1 rt=1 run=6 cols=8",
+    ("q6_K", 8192, 8192, 3): "mma tok=4 kh=1 rt=1 run=4 cols=3",              # N >= 8192: from 3
+    ("q6_K", 28672, 4096, 3): "mma tok=4 kh=1 rt=1 run=14 cols=3",
+    ("q6_K", 28672, 4096, 8): "mma tok=8 kh=2 rt=1 run=7 cols=8",             # image past LDS: two parts
 }
 
 
