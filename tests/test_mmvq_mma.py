@@ -9,7 +9,7 @@ the CPU oracle (ggml-cpu's vec_dot on its own src1 quantization) the reference's
 forms are also pinned by golden records from the reference itself, tests/golden mm_166..mm_172,
 replayed by test_gpu_parity.py.)
 
-Covered: Q4_0, Q8_0, Q4_K, Q5_K, Q6_K (two scales per 32-block: one MFMA chain per half); 1..8 columns (4- and 8-token
+Covered: all five types (Q6_K: two scales per 32-block, one MFMA chain per half); 1..8 columns (4- and 8-token
 forms); ragged rows (N % 16 != 0); Q4_0 / Q8_0 K that ends inside a 128-step (K % 128 = 32, 64,
 96), K-quants at odd super-block counts; the reference's perf shapes (K = 14336, bs 2..8);
 broadcast batch slices (ne12 = 2 * ne02); every per-wave step run (K = 4096 .. 28672) with one and
