@@ -30,7 +30,7 @@ bool mmvq_has_nc(int nc);
 int mmvq_max_k_for_nc(int nc);
 bool mmvq_bigk(int K);
 hipError_t mmvq_ring_launch(int type, const MmArgs &a, int nc, int rpw, uint8_t *img, hipStream_t st);
-hipError_t mmvq_mma_launch(int type, const MmArgs &a, uint8_t *img, int *counters, hipStream_t st);
+hipError_t mmvq_mma_launch(int type, const MmArgs &a, uint8_t *img, hipStream_t st);
 size_t mmvq_mma_img_bytes(int type, const MmArgs &a);
 bool mmvq_mma_supported(int type, const MmArgs &a);
 bool mmvq_mma_one_part(int type, const MmArgs &a);
@@ -265,10 +265,7 @@ static hipError_t run_mmvq(int type, MmArgs m, int c0, int ncols, hipStream_t st
                 return hipSuccess;
             }
             if (uint8_t *img = static_cast<uint8_t *>(scratch->get(mmvq_mma_img_bytes(type, g), st))) {
-                // (the in-launch pre-pass's two counters: the last two 128-B lines of the
-                // zeroed counter block, past any stream-K tile counter)
-                int *cnt = scratch->counters(st);
-                const hipError_t e = mmvq_mma_launch(type, g, img, cnt ? cnt + Scratch::COUNTERS - 64 : nullptr, st);
+                const hipError_t e = mmvq_mma_launch(type, g, img, st);
                 if (e != hipErrorInvalidValue) return e;   // (a shape the launcher refuses: the kernels below)
             }
         }

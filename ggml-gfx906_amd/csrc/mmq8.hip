@@ -1500,7 +1500,7 @@ static Mmq8Plan mmq8_plan(const MmArgs &a) {
     // workgroup >= super-blocks per tile, since tiles > workgroups). GGML_MI355X_MMQ8_SK: 0 never
     // (A/B), 1 whenever the tiles outnumber the workgroups
     const int64_t rounds = (p.tiles + MMQ8_SK_WGS - 1) / MMQ8_SK_WGS;
-    const bool can_sk = slices == 1 && p.ksplit == 1 && p.tr_rows == 128 && p.tiles > MMQ8_SK_WGS && p.tiles <= Scratch::COUNTERS - 64;   // (the last 64: mmvq_mma)
+    const bool can_sk = slices == 1 && p.ksplit == 1 && p.tr_rows == 128 && p.tiles > MMQ8_SK_WGS && p.tiles <= Scratch::COUNTERS;
     p.use_sk = S.mmq8_sk >= 0 ? (S.mmq8_sk == 1 && can_sk) : (can_sk && (double)p.tiles / (double)(rounds * MMQ8_SK_WGS) < 0.85);
     return p;
 }

@@ -54,7 +54,6 @@ typedef int i32x4_t __attribute__((ext_vector_type(4)));
 constexpr int MMA_STEP_K = 128;   // K per step: 4 blocks of 32
 constexpr int MMA_KS = 16;        // waves per workgroup
 constexpr uint32_t MMA_RSRC_W3 = 0x00020000u;   // raw buffer descriptor dword 3 (as mmq8.hip)
-constexpr int MMA_SC1 = 16;                      // buffer-load cache policy: sc1 (gfx940 family)
 
 // activation image of one (slice, step): codes [t TOK][block 4][32 B] in chunk order, then
 // [t][block] {d, d * sum(q)} f32
@@ -83,8 +82,7 @@ __device__ __forceinline__ void mma_xload(const MmArgs &a, const float *col, int
         for (int i = 0; i < 8; ++i) v[i] = col[min(k0 + i, a.K - 1)];
     }
 }
-// (WT: write-through sc1 stores, for the in-launch pre-pass whose image other workgroups read)
-template <int TOK, bool WT = false>
+template <int TOK>
 __device__ __forceinline__ void mma_quant(const MmArgs &a, float (&v)[8], int s, int j, int t, int m, uint8_t *step) {
     const int k0 = s * MMA_STEP_K + 32 * j + mma_elem(m, 0);
 #pragma unroll
@@ -102,20 +100,12 @@ __device__ __forceinline__ void mma_quant(const MmArgs &a, float (&v)[8], int s,
     for (int i = 0; i < 8; ++i) b[i] = __float_as_uint(__builtin_fmaf(v[i], id, MAGIC));
     const uint32_t w0 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(b[3], b[2], 0x0c0c0400u), __builtin_amdgcn_perm(b[1], b[0], 0x0c0c0400u), 0x05040100u);
     const uint32_t w1 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(b[7], b[6], 0x0c0c0400u), __builtin_amdgcn_perm(b[5], b[4], 0x0c0c0400u), 0x05040100u);
-    uint64_t *cq = reinterpret_cast<uint64_t *>(step + (t * 4 + j) * 32 + m * 8);
-    const uint64_t cv = ((uint64_t)(w1 ^ 0x80808080u) << 32) | (w0 ^ 0x80808080u);
-    if constexpr (WT) __hip_atomic_store(cq, cv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else *cq = cv;
+    *reinterpret_cast<uint2 *>(step + (t * 4 + j) * 32 + m * 8) = make_uint2(w0 ^ 0x80808080u, w1 ^ 0x80808080u);
     const int qs = (int)__builtin_amdgcn_udot4(w0, 0x01010101u, __builtin_amdgcn_udot4(w1, 0x01010101u, 0u, false), false) - 1024;
     float fs = (float)qs;
     fs += dpp_f<DPP_XOR1>(fs);
     fs += dpp_f<DPP_XOR2>(fs);
-    if (m == 0) {
-        uint64_t *sq = reinterpret_cast<uint64_t *>(step + TOK * 128 + (t * 4 + j) * 8);
-        const uint64_t sv = ((uint64_t)__float_as_uint(d * fs) << 32) | __float_as_uint(d);
-        if constexpr (WT) __hip_atomic_store(sq, sv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else *sq = sv;
-    }
+    if (m == 0) *reinterpret_cast<float2 *>(step + TOK * 128 + (t * 4 + j) * 8) = make_float2(d, d * fs);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -635,7 +625,7 @@ __global__ __launch_bounds__(TOK * 16) void mma_prequant(const MmArgs a, uint8_t
 // waits for its load). Each step loads its weights D - 1 steps ahead; all weight addresses are
 // per-lane constants plus the step's descriptor base (scalar arithmetic).
 template <int T, int TOK, int RT, int NSTEP, bool PR>
-__global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a, uint8_t *__restrict__ img, int n_steps, int part_steps, int *sync) {
+__global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a, const uint8_t *__restrict__ img, int n_steps, int part_steps) {
     using W = MmaW<T, TOK>;
     static_assert(!PR || ((T == T_Q4_0 || T == T_Q8_0) && NSTEP % 2 == 0), "paired steps: Q4_0 / Q8_0, even runs");
     constexpr int G = 16 / TOK;   // block groups per MFMA
@@ -660,13 +650,7 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
     const uint8_t *wtile = a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03 + (int64_t)row0 * a.nb01;
     const uint32_t nb01 = (uint32_t)a.nb01;
     const uint32_t tile_bytes = (uint32_t)(min(16 * RT, a.N - row0) - 1) * nb01 + (uint32_t)(a.K / QT<T>::blck) * QT<T>::bytes;
-#if MMA_EXP & 4   // (measurement: Q4_K weight loads of 8 rows x 128 contiguous bytes per instruction)
-    const uint32_t xrow = (uint32_t)((lane >> 3) + 8 * (wave & 1)) * nb01;   // (a wave pair: both halves of 16 rows)
-    const MmaLanes lo0 = T == T_Q4_K ? MmaLanes{xrow, xrow + 16 + 16 * (lane & 7), 0}
-                                     : W::lanes(c, g, wave & 1, nb01, (uint32_t)(reinterpret_cast<uintptr_t>(wtile) & 3));
-#else
     const MmaLanes lo0 = W::lanes(c, g, wave & 1, nb01, (uint32_t)(reinterpret_cast<uintptr_t>(wtile) & 3));
-#endif
     MmaLanes lo[RT];
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
@@ -688,47 +672,10 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
         __builtin_amdgcn_make_buffer_rsrc((void *)(img + ((int64_t)z * n_steps + s0) * SB), 0, nbx, MMA_RSRC_W3);
     constexpr int NP = (MMA_KS * NSTEP * SB + 16383) / 16384;
     uint32_t stg[NP][4];
-    // sync != nullptr (one K part, one slice): the column pre-pass runs in this launch. Workgroup b
-    // quantizes steps b, b + grid, ... into the image with write-through (sc1) stores, every
-    // storing wave drains them, and one lane adds the workgroup's step count to sync[0]; the image
-    // is then read with sc1 loads once sync[0] = n_steps (MI355X_MICROARCH.md inter-workgroup
-    // visibility, the single-counter form). Each workgroup produces before it waits, and issues
-    // its first weight loads before it waits, so the hand-off overlaps the weight stream's start
-    // instead of costing a launch. sync[32] counts the workgroups past the wait; the last one
-    // re-arms both counters for the next launch. The poll is bounded (a stale counter would give
-    // wrong sums, never a hang).
-    const bool fused = sync != nullptr;
-    if (fused) {
-        const int nwg = gridDim.x;
-        if (threadIdx.x < TOK * 16) {
-            const int m = threadIdx.x & 3, j = (threadIdx.x >> 2) & 3, t = threadIdx.x >> 4;
-            const float *col = reinterpret_cast<const float *>(a.x + (int64_t)min(t, a.M - 1) * a.nb11);
-            for (int st = blockIdx.x; st < n_steps; st += nwg) {
-                float v[8];
-                if (a.x_aligned16) mma_xload<true>(a, col, st, j, m, v);
-                else mma_xload<false>(a, col, st, j, m, v);
-                mma_quant<TOK, true>(a, v, st, j, t, m, img + (int64_t)st * SB);
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        lds_barrier();
-        const int mine = blockIdx.x < n_steps ? (n_steps - 1 - (int)blockIdx.x) / nwg + 1 : 0;
-        if (threadIdx.x == 0 && mine > 0) __hip_atomic_fetch_add(sync, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    auto issue_x = [&]() __attribute__((always_inline)) {
-        if constexpr (!(MMA_EXP & 1)) {
+    if constexpr (!(MMA_EXP & 1)) {
 #pragma unroll
-            for (int k = 0; k < NP; ++k) {
-                if (fused) {   // (sc1: the other workgroups' write-through stores)
-                    const mma_u4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, threadIdx.x * 16 + k * 16384, 0, MMA_SC1);
-                    stg[k][0] = v[0]; stg[k][1] = v[1]; stg[k][2] = v[2]; stg[k][3] = v[3];
-                } else {
-                    bl16(xr, threadIdx.x * 16 + k * 16384, stg[k]);
-                }
-            }
-        }
-    };
-    if (!fused) issue_x();
+        for (int k = 0; k < NP; ++k) bl16(xr, threadIdx.x * 16 + k * 16384, stg[k]);
+    }
     // B role: column c = token bt of block group bg; codes only where k-group g is in bg's range
     // (the other lanes read the zero bytes after the image, at a fixed address)
     const int bt = c % TOK, bg = c / TOK;
@@ -840,16 +787,6 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
     };
 
     auto stage_x = [&]() __attribute__((always_inline)) {
-        if (fused) {
-            if (threadIdx.x == 0) {
-                for (int spin = 0; spin < (1 << 22); ++spin) {
-                    if (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= n_steps) break;
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            lds_barrier();
-            issue_x();
-        }
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
             const uint32_t o = threadIdx.x * 16 + k * 16384;
@@ -860,11 +797,6 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
         }
         if (threadIdx.x < 8) *reinterpret_cast<uint4 *>(xl + nbx + threadIdx.x * 16) = make_uint4(0, 0, 0, 0);
         lds_barrier();
-        if (fused && threadIdx.x == 0 &&
-            __hip_atomic_fetch_add(sync + 32, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
-            __hip_atomic_store(sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (every workgroup is past its poll)
-            __hip_atomic_store(sync + 32, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
     };
     if constexpr (!PR) {
         W F[D][RT];
@@ -1052,10 +984,6 @@ static MmaPlan mma_plan(int type, const MmArgs &a) {
     return p;
 }
 
-// the column pre-pass inside the main launch: one K part (two parts add into a dst the pre-pass
-// zeroes first) and one batch slice (GGML_MI355X_MMA_FUSE=0: always its own launch)
-static bool mma_fused(const MmArgs &a, int kh) { return settings().mma_fuse != 0 && kh == 1 && a.ne12 * a.ne13 == 1; }
-
 // the plan keeps the K range in one part (dispatch.cpp use_mma)
 bool mmvq_mma_one_part(int type, const MmArgs &a) { return mma_plan(type, a).kh == 1; }
 
@@ -1072,8 +1000,7 @@ std::string mmvq_mma_plan_text(int type, const MmArgs &a) {
     int rt = pl.rt;
     if (type == T_Q5_K || type == T_Q6_K || (type == T_Q8_0 && pl.pr)) rt = 1;
     return "mma tok=" + std::to_string(mma_tok_of(a)) + " kh=" + std::to_string(pl.kh) + " rt=" + std::to_string(rt) +
-           (pl.pr ? " paired" : "") + " run=" + std::to_string(mma_run_len(part, pl.pr)) + (mma_fused(a, pl.kh) ? " fused" : "") +
-           " cols=" + std::to_string(a.M);
+           (pl.pr ? " paired" : "") + " run=" + std::to_string(mma_run_len(part, pl.pr)) + " cols=" + std::to_string(a.M);
 }
 
 size_t mmvq_mma_img_bytes(int, const MmArgs &a) {
@@ -1081,7 +1008,7 @@ size_t mmvq_mma_img_bytes(int, const MmArgs &a) {
 }
 
 template <int T, int TOK, int RT, int NS, bool PR>
-static hipError_t mma_main(const MmArgs &a, uint8_t *img, int S, int part, int kh, int *sync, hipStream_t st) {
+static hipError_t mma_main(const MmArgs &a, const uint8_t *img, int S, int part, int kh, hipStream_t st) {
     constexpr int IMG = mma_lds_img(MmaW<T, TOK>::NSC, TOK, RT);
     if constexpr (MMA_KS * NS * mma_step_bytes<TOK>() > IMG + 16 * mma_step_bytes<TOK>()) {
         return hipErrorInvalidValue;   // (runs whose image cannot fit: never selected)
@@ -1091,69 +1018,64 @@ static hipError_t mma_main(const MmArgs &a, uint8_t *img, int S, int part, int k
         static LdsAttr attr;   // per instantiation and device; > 64 KB of dynamic LDS needs the attribute
         if (lds > 64 * 1024)
             if (const hipError_t e = lds_attr_once(reinterpret_cast<const void *>(kern), attr); e != hipSuccess) return e;
-        hipLaunchKernelGGL(kern, dim3((a.N + 16 * RT - 1) / (16 * RT), a.ne12 * a.ne13, kh), dim3(MMA_KS * WAVE), lds, st, a, img, S, part, sync);
+        hipLaunchKernelGGL(kern, dim3((a.N + 16 * RT - 1) / (16 * RT), a.ne12 * a.ne13, kh), dim3(MMA_KS * WAVE), lds, st, a, img, S, part);
         return hipSuccess;
     }
 }
 
 template <int T, int TOK, int RT, bool PR>
-static hipError_t mma_run(const MmArgs &a, uint8_t *img, int S, int part, int kh, int *sync, hipStream_t st) {
+static hipError_t mma_run(const MmArgs &a, const uint8_t *img, int S, int part, int kh, hipStream_t st) {
     switch (mma_run_len(part, PR)) {   // (pairs: even runs)
-        case 1: if constexpr (!PR) return mma_main<T, TOK, RT, 1, PR>(a, img, S, part, kh, sync, st); else break;
-        case 2: return mma_main<T, TOK, RT, 2, PR>(a, img, S, part, kh, sync, st);
-        case 3: if constexpr (!PR) return mma_main<T, TOK, RT, 3, PR>(a, img, S, part, kh, sync, st); else break;
-        case 4: return mma_main<T, TOK, RT, 4, PR>(a, img, S, part, kh, sync, st);
-        case 5: if constexpr (!PR) return mma_main<T, TOK, RT, 5, PR>(a, img, S, part, kh, sync, st); else break;
-        case 6: return mma_main<T, TOK, RT, 6, PR>(a, img, S, part, kh, sync, st);
-        case 7: if constexpr (!PR) return mma_main<T, TOK, RT, 7, PR>(a, img, S, part, kh, sync, st); else break;
-        case 8: return mma_main<T, TOK, RT, 8, PR>(a, img, S, part, kh, sync, st);
-        case 10: return mma_main<T, TOK, RT, 10, PR>(a, img, S, part, kh, sync, st);
-        case 12: return mma_main<T, TOK, RT, 12, PR>(a, img, S, part, kh, sync, st);
-        case 14: return mma_main<T, TOK, RT, 14, PR>(a, img, S, part, kh, sync, st);
+        case 1: if constexpr (!PR) return mma_main<T, TOK, RT, 1, PR>(a, img, S, part, kh, st); else break;
+        case 2: return mma_main<T, TOK, RT, 2, PR>(a, img, S, part, kh, st);
+        case 3: if constexpr (!PR) return mma_main<T, TOK, RT, 3, PR>(a, img, S, part, kh, st); else break;
+        case 4: return mma_main<T, TOK, RT, 4, PR>(a, img, S, part, kh, st);
+        case 5: if constexpr (!PR) return mma_main<T, TOK, RT, 5, PR>(a, img, S, part, kh, st); else break;
+        case 6: return mma_main<T, TOK, RT, 6, PR>(a, img, S, part, kh, st);
+        case 7: if constexpr (!PR) return mma_main<T, TOK, RT, 7, PR>(a, img, S, part, kh, st); else break;
+        case 8: return mma_main<T, TOK, RT, 8, PR>(a, img, S, part, kh, st);
+        case 10: return mma_main<T, TOK, RT, 10, PR>(a, img, S, part, kh, st);
+        case 12: return mma_main<T, TOK, RT, 12, PR>(a, img, S, part, kh, st);
+        case 14: return mma_main<T, TOK, RT, 14, PR>(a, img, S, part, kh, st);
         default: break;
     }
     return hipErrorInvalidValue;
 }
 
 template <int T, int TOK>
-static hipError_t mma_tok(const MmArgs &a, uint8_t *img, int *counters, hipStream_t st) {
+static hipError_t mma_tok(const MmArgs &a, uint8_t *img, hipStream_t st) {
     const MmaPlan pl = mma_plan(T, a);
     const int S = mma_steps(a), kh = pl.kh, part = mma_part_steps(a, kh);
     const dim3 pg(S, a.ne12 * a.ne13);
-    int *sync = counters != nullptr && mma_fused(a, pl.kh) ? counters : nullptr;
     if (settings().diag & 256) {   // (measurement: no pre-pass)
-        sync = nullptr;
-    } else if (sync) {             // (the pre-pass runs inside the main launch)
     } else if (a.x_aligned16) hipLaunchKernelGGL((mma_prequant<TOK, true>), pg, dim3(TOK * 16), 0, st, a, img, kh == 2);
     else hipLaunchKernelGGL((mma_prequant<TOK, false>), pg, dim3(TOK * 16), 0, st, a, img, kh == 2);
     hipError_t e;
-    if constexpr (T == T_Q5_K || T == T_Q6_K) e = mma_run<T, TOK, 1, false>(a, img, S, part, kh, sync, st);
+    if constexpr (T == T_Q5_K || T == T_Q6_K) e = mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
     else if constexpr (T == T_Q8_0) {
-        if (pl.pr) e = mma_run<T, TOK, 1, true>(a, img, S, part, kh, sync, st);   // (two tiles of pairs would spill)
-        else e = pl.rt == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, sync, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, sync, st);
+        if (pl.pr) e = mma_run<T, TOK, 1, true>(a, img, S, part, kh, st);   // (two tiles of pairs would spill)
+        else e = pl.rt == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
     } else if constexpr (T == T_Q4_0) {
-        if (pl.pr) e = pl.rt == 2 ? mma_run<T, TOK, 2, true>(a, img, S, part, kh, sync, st) : mma_run<T, TOK, 1, true>(a, img, S, part, kh, sync, st);
-        else e = pl.rt == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, sync, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, sync, st);
-    } else e = pl.rt == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, sync, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, sync, st);
+        if (pl.pr) e = pl.rt == 2 ? mma_run<T, TOK, 2, true>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, true>(a, img, S, part, kh, st);
+        else e = pl.rt == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
+    } else e = pl.rt == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
     return e != hipSuccess ? e : hipGetLastError();
 }
 
 template <int T>
-static hipError_t mma_type(const MmArgs &a, uint8_t *img, int *counters, hipStream_t st) {
-    return mma_tok_of(a) == 4 ? mma_tok<T, 4>(a, img, counters, st) : mma_tok<T, 8>(a, img, counters, st);
+static hipError_t mma_type(const MmArgs &a, uint8_t *img, hipStream_t st) {
+    return mma_tok_of(a) == 4 ? mma_tok<T, 4>(a, img, st) : mma_tok<T, 8>(a, img, st);
 }
 
-// plain MUL_MAT with 1 <= M <= 8 columns (mmvq_mma_supported), img = mmvq_mma_img_bytes of scratch;
-// counters: two zeroed ints 128 B apart that every launch leaves zero (nullptr: the pre-pass as
-// a launch of its own)
-hipError_t mmvq_mma_launch(int type, const MmArgs &a, uint8_t *img, int *counters, hipStream_t st) {
+// plain MUL_MAT with 1 <= M <= 8 columns (mmvq_mma_supported), img = mmvq_mma_img_bytes of scratch
+hipError_t mmvq_mma_launch(int type, const MmArgs &a, uint8_t *img, hipStream_t st) {
     if (!mmvq_mma_supported(type, a) || img == nullptr) return hipErrorInvalidValue;
     switch (type) {
-        case T_Q4_0: return mma_type<T_Q4_0>(a, img, counters, st);
-        case T_Q8_0: return mma_type<T_Q8_0>(a, img, counters, st);
-        case T_Q4_K: return mma_type<T_Q4_K>(a, img, counters, st);
-        case T_Q5_K: return mma_type<T_Q5_K>(a, img, counters, st);
-        case T_Q6_K: return mma_type<T_Q6_K>(a, img, counters, st);
+        case T_Q4_0: return mma_type<T_Q4_0>(a, img, st);
+        case T_Q8_0: return mma_type<T_Q8_0>(a, img, st);
+        case T_Q4_K: return mma_type<T_Q4_K>(a, img, st);
+        case T_Q5_K: return mma_type<T_Q5_K>(a, img, st);
+        case T_Q6_K: return mma_type<T_Q6_K>(a, img, st);
         default: return hipErrorInvalidValue;
     }
 }

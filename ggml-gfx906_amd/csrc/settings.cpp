@@ -31,7 +31,6 @@ static Settings load_settings() {
     s.mma = i("GGML_MI355X_MMA", -1);
     s.mma_pair = i("GGML_MI355X_MMA_PAIR", -1);
     s.mma_kh = i("GGML_MI355X_MMA_KH", 0);
-    s.mma_fuse = i("GGML_MI355X_MMA_FUSE", 1);
     s.mma_rt = i("GGML_MI355X_MMA_RT", 0);
     s.solo = i("GGML_MI355X_SOLO", -1);
     s.mmq_repack_min = i("GGML_MI355X_MMQ_REPACK_MIN", 1 << 30);

@@ -24,7 +24,6 @@ struct Settings {
     int mma_pair = -1;            // GGML_MI355X_MMA_PAIR: 0/1 force unpaired / paired steps (-1 plan)
     int mma_kh = 0;               // GGML_MI355X_MMA_KH: 1 / 2 force one / two K parts (0 plan)
     int mma_rt = 0;               // GGML_MI355X_MMA_RT: 1/2 row tiles per workgroup (0 plan)
-    int mma_fuse = 1;             // GGML_MI355X_MMA_FUSE: 0 = the column pre-pass as its own launch
     int solo = -1;                // GGML_MI355X_SOLO: single-wave kernel for one column (-1 rule, 0 off, 1 on, n rows per wave)
     // ---- mat-mat (ne11 > 8)
     int mmq_repack_min = 1 << 30; // GGML_MI355X_MMQ_REPACK_MIN: per-call repack from this many tokens (0 never)

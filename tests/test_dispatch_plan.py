@@ -52,38 +52,38 @@ PLANS = {
 PERF = {
     ("q4_0", 1): "ring nc=1 rpw=1 cols=1",
     ("q4_0", 2): "ring nc=2 rpw=2 cols=2",
-    ("q4_0", 3): "mma tok=4 kh=1 rt=1 paired run=8 fused cols=3",
-    ("q4_0", 4): "mma tok=4 kh=1 rt=1 paired run=8 fused cols=4",
-    ("q4_0", 5): "mma tok=8 kh=1 rt=1 paired run=8 fused cols=5",
-    ("q4_0", 8): "mma tok=8 kh=1 rt=1 paired run=8 fused cols=8",
+    ("q4_0", 3): "mma tok=4 kh=1 rt=1 paired run=8 cols=3",
+    ("q4_0", 4): "mma tok=4 kh=1 rt=1 paired run=8 cols=4",
+    ("q4_0", 5): "mma tok=8 kh=1 rt=1 paired run=8 cols=5",
+    ("q4_0", 8): "mma tok=8 kh=1 rt=1 paired run=8 cols=8",
     ("q4_0", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
     ("q8_0", 1): "ring nc=1 rpw=1 cols=1",
     ("q8_0", 2): "ring nc=2 rpw=2 cols=2",
-    ("q8_0", 3): "mma tok=4 kh=1 rt=1 paired run=8 fused cols=3",
-    ("q8_0", 4): "mma tok=4 kh=1 rt=1 paired run=8 fused cols=4",
-    ("q8_0", 5): "mma tok=8 kh=1 rt=1 paired run=8 fused cols=5",
-    ("q8_0", 8): "mma tok=8 kh=1 rt=1 paired run=8 fused cols=8",
+    ("q8_0", 3): "mma tok=4 kh=1 rt=1 paired run=8 cols=3",
+    ("q8_0", 4): "mma tok=4 kh=1 rt=1 paired run=8 cols=4",
+    ("q8_0", 5): "mma tok=8 kh=1 rt=1 paired run=8 cols=5",
+    ("q8_0", 8): "mma tok=8 kh=1 rt=1 paired run=8 cols=8",
     ("q8_0", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
     ("q4_K", 1): "ring nc=1 rpw=2 cols=1",
     ("q4_K", 2): "ring nc=2 rpw=2 cols=2",
-    ("q4_K", 3): "mma tok=4 kh=1 rt=1 run=7 fused cols=3",
-    ("q4_K", 4): "mma tok=4 kh=1 rt=1 run=7 fused cols=4",
-    ("q4_K", 5): "mma tok=8 kh=1 rt=1 run=7 fused cols=5",
-    ("q4_K", 8): "mma tok=8 kh=1 rt=1 run=7 fused cols=8",
+    ("q4_K", 3): "mma tok=4 kh=1 rt=1 run=7 cols=3",
+    ("q4_K", 4): "mma tok=4 kh=1 rt=1 run=7 cols=4",
+    ("q4_K", 5): "mma tok=8 kh=1 rt=1 run=7 cols=5",
+    ("q4_K", 8): "mma tok=8 kh=1 rt=1 run=7 cols=8",
     ("q4_K", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
     ("q5_K", 1): "ring nc=1 rpw=2 cols=1",
     ("q5_K", 2): "ring nc=2 rpw=2 cols=2",
-    ("q5_K", 3): "mma tok=4 kh=1 rt=1 run=7 fused cols=3",
-    ("q5_K", 4): "mma tok=4 kh=1 rt=1 run=7 fused cols=4",
-    ("q5_K", 5): "mma tok=8 kh=1 rt=1 run=7 fused cols=5",
-    ("q5_K", 8): "mma tok=8 kh=1 rt=1 run=7 fused cols=8",
+    ("q5_K", 3): "mma tok=4 kh=1 rt=1 run=7 cols=3",
+    ("q5_K", 4): "mma tok=4 kh=1 rt=1 run=7 cols=4",
+    ("q5_K", 5): "mma tok=8 kh=1 rt=1 run=7 cols=5",
+    ("q5_K", 8): "mma tok=8 kh=1 rt=1 run=7 cols=8",
     ("q5_K", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
     ("q6_K", 1): "ring nc=1 rpw=1 cols=1",
     ("q6_K", 2): "ring nc=2 rpw=1 cols=2",
-    ("q6_K", 3): "mma tok=4 kh=1 rt=1 run=7 fused cols=3",
-    ("q6_K", 4): "mma tok=4 kh=1 rt=1 run=7 fused cols=4",
-    ("q6_K", 5): "mma tok=8 kh=1 rt=1 run=7 fused cols=5",
-    ("q6_K", 8): "mma tok=8 kh=1 rt=1 run=7 fused cols=8",
+    ("q6_K", 3): "mma tok=4 kh=1 rt=1 run=7 cols=3",
+    ("q6_K", 4): "mma tok=4 kh=1 rt=1 run=7 cols=4",
+    ("q6_K", 5): "mma tok=8 kh=1 rt=1 run=7 cols=5",
+    ("q6_K", 8): "mma tok=8 kh=1 rt=1 run=7 cols=8",
     ("q6_K", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
 }
 
@@ -92,28 +92,28 @@ PERF = {
 # sweep profiles/r06_mma_plan_sweep.txt): (name, K, N, columns) -> plan text
 MMA_RULE = {
     ("q4_0", 4096, 4096, 4): "mmvq nc=4 lpr=64 rpw=2 grid=256x1x1",           # small: VALU up to 4
-    ("q4_0", 4096, 4096, 5): "mma tok=8 kh=1 rt=1 paired run=2 fused cols=5",       # one K part, one tile
-    ("q4_0", 8192, 8192, 3): "mma tok=4 kh=1 rt=2 paired run=4 fused cols=3",       # two tiles at N, K >= 8192
-    ("q4_0", 4096, 14336, 8): "mma tok=8 kh=1 rt=2 paired run=2 fused cols=8",      # two tiles at N >= 12288
-    ("q8_0", 11008, 4096, 3): "mma tok=4 kh=1 rt=1 run=6 fused cols=3",             # unpaired, one tile
+    ("q4_0", 4096, 4096, 5): "mma tok=8 kh=1 rt=1 paired run=2 cols=5",       # one K part, one tile
+    ("q4_0", 8192, 8192, 3): "mma tok=4 kh=1 rt=2 paired run=4 cols=3",       # two tiles at N, K >= 8192
+    ("q4_0", 4096, 14336, 8): "mma tok=8 kh=1 rt=2 paired run=2 cols=8",      # two tiles at N >= 12288
+    ("q8_0", 11008, 4096, 3): "mma tok=4 kh=1 rt=1 run=6 cols=3",             # unpaired, one tile
     ("q8_0", 8192, 4096, 4): "ring-pre nc=4 rpw=1 cols=4",                    # K < 11008: from 5
-    ("q8_0", 8192, 4096, 5): "mma tok=8 kh=1 rt=1 run=4 fused cols=5",
-    ("q4_K", 4096, 14336, 8): "mma tok=8 kh=1 rt=2 run=2 fused cols=8",
-    ("q4_K", 14336, 4096, 8): "mma tok=8 kh=1 rt=1 run=7 fused cols=8",             # one tile: one part fits
+    ("q8_0", 8192, 4096, 5): "mma tok=8 kh=1 rt=1 run=4 cols=5",
+    ("q4_K", 4096, 14336, 8): "mma tok=8 kh=1 rt=2 run=2 cols=8",
+    ("q4_K", 14336, 4096, 8): "mma tok=8 kh=1 rt=1 run=7 cols=8",             # one tile: one part fits
     ("q4_K", 24576, 4096, 8): "mma tok=8 kh=2 rt=2 run=6 cols=8",             # image past LDS: two parts
     ("q4_K", 28672, 4096, 8): "ring-pre nc=8 rpw=1 cols=8",                   # no part size fits: VALU
     ("q5_K", 4096, 4096, 5): "mma tok=8 kh=2 rt=1 run=1 cols=5",              # Q5_K small: two parts
-    ("q5_K", 8192, 4096, 5): "mma tok=8 kh=1 rt=1 run=4 fused cols=5",
-    ("q5_K", 14336, 4096, 3): "mma tok=4 kh=1 rt=1 run=7 fused cols=3",
-    ("q5_K", 14336, 4096, 5): "mma tok=8 kh=1 rt=1 run=7 fused cols=5",
+    ("q5_K", 8192, 4096, 5): "mma tok=8 kh=1 rt=1 run=4 cols=5",
+    ("q5_K", 14336, 4096, 3): "mma tok=4 kh=1 rt=1 run=7 cols=3",
+    ("q5_K", 14336, 4096, 5): "mma tok=8 kh=1 rt=1 run=7 cols=5",
     ("q5_K", 28672, 4096, 3): "ring-pre nc=4 rpw=1 cols=3",                   # past K = 16384: VALU to 7
     # Q6_K (round 6, profiles/r06_q6k_mma.txt)
     ("q6_K", 4096, 4096, 3): "mmvq nc=3 lpr=64 rpw=1 grid=512x1x1",           # K < 8192: from 5
     ("q6_K", 4096, 4096, 5): "mma tok=8 kh=2 rt=1 run=1 cols=5",              # small: two parts
     ("q6_K", 11008, 4096, 5): "ring-pre nc=8 rpw=1 cols=5",                   # 8192 <= K < 12288, N < 8192: 8
-    ("q6_K", 11008, 4096, 8): "mma tok=8 kh=1 rt=1 run=6 fused cols=8",
-    ("q6_K", 8192, 8192, 3): "mma tok=4 kh=1 rt=1 run=4 fused cols=3",              # N >= 8192: from 3
-    ("q6_K", 28672, 4096, 3): "mma tok=4 kh=1 rt=1 run=14 fused cols=3",
+    ("q6_K", 11008, 4096, 8): "mma tok=8 kh=1 rt=1 run=6 cols=8",
+    ("q6_K", 8192, 8192, 3): "mma tok=4 kh=1 rt=1 run=4 cols=3",              # N >= 8192: from 3
+    ("q6_K", 28672, 4096, 3): "mma tok=4 kh=1 rt=1 run=14 cols=3",
     ("q6_K", 28672, 4096, 8): "mma tok=8 kh=2 rt=1 run=7 cols=8",             # image past LDS: two parts
 }
 

@@ -185,24 +185,3 @@ def test_mma_paired_steps(mm, t, M_, K):
     assert np.array_equal(g1.view(np.uint32), g2.view(np.uint32)), "result not repeatable"
     valu = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 0})
     assert qref.nmse(g1, valu) <= 1e-10
-
-
-@pytest.mark.parametrize("t,N,M_,K", [(qref.Q4_0, 200, 8, 14336), (qref.Q4_K, 32, 3, 14336), (qref.Q6_K, 4096, 5, 4096),
-                                      (qref.Q8_0, 64, 4, 28672), (qref.Q5_K, 100, 8, 8192)],
-                         ids=["q4_0", "q4_K-2wg", "q6_K", "q8_0-4wg", "q5_K"])
-def test_mma_in_launch_prepass(mm, t, N, M_, K):
-    """the column pre-pass inside the main launch (GGML_MI355X_MMA_FUSE, on by default for one K
-    part and one batch slice): the workgroups quantize the image steps, publish them through a
-    counter and read them back, so the image holds the bytes the pre-pass launch writes and the
-    result is bit-identical to it; three calls in a row (the last workgroup re-arms the counters);
-    fewer workgroups than steps (N = 32: 2 workgroups of 56 steps each; N = 64 at K = 28672: 4
-    of 56)"""
-    a, b, out_ne = operands(t, N, M_, K, 17)
-    env = {"GGML_MI355X_MMA": 1}
-    fused = [run_with(mm, a, b, out_ne, env) for _ in range(3)]
-    sep = run_with(mm, a, b, out_ne, {**env, "GGML_MI355X_MMA_FUSE": 0})
-    assert np.all(np.isfinite(sep))
-    for g in fused:
-        assert np.array_equal(g.view(np.uint32), sep.view(np.uint32)), "in-launch pre-pass differs from the pre-pass launch"
-    valu = run_with(mm, a, b, out_ne, {"GGML_MI355X_MMA": 0})
-    assert qref.nmse(sep, valu) <= 1e-10
