@@ -37,7 +37,8 @@
 #include <type_traits>
 
 // measurement builds only (scripts/mma_exp.sh; results wrong by design): bit 1 = no activation
-// loads (pre-pass and records), bit 2 = no weight loads
+// loads (pre-pass and records), bit 2 = no weight loads, bit 4 = Q4_K weight loads reading 8 rows x
+// 128 contiguous bytes per instruction (scripts/gpu_r06_rowc.sh)
 #ifndef MMA_EXP
 #define MMA_EXP 0
 #endif
@@ -650,7 +651,13 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
     const uint8_t *wtile = a.w + (int64_t)(i12 / a.r2) * a.nb02 + (int64_t)(i13 / a.r3) * a.nb03 + (int64_t)row0 * a.nb01;
     const uint32_t nb01 = (uint32_t)a.nb01;
     const uint32_t tile_bytes = (uint32_t)(min(16 * RT, a.N - row0) - 1) * nb01 + (uint32_t)(a.K / QT<T>::blck) * QT<T>::bytes;
+#if MMA_EXP & 4   // (measurement: Q4_K weight loads of 8 rows x 128 contiguous bytes per instruction)
+    const uint32_t xrow = (uint32_t)((lane >> 3) + 8 * (wave & 1)) * nb01;   // (a wave pair: both halves of 16 rows)
+    const MmaLanes lo0 = T == T_Q4_K ? MmaLanes{xrow, xrow + 16 + 16 * (lane & 7), 0}
+                                     : W::lanes(c, g, wave & 1, nb01, (uint32_t)(reinterpret_cast<uintptr_t>(wtile) & 3));
+#else
     const MmaLanes lo0 = W::lanes(c, g, wave & 1, nb01, (uint32_t)(reinterpret_cast<uintptr_t>(wtile) & 3));
+#endif
     MmaLanes lo[RT];
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
