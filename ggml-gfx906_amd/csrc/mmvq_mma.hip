@@ -575,6 +575,48 @@ template <int T, int TOK> struct MmaPair {
     }
 };
 
+// Q4_K paired steps (the two halves of a super-block): the 128 qs bytes of the tile's 16 rows are
+// loaded row-contiguously, 8 rows x 128 bytes per wave instruction (instruction i: lane l holds
+// row 8i + l / 8, piece l % 8), where the unpaired form gathers 16 rows x 64 bytes per instruction
+// per step (the gather shape costs 8-12 % of the kernel, profiles/r06_mma_rowcontig_exp.txt);
+// each lane then takes the piece MmaW<Q4_K> would have loaded for each half (piece 4h + g of row
+// c) by ds_bpermute from the instruction holding row c, and the 16-B header is loaded once for
+// both halves: 3 load instructions per super-block instead of 4.
+template <int TOK> struct MmaPair<T_Q4_K, TOK> {
+    uint32_t H[4], P0[4], P1[4];
+    __device__ static MmaLanes lanes(int r, int g, uint32_t nb01) {
+        const uint32_t tile = (uint32_t)(r & ~15) * nb01;
+        const int l = (r & 15) + 16 * g;
+        const uint32_t q = tile + (uint32_t)(l >> 3) * nb01 + 16 + 16 * (l & 7);
+        return {tile + (uint32_t)(r & 15) * nb01, q, q + 8 * nb01};
+    }
+    __device__ inline void load(__amdgpu_buffer_rsrc_t rs, const MmaLanes &lo) {
+        bl16(rs, lo.a, H);
+        bl16(rs, lo.b, P0);
+        bl16(rs, lo.c, P1);
+    }
+    __device__ inline void split(MmaW<T_Q4_K, TOK> &X, MmaW<T_Q4_K, TOK> &Y) {
+        pin(H);
+        pin(P0);
+        pin(P1);
+        const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+        const int src0 = 4 * (8 * (c & 7) + g), src1 = src0 + 16;   // (byte addresses: piece g, 4 + g)
+        const bool hi = c >= 8;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t a0 = __builtin_amdgcn_ds_bpermute(src0, P0[k]), b0 = __builtin_amdgcn_ds_bpermute(src0, P1[k]);
+            const uint32_t a1 = __builtin_amdgcn_ds_bpermute(src1, P0[k]), b1 = __builtin_amdgcn_ds_bpermute(src1, P1[k]);
+            X.QV[k] = hi ? b0 : a0;
+            Y.QV[k] = hi ? b1 : a1;
+            X.H[k] = Y.H[k] = H[k];
+        }
+        X.h = 0;
+        Y.h = 1;
+    }
+};
+template <int T, int TOK> struct PairHalfOf { using type = MmaHalf<T, TOK>; };
+template <int TOK> struct PairHalfOf<T_Q4_K, TOK> { using type = MmaW<T_Q4_K, TOK>; };
+
 // ------------------------------------------------------------------------------------------
 // step sets in flight per wave (D - 1 steps ahead), within the 128 VGPRs of 16 waves per CU
 #ifdef MMA_D
@@ -628,7 +670,7 @@ __global__ __launch_bounds__(TOK * 16) void mma_prequant(const MmArgs a, uint8_t
 template <int T, int TOK, int RT, int NSTEP, bool PR>
 __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a, const uint8_t *__restrict__ img, int n_steps, int part_steps) {
     using W = MmaW<T, TOK>;
-    static_assert(!PR || ((T == T_Q4_0 || T == T_Q8_0) && NSTEP % 2 == 0), "paired steps: Q4_0 / Q8_0, even runs");
+    static_assert(!PR || ((T == T_Q4_0 || T == T_Q8_0 || T == T_Q4_K) && NSTEP % 2 == 0), "paired steps: Q4_0 / Q8_0 / Q4_K, even runs");
     constexpr int G = 16 / TOK;   // block groups per MFMA
     constexpr int L = 4 / G;      // k-groups per block group
     constexpr int P = 4 / G;      // MFMA outputs per step
@@ -859,7 +901,7 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
                 load_x(X[(k + 1) % DP][1], step_of(2 * j + 3));
             }
             __builtin_amdgcn_sched_barrier(0);
-            MmaHalf<T, TOK> H0[RT], H1[RT];
+            typename PairHalfOf<T, TOK>::type H0[RT], H1[RT];
 #pragma unroll
             for (int t = 0; t < RT; ++t) F[k][t].split(H0[t], H1[t]);
             compute(H0, X[k][0], step_of(2 * j));
@@ -918,6 +960,7 @@ static int mma_part_steps(const MmArgs &a, int kh) {
 
 // Q4_0 / Q8_0 rows contiguous and 4-byte aligned (paired steps load aligned 36 / 68-byte windows)
 static bool mma_pair_aligned(int type, const MmArgs &a) {
+    if (type == T_Q4_K) return true;   // (rows loaded one by one: any row stride)
     if (type != T_Q4_0 && type != T_Q8_0) return false;
     const int64_t row = (int64_t)(a.K / 32) * (type == T_Q4_0 ? 18 : 34);
     return a.nb01 == row && row % 4 == 0 && a.nb02 % 4 == 0 && a.nb03 % 4 == 0 && (reinterpret_cast<uintptr_t>(a.w) & 3) == 0;
@@ -957,7 +1000,9 @@ static bool mma_part_fits(int type, const MmArgs &a, int part, bool pr, int rt) 
 // profiles/r06_mma_plan_sweep.txt; round 5 chose from eager launches, whose period the host's
 // launch rate bounded):
 //   pr  paired steps: Q4_0 always, Q8_0 below K = 8192 and from 12288 (at 11008 the unpaired
-//       form with two tiles wins), where the rows allow it;
+//       form with two tiles wins), where the rows allow it; Q4_K at 1..4 columns from K = 12288
+//       (28672 x 4096 at 3 columns 20.3 vs 22.3 us, 12288 x 4096 12.7 vs 13.1; even at 8192 and
+//       +6 % at 11008; at 5..8 columns the pairs are 6-10 % slower, profiles/r06_q4k_pairs.txt);
 //   kh  one K part wherever the whole column image fits the workgroup's LDS: 0.85-0.95x the
 //       two-part time (no dst zeroing in the pre-pass, no atomic adds, a wave walks twice the
 //       steps); two parts only for images that do not fit (e.g. Q4_0 at 5..8 columns from K =
@@ -977,7 +1022,9 @@ static MmaPlan mma_plan(int type, const MmArgs &a) {
     const int S = mma_steps(a);
     MmaPlan p;
     const int pe = settings().mma_pair;
-    const bool want = pe >= 0 ? pe == 1 : (type == T_Q4_0 || (type == T_Q8_0 && (a.K < 8192 || a.K >= 12288)));
+    const bool want = pe >= 0 ? pe == 1
+                              : (type == T_Q4_0 || (type == T_Q8_0 && (a.K < 8192 || a.K >= 12288)) ||
+                                 (type == T_Q4_K && a.M <= 4 && a.K >= 12288));
     p.pr = want && mma_pair_aligned(type, a);
     const bool two_ok = p.pr ? S >= 64 : S >= 32;
     const int ke = settings().mma_kh, re = settings().mma_rt;
@@ -1063,6 +1110,9 @@ static hipError_t mma_tok(const MmArgs &a, uint8_t *img, hipStream_t st) {
         if (pl.pr) e = mma_run<T, TOK, 1, true>(a, img, S, part, kh, st);   // (two tiles of pairs would spill)
         else e = pl.rt == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
     } else if constexpr (T == T_Q4_0) {
+        if (pl.pr) e = pl.rt == 2 ? mma_run<T, TOK, 2, true>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, true>(a, img, S, part, kh, st);
+        else e = pl.rt == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
+    } else if constexpr (T == T_Q4_K) {
         if (pl.pr) e = pl.rt == 2 ? mma_run<T, TOK, 2, true>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, true>(a, img, S, part, kh, st);
         else e = pl.rt == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
     } else e = pl.rt == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);

@@ -66,8 +66,8 @@ PERF = {
     ("q8_0", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
     ("q4_K", 1): "ring nc=1 rpw=2 cols=1",
     ("q4_K", 2): "ring nc=2 rpw=2 cols=2",
-    ("q4_K", 3): "mma tok=4 kh=1 rt=1 run=7 cols=3",
-    ("q4_K", 4): "mma tok=4 kh=1 rt=1 run=7 cols=4",
+    ("q4_K", 3): "mma tok=4 kh=1 rt=1 paired run=8 cols=3",
+    ("q4_K", 4): "mma tok=4 kh=1 rt=1 paired run=8 cols=4",
     ("q4_K", 5): "mma tok=8 kh=1 rt=1 run=7 cols=5",
     ("q4_K", 8): "mma tok=8 kh=1 rt=1 run=7 cols=8",
     ("q4_K", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
@@ -102,6 +102,8 @@ MMA_RULE = {
     ("q4_K", 14336, 4096, 8): "mma tok=8 kh=1 rt=1 run=7 cols=8",             # one tile: one part fits
     ("q4_K", 24576, 4096, 8): "mma tok=8 kh=2 rt=2 run=6 cols=8",             # image past LDS: two parts
     ("q4_K", 28672, 4096, 8): "ring-pre nc=8 rpw=1 cols=8",                   # no part size fits: VALU
+    ("q4_K", 28672, 4096, 3): "mma tok=4 kh=1 rt=1 paired run=14 cols=3",     # 1..4 columns from K = 12288: pairs
+    ("q4_K", 11008, 4096, 3): "mma tok=4 kh=1 rt=1 run=6 cols=3",
     ("q5_K", 4096, 4096, 5): "mma tok=8 kh=2 rt=1 run=1 cols=5",              # Q5_K small: two parts
     ("q5_K", 8192, 4096, 5): "mma tok=8 kh=1 rt=1 run=4 cols=5",
     ("q5_K", 14336, 4096, 3): "mma tok=4 kh=1 rt=1 run=7 cols=3",
