@@ -34,6 +34,7 @@ hipError_t mmvq_mma_launch(int type, const MmArgs &a, uint8_t *img, hipStream_t 
 size_t mmvq_mma_img_bytes(int type, const MmArgs &a);
 bool mmvq_mma_supported(int type, const MmArgs &a);
 bool mmvq_mma_one_part(int type, const MmArgs &a);
+bool mmvq_mma_paired(int type, const MmArgs &a);
 size_t mmvq_ring_img_bytes(const MmArgs &a, int nc);
 hipError_t dequant_launch(int type, const void *src, float *dst, int64_t n, hipStream_t st);
 struct RowsArgs {
@@ -214,7 +215,9 @@ static int ring_pre_min() {
 // (below K = 8192 the whole-K VALU kernel with 16-lane rows, mmvq.hip lanes_per_row, takes 3..4
 // columns: Q4_0 4096 x 14336 at 3 10.6 vs 14.7 us, Q4_K at 4 12.5 vs 17.2)
 //   Q5_K  K < 8192: 5; to K = 16384 3 where the plan keeps one K part (its image fits the LDS;
-//         elsewhere the VALU kernels win up to 7 columns: 27.4 vs 28.8 us at 28672 x 4096), and 8
+//         elsewhere the unpaired form loses to the VALU kernels up to 7 columns: 27.4 vs 28.8 us
+//         at 28672 x 4096), 3 at any K where the plan takes paired steps (28672 x 4096 at 3
+//         columns 23.4 vs 27.4, profiles/r06_q5k_pairs.txt), and 8
 //   Q6_K  K < 8192: 5; 3 from K = 12288, or from 8192 at N >= 8192; else 8 (profiles/r06_q6k_mma.txt:
 //         14336 x 4096 at 3..8 columns 18.0-18.4 vs 21.3-27.3 us, 4096 x 4096 at 5..8 9.7-9.9 vs
 //         13.2-14.2; at 11008 x 4096 the VALU kernels stay ahead to 5 columns)
@@ -235,7 +238,8 @@ static bool use_mma(int type, const MmArgs &g) {
             return cols >= (K >= 11008 || N >= 8192 ? 3 : 4);
         case T_Q8_0: return cols >= (K >= 11008 ? 3 : 5);
         case T_Q4_K: return cols >= (K >= 8192 ? 3 : 5);
-        case T_Q5_K: return K < 8192 ? cols >= 5 : cols >= 8 || (cols >= 3 && K <= 16384 && mmvq_mma_one_part(type, g));
+        case T_Q5_K:
+            return K < 8192 ? cols >= 5 : cols >= 8 || (cols >= 3 && ((K <= 16384 && mmvq_mma_one_part(type, g)) || mmvq_mma_paired(type, g)));
         case T_Q6_K: return cols >= (K >= 12288 || (K >= 8192 && N >= 8192) ? 3 : K >= 8192 ? 8 : 5);
         default: return false;
     }

@@ -33,7 +33,9 @@
 //  * weight loads go through a per-step buffer descriptor (scalar base, per-lane constant
 //    offsets; steps past K have no records, so they read zeros); the number of load
 //    instructions per step is what bounds the kernel, so Q4_0 / Q8_0 at long K
-//    load two adjacent blocks per lane for two steps at once (paired steps).
+//    load two adjacent blocks per lane for two steps at once (paired steps), and Q4_K at long K
+//    and 1..4 columns loads a super-block's qs row-contiguously and permutes it (MmaPair<T_Q4_K>);
+//  * Q6_K has a scale per 16 weights: one MFMA chain per 16-element half of a block (MmaW<T_Q6_K>).
 #include <type_traits>
 
 // measurement builds only (scripts/mma_exp.sh; results wrong by design): bit 1 = no activation
@@ -549,7 +551,7 @@ template <int T, int TOK> struct MmaPair {
     static constexpr int NV = T == T_Q4_0 ? 9 : 17;   // 36 / 68 bytes
     uint32_t V[NV];
     __device__ static MmaLanes lanes(int r, int g, uint32_t nb01) { return {r * nb01 + (2u * QT<T>::bytes) * g, 0, 0}; }
-    __device__ inline void load(__amdgpu_buffer_rsrc_t rs, const MmaLanes &lo) {
+    __device__ inline void load(__amdgpu_buffer_rsrc_t rs, const MmaLanes &lo, uint32_t) {
 #pragma unroll
         for (int k = 0; k + 4 <= NV; k += 4) bl16(rs, lo.a + 4 * k, V + k);
         V[NV - 1] = __builtin_amdgcn_raw_buffer_load_b32(rs, lo.a + 4 * (NV - 1), 0, 0);
@@ -582,23 +584,32 @@ template <int T, int TOK> struct MmaPair {
 // each lane then takes the piece MmaW<Q4_K> would have loaded for each half (piece 4h + g of row
 // c) by ds_bpermute from the instruction holding row c, and the 16-B header is loaded once for
 // both halves: 3 load instructions per super-block instead of 4.
-template <int TOK> struct MmaPair<T_Q4_K, TOK> {
-    uint32_t H[4], P0[4], P1[4];
+// Q5_K likewise (qs at 48), its qh piece (half g & 1 of the 32 qh bytes, the same for both halves
+// of the super-block) loaded once per super-block too: 4 load instructions instead of 6.
+template <int T, int TOK> struct MmaPairK {
+    static constexpr bool QH = T == T_Q5_K;
+    static constexpr uint32_t QS = QH ? 48 : 16;
+    uint32_t H[4], P0[4], P1[4], QHV[QH ? 4 : 1];
     __device__ static MmaLanes lanes(int r, int g, uint32_t nb01) {
-        const uint32_t tile = (uint32_t)(r & ~15) * nb01;
+        const uint32_t tile = (uint32_t)(r & ~15) * nb01, row = tile + (uint32_t)(r & 15) * nb01;
         const int l = (r & 15) + 16 * g;
-        const uint32_t q = tile + (uint32_t)(l >> 3) * nb01 + 16 + 16 * (l & 7);
-        return {tile + (uint32_t)(r & 15) * nb01, q, q + 8 * nb01};
+        return {row, tile + (uint32_t)(l >> 3) * nb01 + QS + 16 * (l & 7), row + 16 + 16 * (g & 1)};
     }
-    __device__ inline void load(__amdgpu_buffer_rsrc_t rs, const MmaLanes &lo) {
+    __device__ inline void load(__amdgpu_buffer_rsrc_t rs, const MmaLanes &lo, uint32_t nb01) {
         bl16(rs, lo.a, H);
         bl16(rs, lo.b, P0);
-        bl16(rs, lo.c, P1);
+        bl16(rs, lo.b + 8 * nb01, P1);
+        if constexpr (QH) bl16(rs, lo.c, QHV);
     }
-    __device__ inline void split(MmaW<T_Q4_K, TOK> &X, MmaW<T_Q4_K, TOK> &Y) {
+    __device__ inline void split(MmaW<T, TOK> &X, MmaW<T, TOK> &Y) {
         pin(H);
         pin(P0);
         pin(P1);
+        if constexpr (QH) {
+            pin(QHV);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) X.QHV[k] = Y.QHV[k] = QHV[k];
+        }
         const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
         const int src0 = 4 * (8 * (c & 7) + g), src1 = src0 + 16;   // (byte addresses: piece g, 4 + g)
         const bool hi = c >= 8;
@@ -614,8 +625,9 @@ template <int TOK> struct MmaPair<T_Q4_K, TOK> {
         Y.h = 1;
     }
 };
-template <int T, int TOK> struct PairHalfOf { using type = MmaHalf<T, TOK>; };
-template <int TOK> struct PairHalfOf<T_Q4_K, TOK> { using type = MmaW<T_Q4_K, TOK>; };
+template <int T, int TOK> struct PairOf { using type = MmaPair<T, TOK>; using half = MmaHalf<T, TOK>; };
+template <int TOK> struct PairOf<T_Q4_K, TOK> { using type = MmaPairK<T_Q4_K, TOK>; using half = MmaW<T_Q4_K, TOK>; };
+template <int TOK> struct PairOf<T_Q5_K, TOK> { using type = MmaPairK<T_Q5_K, TOK>; using half = MmaW<T_Q5_K, TOK>; };
 
 // ------------------------------------------------------------------------------------------
 // step sets in flight per wave (D - 1 steps ahead), within the 128 VGPRs of 16 waves per CU
@@ -670,7 +682,7 @@ __global__ __launch_bounds__(TOK * 16) void mma_prequant(const MmArgs a, uint8_t
 template <int T, int TOK, int RT, int NSTEP, bool PR>
 __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a, const uint8_t *__restrict__ img, int n_steps, int part_steps) {
     using W = MmaW<T, TOK>;
-    static_assert(!PR || ((T == T_Q4_0 || T == T_Q8_0 || T == T_Q4_K) && NSTEP % 2 == 0), "paired steps: Q4_0 / Q8_0 / Q4_K, even runs");
+    static_assert(!PR || (T != T_Q6_K && NSTEP % 2 == 0), "paired steps: not Q6_K, even runs");
     constexpr int G = 16 / TOK;   // block groups per MFMA
     constexpr int L = 4 / G;      // k-groups per block group
     constexpr int P = 4 / G;      // MFMA outputs per step
@@ -879,7 +891,7 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
         // one pair (two steps) ahead; a pair's descriptor is its first step's (the second step's
         // blocks follow in the row; past the part its columns are zero)
         constexpr int DP = 2;
-        using WP = MmaPair<T, TOK>;
+        using WP = typename PairOf<T, TOK>::type;
         MmaLanes lp[RT];
 #pragma unroll
         for (int t = 0; t < RT; ++t) lp[t] = WP::lanes(c + 16 * t, g, nb01);
@@ -887,7 +899,7 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
         Xf X[DP][2];
 #pragma unroll
         for (int t = 0; t < RT; ++t)
-            if constexpr (!(MMA_EXP & 2)) F[0][t].load(wrs(step_of(0)), lp[t]);
+            if constexpr (!(MMA_EXP & 2)) F[0][t].load(wrs(step_of(0)), lp[t], nb01);
         stage_x();
         load_x(X[0][0], step_of(0));
         load_x(X[0][1], step_of(1));
@@ -896,12 +908,12 @@ __global__ __launch_bounds__(MMA_KS * WAVE) void mmvq_mma_kernel(const MmArgs a,
             if (j + 1 < NSTEP / 2) {
 #pragma unroll
                 for (int t = 0; t < RT; ++t)
-                    if constexpr (!(MMA_EXP & 2)) F[(k + 1) % DP][t].load(wrs(step_of(2 * j + 2)), lp[t]);
+                    if constexpr (!(MMA_EXP & 2)) F[(k + 1) % DP][t].load(wrs(step_of(2 * j + 2)), lp[t], nb01);
                 load_x(X[(k + 1) % DP][0], step_of(2 * j + 2));
                 load_x(X[(k + 1) % DP][1], step_of(2 * j + 3));
             }
             __builtin_amdgcn_sched_barrier(0);
-            typename PairHalfOf<T, TOK>::type H0[RT], H1[RT];
+            typename PairOf<T, TOK>::half H0[RT], H1[RT];
 #pragma unroll
             for (int t = 0; t < RT; ++t) F[k][t].split(H0[t], H1[t]);
             compute(H0, X[k][0], step_of(2 * j));
@@ -960,7 +972,7 @@ static int mma_part_steps(const MmArgs &a, int kh) {
 
 // Q4_0 / Q8_0 rows contiguous and 4-byte aligned (paired steps load aligned 36 / 68-byte windows)
 static bool mma_pair_aligned(int type, const MmArgs &a) {
-    if (type == T_Q4_K) return true;   // (rows loaded one by one: any row stride)
+    if (type == T_Q4_K || type == T_Q5_K) return true;   // (rows loaded one by one: any row stride)
     if (type != T_Q4_0 && type != T_Q8_0) return false;
     const int64_t row = (int64_t)(a.K / 32) * (type == T_Q4_0 ? 18 : 34);
     return a.nb01 == row && row % 4 == 0 && a.nb02 % 4 == 0 && a.nb03 % 4 == 0 && (reinterpret_cast<uintptr_t>(a.w) & 3) == 0;
@@ -1000,9 +1012,14 @@ static bool mma_part_fits(int type, const MmArgs &a, int part, bool pr, int rt) 
 // profiles/r06_mma_plan_sweep.txt; round 5 chose from eager launches, whose period the host's
 // launch rate bounded):
 //   pr  paired steps: Q4_0 always, Q8_0 below K = 8192 and from 12288 (at 11008 the unpaired
-//       form with two tiles wins), where the rows allow it; Q4_K at 1..4 columns from K = 12288
-//       (28672 x 4096 at 3 columns 20.3 vs 22.3 us, 12288 x 4096 12.7 vs 13.1; even at 8192 and
-//       +6 % at 11008; at 5..8 columns the pairs are 6-10 % slower, profiles/r06_q4k_pairs.txt);
+//       form with two tiles wins), where the rows allow it; the K-quant pairs where rows are
+//       whole 128-B lines apart (K = 11008: 43 super-blocks, rows 48 / 16 B off a line, pairs
+//       4-6 % slower): Q4_K at 1..4 columns from K = 12288 (28672 x 4096 at 3 columns 20.3 vs
+//       22.3 us, 12288 x 4096 12.7 vs 13.1; at 5..8 columns 6-10 % slower,
+//       profiles/r06_q4k_pairs.txt), Q5_K at any column count where the whole K fits one part
+//       (28672 x 4096 at 3..4 columns 23.4-25.2 vs 28.5, 12288 x 4096 14.3-15.0 vs 15.7-15.9,
+//       4096 x 14336 at 5..8 16.7-18.7 vs 18.4-21.0; two parts paired were 1-5 % slower on one
+//       box of two, profiles/r06_q5k_pairs.txt);
 //   kh  one K part wherever the whole column image fits the workgroup's LDS: 0.85-0.95x the
 //       two-part time (no dst zeroing in the pre-pass, no atomic adds, a wave walks twice the
 //       steps); two parts only for images that do not fit (e.g. Q4_0 at 5..8 columns from K =
@@ -1022,9 +1039,11 @@ static MmaPlan mma_plan(int type, const MmArgs &a) {
     const int S = mma_steps(a);
     MmaPlan p;
     const int pe = settings().mma_pair;
+    const bool lines = a.nb01 % 128 == 0;   // (K-quant pairs: rows whole 128-B lines apart)
     const bool want = pe >= 0 ? pe == 1
                               : (type == T_Q4_0 || (type == T_Q8_0 && (a.K < 8192 || a.K >= 12288)) ||
-                                 (type == T_Q4_K && a.M <= 4 && a.K >= 12288));
+                                 (type == T_Q4_K && lines && a.M <= 4 && a.K >= 12288) ||
+                                 (type == T_Q5_K && lines && mma_part_fits(type, a, S, true, 1)));
     p.pr = want && mma_pair_aligned(type, a);
     const bool two_ok = p.pr ? S >= 64 : S >= 32;
     const int ke = settings().mma_kh, re = settings().mma_rt;
@@ -1038,8 +1057,9 @@ static MmaPlan mma_plan(int type, const MmArgs &a) {
     return p;
 }
 
-// the plan keeps the K range in one part (dispatch.cpp use_mma)
+// the plan keeps the K range in one part / takes paired steps (dispatch.cpp use_mma)
 bool mmvq_mma_one_part(int type, const MmArgs &a) { return mma_plan(type, a).kh == 1; }
+bool mmvq_mma_paired(int type, const MmArgs &a) { return mma_plan(type, a).pr; }
 
 bool mmvq_mma_supported(int type, const MmArgs &a) {
     if (!(type == T_Q4_0 || type == T_Q8_0 || type == T_Q4_K || type == T_Q5_K || type == T_Q6_K) || a.M < 1 || a.M > 8) return false;
@@ -1105,7 +1125,8 @@ static hipError_t mma_tok(const MmArgs &a, uint8_t *img, hipStream_t st) {
     } else if (a.x_aligned16) hipLaunchKernelGGL((mma_prequant<TOK, true>), pg, dim3(TOK * 16), 0, st, a, img, kh == 2);
     else hipLaunchKernelGGL((mma_prequant<TOK, false>), pg, dim3(TOK * 16), 0, st, a, img, kh == 2);
     hipError_t e;
-    if constexpr (T == T_Q5_K || T == T_Q6_K) e = mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
+    if constexpr (T == T_Q6_K) e = mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
+    else if constexpr (T == T_Q5_K) e = pl.pr ? mma_run<T, TOK, 1, true>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);
     else if constexpr (T == T_Q8_0) {
         if (pl.pr) e = mma_run<T, TOK, 1, true>(a, img, S, part, kh, st);   // (two tiles of pairs would spill)
         else e = pl.rt == 2 ? mma_run<T, TOK, 2, false>(a, img, S, part, kh, st) : mma_run<T, TOK, 1, false>(a, img, S, part, kh, st);

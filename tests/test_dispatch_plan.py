@@ -73,10 +73,10 @@ PERF = {
     ("q4_K", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
     ("q5_K", 1): "ring nc=1 rpw=2 cols=1",
     ("q5_K", 2): "ring nc=2 rpw=2 cols=2",
-    ("q5_K", 3): "mma tok=4 kh=1 rt=1 run=7 cols=3",
-    ("q5_K", 4): "mma tok=4 kh=1 rt=1 run=7 cols=4",
-    ("q5_K", 5): "mma tok=8 kh=1 rt=1 run=7 cols=5",
-    ("q5_K", 8): "mma tok=8 kh=1 rt=1 run=7 cols=8",
+    ("q5_K", 3): "mma tok=4 kh=1 rt=1 paired run=8 cols=3",
+    ("q5_K", 4): "mma tok=4 kh=1 rt=1 paired run=8 cols=4",
+    ("q5_K", 5): "mma tok=8 kh=1 rt=1 paired run=8 cols=5",
+    ("q5_K", 8): "mma tok=8 kh=1 rt=1 paired run=8 cols=8",
     ("q5_K", 512): "mmq8 tile=128x64 tiles=256 ksplit=1",
     ("q6_K", 1): "ring nc=1 rpw=1 cols=1",
     ("q6_K", 2): "ring nc=2 rpw=1 cols=2",
@@ -104,11 +104,13 @@ MMA_RULE = {
     ("q4_K", 28672, 4096, 8): "ring-pre nc=8 rpw=1 cols=8",                   # no part size fits: VALU
     ("q4_K", 28672, 4096, 3): "mma tok=4 kh=1 rt=1 paired run=14 cols=3",     # 1..4 columns from K = 12288: pairs
     ("q4_K", 11008, 4096, 3): "mma tok=4 kh=1 rt=1 run=6 cols=3",
-    ("q5_K", 4096, 4096, 5): "mma tok=8 kh=2 rt=1 run=1 cols=5",              # Q5_K small: two parts
-    ("q5_K", 8192, 4096, 5): "mma tok=8 kh=1 rt=1 run=4 cols=5",
-    ("q5_K", 14336, 4096, 3): "mma tok=4 kh=1 rt=1 run=7 cols=3",
-    ("q5_K", 14336, 4096, 5): "mma tok=8 kh=1 rt=1 run=7 cols=5",
-    ("q5_K", 28672, 4096, 3): "ring-pre nc=4 rpw=1 cols=3",                   # past K = 16384: VALU to 7
+    ("q5_K", 4096, 4096, 5): "mma tok=8 kh=1 rt=1 paired run=2 cols=5",       # pairs: one part (S < 64)
+    ("q5_K", 8192, 4096, 5): "mma tok=8 kh=1 rt=1 paired run=4 cols=5",
+    ("q5_K", 14336, 4096, 3): "mma tok=4 kh=1 rt=1 paired run=8 cols=3",
+    ("q5_K", 14336, 4096, 5): "mma tok=8 kh=1 rt=1 paired run=8 cols=5",
+    ("q5_K", 28672, 4096, 3): "mma tok=4 kh=1 rt=1 paired run=14 cols=3",     # paired: from 3 at any K
+    ("q5_K", 28672, 4096, 5): "ring-pre nc=8 rpw=1 cols=5",                   # two parts: unpaired, VALU to 7
+    ("q5_K", 11008, 4096, 3): "mma tok=4 kh=1 rt=1 run=6 cols=3",             # rows off 128-B lines: unpaired
     # Q6_K (round 6, profiles/r06_q6k_mma.txt)
     ("q6_K", 4096, 4096, 3): "mmvq nc=3 lpr=64 rpw=1 grid=512x1x1",           # K < 8192: from 5
     ("q6_K", 4096, 4096, 5): "mma tok=8 kh=2 rt=1 run=1 cols=5",              # small: two parts

@@ -190,12 +190,14 @@ def test_mma_paired_steps(mm, t, M_, K):
 @pytest.mark.parametrize("rt", [1, 2])
 @pytest.mark.parametrize("K", [4096, 4352, 14336, 28672])
 @pytest.mark.parametrize("M_", [3, 8])
-def test_mma_q4k_paired_steps(mm, M_, K, rt):
-    """Q4_K paired steps (GGML_MI355X_MMA_PAIR=1): both halves of a super-block per wave, the qs
-    bytes of 16 rows loaded 8 rows x 128 B per instruction and handed to the MFMA lanes by
-    ds_bpermute; K = 4352 has an odd super-block count; ragged rows (N = 200); one and two row
-    tiles; run twice for bitwise repeatability"""
-    a, b, out_ne = operands(qref.Q4_K, 200, M_, K, 19)
+@pytest.mark.parametrize("t", [qref.Q4_K, qref.Q5_K], ids=lambda t: qref.NAMES[t])
+def test_mma_kquant_paired_steps(mm, t, M_, K, rt):
+    """Q4_K / Q5_K paired steps (GGML_MI355X_MMA_PAIR=1): both halves of a super-block per wave,
+    the qs bytes of 16 rows loaded 8 rows x 128 B per instruction and handed to the MFMA lanes by
+    ds_bpermute, header (and Q5_K's qh piece) once per super-block; K = 4352 has an odd
+    super-block count; ragged rows (N = 200); one and two row tiles (Q5_K: one); run twice for
+    bitwise repeatability"""
+    a, b, out_ne = operands(t, 200, M_, K, 19)
     env = {"GGML_MI355X_MMA": 1, "GGML_MI355X_MMA_PAIR": 1, "GGML_MI355X_MMA_RT": rt}
     g1 = run_with(mm, a, b, out_ne, env)
     g2 = run_with(mm, a, b, out_ne, env)
