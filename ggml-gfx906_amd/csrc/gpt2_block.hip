@@ -348,6 +348,14 @@ __device__ __forceinline__ void ln_quantize(const BlockArgs &a, float4 (&xa)[1][
 
 __device__ __forceinline__ void load_ln(const float *gp, const float *bp, int E, float4 (&g)[1][2], float4 (&bb)[1][2]) {
     const int k0 = min((int)(threadIdx.x >> 2) * 32 + (int)(threadIdx.x & 3) * 8, E - 8);
+    // only the waves holding a thread t < E / 8 (the threads whose block kb0 = t / 4 exists)
+    // load: the prologue's issue phase is paced by the CU's vector-memory instruction rate, so a
+    // wave-instruction of clamped duplicates costs about what a useful one does (2 of 8 waves at
+    // n_embd 768: attention block 9.07 -> 8.69 us, engine +1.7 %, profiles/r06_gpt2_prologue_ab.txt).
+    // Skipping the duplicate residual slots, bias loads or q/k/v rows the same way measured slower
+    // (branches between the residual and weight issues), and is not done.
+    g[0][0] = g[0][1] = bb[0][0] = bb[0][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (__builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) * WAVE >= E / 8) return;
     g[0][0] = reinterpret_cast<const float4 *>(gp + k0)[0];
     g[0][1] = reinterpret_cast<const float4 *>(gp + k0)[1];
     bb[0][0] = reinterpret_cast<const float4 *>(bp + k0)[0];
@@ -442,13 +450,22 @@ __global__ __launch_bounds__(BT) void attn_block_kernel(const BlockArgs a) {
     const float4 q4 = reinterpret_cast<const float4 *>(qkv_s)[d4];
     float m = -INFINITY, l = 0.f;
     float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    // a wave issues only the key slots u that hold a key of one of its four groups (the wave's
+    // first group is the lowest; no other load is in flight here, so the branch costs no wait):
+    // at short contexts most of a round's AU slots lie past nk. Skipped slots read zeros (their
+    // scores are -inf and their weights 0, so the values must be finite). Measured neutral
+    // (profiles/r06_gpt2_prologue_ab.txt), kept with the layer-norm trim it was measured beside.
+    const int wg0 = __builtin_amdgcn_readfirstlane(wave) * 4;
     for (int jb = 0; jb < nk; jb += AGROUPS * AU) {
         float4 kk[AU], vv[AU];
 #pragma unroll
         for (int u = 0; u < AU; ++u) {
             const int jc = min(jb + u * AGROUPS + grp, nk - 1);
-            kk[u] = reinterpret_cast<const float4 *>(K + (int64_t)jc * E)[d4];
-            vv[u] = reinterpret_cast<const float4 *>(Vc + (int64_t)jc * E)[d4];
+            kk[u] = vv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (jb + u * AGROUPS + wg0 < nk) {
+                kk[u] = reinterpret_cast<const float4 *>(K + (int64_t)jc * E)[d4];
+                vv[u] = reinterpret_cast<const float4 *>(Vc + (int64_t)jc * E)[d4];
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
         float sc[AU];
