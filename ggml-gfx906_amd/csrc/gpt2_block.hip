@@ -30,6 +30,7 @@
 // contiguous. Measured choices: 128-unit slices beat 256 (4207 vs 3850
 // tokens/s, GPT-2 117M Q4_0), LDS-only barriers keep weight streams in flight.
 #include <algorithm>
+#include <type_traits>
 
 #include "mmvq_impl.h"
 
@@ -572,7 +573,11 @@ __global__ __launch_bounds__(BT) void mlp_block_kernel(const BlockArgs a) {
     float4 g[1][2], bb[1][2];
     load_ln(a.ln_g, a.ln_b, E, g, bb);
     const float fb = a.b_fc[j * MLP_SLICE + min(tid, MLP_SLICE - 1)];
-    RowsDot<T, 16, MLP_SLICE / 32, FNIT> fd;
+    // fc rows: n_embd 768 (FNIT 3): 4 lanes per row, 3 slots each, one row per lane (every lane
+    // and every wave live: 8 waves x 16 rows = the slice's 128); otherwise (FNIT 1): 16 lanes per
+    // row, one slot each, four rows per lane
+    using FD = std::conditional_t<FNIT == 1, RowsDot<T, 16, MLP_SLICE / 32, 1>, RowsDot<T, 4, MLP_SLICE / 128, FNIT>>;
+    FD fd;
     fd.load([&](int r) { return a.w_fc + (int64_t)(j * MLP_SLICE + r) * a.nb_fc; }, MLP_SLICE, 0, 0, E / 64);
     __builtin_amdgcn_sched_barrier(0);
     stamp(a, 1, 8);
@@ -586,7 +591,7 @@ __global__ __launch_bounds__(BT) void mlp_block_kernel(const BlockArgs a) {
     stamp(a, 1, 2);
 
     if (a.stamps != nullptr) {   // diagnostics: this wave's fc weights have landed
-        uint32_t probe = reinterpret_cast<const uint32_t *>(&fd.f[0][MLP_SLICE / 32 - 1])[0];
+        uint32_t probe = reinterpret_cast<const uint32_t *>(&fd.f[0][FNIT == 1 ? MLP_SLICE / 32 - 1 : 0])[0];
         asm volatile("" : "+v"(probe));
         if (probe == 0x12345u && threadIdx.x == 999) stamp(a, 1, 10);
         stamp(a, 1, 9);
@@ -651,7 +656,15 @@ hipError_t launch_pair(bool attn, const BlockArgs &a, hipStream_t st) {
         if constexpr (REPACK<T>) hipLaunchKernelGGL((attn_block_kernel<T, 1, 3, true>), dim3(a.n_head, a.n_seq), dim3(BT), 0, st, a);
         else return hipErrorInvalidValue;
     } else if (attn) hipLaunchKernelGGL((attn_block_kernel<T, 1, RR>), dim3(a.n_head, a.n_seq), dim3(BT), 0, st, a);
-    else hipLaunchKernelGGL((mlp_block_kernel<T, 1, RR>), dim3(4 * a.E / MLP_SLICE, a.n_seq), dim3(BT), 0, st, a);
+    else {
+        if constexpr (REPACK<T>) {
+            if (a.E == 768) {
+                hipLaunchKernelGGL((mlp_block_kernel<T, 3, RR>), dim3(4 * a.E / MLP_SLICE, a.n_seq), dim3(BT), 0, st, a);
+                return hipGetLastError();
+            }
+        }
+        hipLaunchKernelGGL((mlp_block_kernel<T, 1, RR>), dim3(4 * a.E / MLP_SLICE, a.n_seq), dim3(BT), 0, st, a);
+    }
     return hipGetLastError();
 }
 
